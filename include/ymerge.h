@@ -1,0 +1,108 @@
+/*
+ * ymerge.h — C ABI of the MI355X batched Yjs update-compaction engine.
+ *
+ * Drop-in boundary for yrs' binary-update algebra (lib0 v1):
+ *   ymerge_updates_v1                  replaces yrs::merge_updates_v1                 yrs/src/alt.rs:15-28
+ *   ydiff_updates_v1                   replaces yrs::diff_updates_v1                  yrs/src/alt.rs:73-81
+ *   yencode_state_vector_from_update_v1 replaces yrs::encode_state_vector_from_update_v1 yrs/src/alt.rs:54-57
+ *   ybinary_destroy                    same contract as yffi's ybinary_destroy       yffi/src/lib.rs:384-388
+ * yffi in this snapshot exports no merge/diff-of-updates function;
+ * the signatures follow yffi conventions: `const char *` + `uint32_t` length
+ * inputs, a library-owned `char *` result with its length in `*out_len`, NULL on
+ * a decode failure (yffi/src/lib.rs:802-829), error codes as yffi's
+ * (yffi/src/lib.rs:1137-1174): 2 VAR_INT, 3 EOS, 4 UNEXPECTED_VALUE, 5 INVALID_JSON,
+ * 6 OTHER, 7 NOT_ENOUGH_MEMORY, plus 20 REFERENCE_PANIC (yrs itself would panic)
+ * and 21 UNSUPPORTED (content class not restated on the device yet).
+ *
+ * Batched entry points take one contiguous byte arena for many documents:
+ * doc d owns updates [doc_upd[d], doc_upd[d+1]), update u owns bytes
+ * [upd_off[u], upd_off[u+1]).  Each document's output equals the single-document
+ * function on that document's updates.
+ *
+ * Thread safety: every function is safe to call concurrently; a ymerge_ctx
+ * serialises the batches submitted to it on its own HIP stream.
+ */
+#ifndef YMERGE_H
+#define YMERGE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define YMERGE_OK 0
+#define YMERGE_ERR_VAR_INT 2
+#define YMERGE_ERR_EOS 3
+#define YMERGE_ERR_UNEXPECTED_VALUE 4
+#define YMERGE_ERR_INVALID_JSON 5
+#define YMERGE_ERR_OTHER 6
+#define YMERGE_ERR_NOT_ENOUGH_MEMORY 7
+#define YMERGE_ERR_REFERENCE_PANIC 20
+#define YMERGE_ERR_UNSUPPORTED 21
+#define YMERGE_ERR_DEVICE 30 /* no usable MI355X / HIP failure */
+
+/* ---------------------------------------------------------------- single document (yffi style) */
+char *ymerge_updates_v1(const char *const *updates, const uint32_t *updates_len, uint32_t updates_count,
+                        uint32_t *out_len);
+char *ydiff_updates_v1(const char *update, uint32_t update_len, const char *state_vector, uint32_t sv_len,
+                       uint32_t *out_len);
+char *yencode_state_vector_from_update_v1(const char *update, uint32_t update_len, uint32_t *out_len);
+void ybinary_destroy(char *ptr, uint32_t len);
+/* error code of the last failed call on this thread (0 after a success) */
+uint8_t ymerge_last_error(void);
+
+/* ---------------------------------------------------------------- batched, device-resident */
+typedef struct ymerge_ctx ymerge_ctx;
+ymerge_ctx *ymerge_ctx_create(int device);
+void ymerge_ctx_destroy(ymerge_ctx *ctx);
+
+/* Per-batch statistics (device event timings of the last batch, ms). */
+typedef struct {
+  uint64_t n_docs, bytes_in, bytes_out;
+  uint64_t docs_fast, docs_exact, docs_error;
+  float ms_total, ms_plan, ms_write, ms_count;
+} ymerge_stats;
+
+/* Device-resident result, owned by the context, valid until the next batch. */
+typedef struct {
+  uint8_t *d_out;      /* output arena */
+  uint64_t *d_out_off; /* n_docs + 1 offsets (documents with status != 0 are empty) */
+  uint8_t *d_status;   /* n_docs status codes */
+  uint64_t out_bytes;  /* arena size */
+} ymerge_device_result;
+
+/* merge_updates_v1 over a batch whose arena/offsets already live in HBM of the
+ * context's device.  Returns 0 or YMERGE_ERR_DEVICE. */
+int ymerge_updates_v1_batch_device(ymerge_ctx *ctx, const uint8_t *d_bytes, const uint64_t *d_upd_off,
+                                   const uint64_t *d_doc_upd, uint64_t n_docs, ymerge_device_result *res);
+/* encode_state_vector_from_update_v1 / diff_updates_v1: one update per document
+ * (d_upd_off has n_docs + 1 entries); diff also takes one encoded state vector
+ * per document. */
+int yencode_state_vector_from_update_v1_batch_device(ymerge_ctx *ctx, const uint8_t *d_bytes,
+                                                     const uint64_t *d_upd_off, uint64_t n_docs,
+                                                     ymerge_device_result *res);
+int ydiff_updates_v1_batch_device(ymerge_ctx *ctx, const uint8_t *d_bytes, const uint64_t *d_upd_off,
+                                  const uint8_t *d_sv_bytes, const uint64_t *d_sv_off, uint64_t n_docs,
+                                  ymerge_device_result *res);
+/* copy the last device result to host buffers (out: out_bytes, out_off: n_docs+1, status: n_docs) */
+int ymerge_result_to_host(ymerge_ctx *ctx, const ymerge_device_result *res, uint64_t n_docs, uint8_t *out,
+                          uint64_t *out_off, uint8_t *status);
+void ymerge_last_stats(ymerge_ctx *ctx, ymerge_stats *stats);
+
+/* ---------------------------------------------------------------- batched, host memory */
+typedef struct {
+  uint8_t *out;      /* library-owned arena */
+  uint64_t *out_off; /* n_docs + 1 */
+  uint8_t *status;   /* n_docs */
+  uint64_t n_docs, out_bytes;
+} ymerge_batch_result;
+int ymerge_updates_v1_batch(ymerge_ctx *ctx, const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_updates,
+                            const uint64_t *doc_upd, uint64_t n_docs, ymerge_batch_result **res);
+void ymerge_batch_result_destroy(ymerge_batch_result *res);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

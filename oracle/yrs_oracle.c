@@ -422,13 +422,15 @@ static void upd_free(upd_t *u) {
 }
 
 /* ------------------------------------------------------------------ Any (any.rs:37-83) */
-static int any_skip(upd_t *u, rd_t *r, int depth) {
-  if (depth > 1024) return YO_ERR_REFERENCE_PANIC;
+/* Validates one Any value.  Policy shared with the device: a container nested
+ * 64 deep -> UNSUPPORTED; duplicate keys in an ItemContent::Any map -> UNSUPPORTED
+ * (yrs collapses them into a RandomState HashMap whose order is random anyway). */
+static int any_skip2(rd_t *r, int depth, bool check_dups) {
   uint8_t tag;
   TRY(rd_u8(r, &tag));
-  const uint8_t *s = NULL;
+  const uint8_t *s;
   uint32_t n32;
-  uint64_t n = 0;
+  uint64_t n;
   int64_t i64;
   switch (tag) {
   case 127: case 126: case 121: case 120: return 0;
@@ -436,22 +438,37 @@ static int any_skip(upd_t *u, rd_t *r, int depth) {
   case 124: return rd_exact(r, 4, &s);
   case 123: case 122: return rd_exact(r, 8, &s);
   case 119: case 116: return rd_buf(r, &s, &n32);
-  case 118: /* HashMap::with_capacity(len): (String, Any) = 48 bytes */
+  case 118: { /* HashMap::with_capacity(len): (String, Any) = 48 bytes */
     TRY(rd_var_u64(r, &n));
     if (n && (n > (1ull << 40) || cap_to_buckets((size_t)n) * 49ull > ALLOC_LIMIT)) return YO_ERR_REFERENCE_PANIC;
+    if (depth >= 64) return YO_ERR_UNSUPPORTED;
+    size_t map_start = r->i;
     for (uint64_t i = 0; i < n; i++) {
       TRY(rd_buf(r, &s, &n32));
-      TRY(any_skip(u, r, depth + 1));
+      if (check_dups) {
+        rd_t q = {r->p, r->n, map_start};
+        for (uint64_t j = 0; j < i; j++) {
+          const uint8_t *ks;
+          uint32_t kn;
+          rd_buf(&q, &ks, &kn);
+          if (kn == n32 && !memcmp(ks, s, kn)) return YO_ERR_UNSUPPORTED;
+          any_skip2(&q, depth + 1, false);
+        }
+      }
+      TRY(any_skip2(r, depth + 1, check_dups));
     }
     return 0;
+  }
   case 117: /* Vec::with_capacity(len): Any = 24 bytes */
     TRY(rd_var_u64(r, &n));
     if (n > ALLOC_LIMIT / 24) return YO_ERR_REFERENCE_PANIC;
-    for (uint64_t i = 0; i < n; i++) TRY(any_skip(u, r, depth + 1));
+    if (depth >= 64) return YO_ERR_UNSUPPORTED;
+    for (uint64_t i = 0; i < n; i++) TRY(any_skip2(r, depth + 1, check_dups));
     return 0;
   default: return YO_ERR_UNEXPECTED_VALUE;
   }
 }
+static int any_skip(upd_t *u, rd_t *r, int depth) { return any_skip2(r, depth, false); }
 
 /* Any::encode number rules (any.rs:136-154) */
 static void num_encode(wb_t *w, double x) {
@@ -655,7 +672,7 @@ static int content_decode(upd_t *u, rd_t *r, uint8_t ref, blk_t *b) {
       span_t s;
       s.p = r->p + r->i;
       size_t st = r->i;
-      TRY(any_skip(u, r, 0));
+      TRY(any_skip2(r, 0, true));
       s.n = (uint32_t)(r->i - st);
       VPUSH(u->elems, s);
     }
@@ -747,6 +764,7 @@ static int idr_decode(rd_t *r, idr_t *out) {
     uint32_t c, l;
     TRY(rd_var_u32(r, &c));
     TRY(rd_var_u32(r, &l));
+    if ((uint64_t)c + l > UINT32_MAX) return YO_ERR_REFERENCE_PANIC;
     out->cont = 1;
     out->c.s = c;
     out->c.e = c + l;
@@ -757,6 +775,7 @@ static int idr_decode(rd_t *r, idr_t *out) {
     uint32_t c, l;
     TRY(rd_var_u32(r, &c));
     TRY(rd_var_u32(r, &l));
+    if ((uint64_t)c + l > UINT32_MAX) return YO_ERR_REFERENCE_PANIC;
     rng_t g = {c, c + l};
     VPUSH(out->v, g);
   }
@@ -790,6 +809,7 @@ static int decode_update(upd_t *u, const uint8_t *p, size_t n) {
       bool has;
       TRY(decode_block(u, &r, c32, clock, &b, &has));
       if (has) {
+        if ((uint64_t)clock + b.len > UINT32_MAX) return YO_ERR_REFERENCE_PANIC;
         clock += b.len;
         if (b.unsupported) u->unsupported = 1;
         VPUSH(u->blocks, b);

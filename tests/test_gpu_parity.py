@@ -1,0 +1,124 @@
+"""GPU parity: the HIP engine (through the C ABI) against the CPU oracle, byte for
+byte, on the reference KATs, the Yjs-generated fixtures, synthetic batches of
+every BASELINE config, error/fuzz cases and the full automerge-paper trace."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import workloads
+from conftest import ROOT
+from test_oracle_kats import ALT_DIFF, ALT_MERGE_1, ALT_MERGE_2, ALT_SV, COMPAT
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def engine():
+    import ymerge
+    e = ymerge.Engine(0)
+    yield e
+    e.close()
+
+
+def run_batch(engine, batch):
+    return engine.merge_host(batch.data, batch.upd_off, batch.doc_upd)
+
+
+def check_batch(engine, oracle, batch, mode=1):
+    out, off, st = run_batch(engine, batch)
+    exp, eoff, est = oracle.merge_batch(batch.data, batch.upd_off, batch.doc_upd, mode=mode, threads=8)
+    bad = np.nonzero(st != est)[0]
+    assert len(bad) == 0, f"status mismatch at docs {bad[:10]}: gpu {st[bad[:10]]} oracle {est[bad[:10]]}"
+    for d in range(batch.n_docs):
+        g = out[int(off[d]):int(off[d + 1])].tobytes()
+        e = exp[int(eoff[d]):int(eoff[d + 1])]
+        if g != e:
+            k = next((i for i in range(min(len(g), len(e))) if g[i] != e[i]), min(len(g), len(e)))
+            pytest.fail(f"doc {d}: first byte diff at {k} (gpu len {len(g)}, oracle len {len(e)})\n"
+                        f"gpu    {g[max(0, k - 16):k + 16].hex()}\noracle {e[max(0, k - 16):k + 16].hex()}")
+    return out, off, st
+
+
+def batch_of(docs):
+    parts, offs, dus, tot = [], [0], [0], 0
+    for ups in docs:
+        for u in ups:
+            parts.append(np.frombuffer(bytes(u) or b"", dtype=np.uint8))
+            tot += len(u)
+            offs.append(tot)
+        dus.append(len(offs) - 1)
+    data = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+    return workloads.Batch(data, np.array(offs, np.uint64), np.array(dus, np.uint64))
+
+
+def test_alt_kats_single_doc_abi():
+    import ymerge
+    for a, b, exp in (ALT_MERGE_1, ALT_MERGE_2):
+        assert list(ymerge.merge_updates_v1([bytes(a), bytes(b)])) == exp
+    for u in COMPAT.values():
+        assert ymerge.merge_updates_v1([bytes(u)]) == bytes(u)
+    with pytest.raises(ymerge.YrsError) as ei:
+        ymerge.merge_updates_v1([b""])
+    assert ei.value.code == 3
+
+
+def test_yjs_fixture_batch(engine, oracle):
+    with open(os.path.join(ROOT, "tests", "golden", "yjs_fixtures.json")) as f:
+        cases = json.load(f)["cases"]
+    docs = [[bytes.fromhex(h) for h in c["updates"]] for c in cases]
+    check_batch(engine, oracle, batch_of(docs))
+
+
+def test_edge_docs(engine, oracle):
+    docs = [[], [b""], [bytes([0, 0])], [bytes([0x80] * 12)], [bytes([1, 1, 5, 0, 0x0C, 1, 0])],
+            [bytes(ALT_MERGE_1[0]), b"\x01"], [bytes(ALT_MERGE_1[0])] * 5,
+            [bytes(ALT_MERGE_2[0]), bytes(ALT_MERGE_2[1])], [bytes(ALT_MERGE_2[1]), bytes(ALT_MERGE_2[0])]]
+    check_batch(engine, oracle, batch_of(docs))
+
+
+def test_fuzz_corruptions(engine, oracle):
+    with open(os.path.join(ROOT, "tests", "golden", "yjs_fixtures.json")) as f:
+        cases = json.load(f)["cases"]
+    rng = np.random.default_rng(1234)
+    docs = []
+    for c in cases:
+        ups = [bytearray.fromhex(h) for h in c["updates"]][:40]
+        for _ in range(6):
+            mut = [bytearray(u) for u in ups]
+            for _ in range(rng.integers(1, 4)):
+                u = mut[rng.integers(len(mut))]
+                if len(u) == 0:
+                    continue
+                op = rng.integers(3)
+                i = rng.integers(len(u))
+                if op == 0:
+                    u[i] = rng.integers(256)
+                elif op == 1:
+                    del u[i:]
+                else:
+                    u.insert(i, rng.integers(256))
+            docs.append([bytes(u) for u in mut])
+    check_batch(engine, oracle, batch_of(docs))
+
+
+def test_c2_batch(engine, oracle):
+    check_batch(engine, oracle, workloads.text_docs(300, 1000))
+
+
+def test_c2_many_clients(engine, oracle):
+    check_batch(engine, oracle, workloads.text_docs(200, 400, seed=77, min_clients=5, max_clients=12))
+
+
+def test_c3_zipf_batch(engine, oracle):
+    check_batch(engine, oracle, workloads.zipf_docs(2000, seed=0x5EED))
+
+
+def test_c4_delete_heavy(engine, oracle):
+    check_batch(engine, oracle, workloads.delete_heavy_docs(24, ops_per_doc=2000), mode=1)
+
+
+def test_c1_automerge_trace(engine, oracle):
+    b, _ = workloads.trace_updates()
+    check_batch(engine, oracle, b, mode=1)

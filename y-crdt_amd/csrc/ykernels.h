@@ -1,0 +1,24 @@
+// ykernels.h — launch interface between the host engine (ymerge_host.cpp) and the
+// gfx950 kernels.  Plain device pointers only.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ym {
+// A batch of documents in HBM: doc d owns updates [doc_upd[d], doc_upd[d+1]);
+// update u owns bytes [upd_off[u], upd_off[u+1]) of `bytes`.
+struct BatchIn {
+  const uint8_t *bytes;
+  const uint64_t *upd_off;
+  const uint64_t *doc_upd;
+  uint32_t n_docs;
+};
+
+void launch_seq_count(const BatchIn &b, uint8_t *status, uint32_t *counts, uint64_t *need, hipStream_t s);
+void launch_seq_merge(bool write, const BatchIn &b, const uint8_t *status, const uint32_t *counts,
+                      const uint64_t *scr_off, uint32_t *scratch, uint64_t *sizes, const uint64_t *out_off,
+                      uint8_t *out, uint8_t *status_out, hipStream_t s);
+// exclusive scan: out[0..n] (out[n] = total); tmp needs >= (n/2048 + 2) u64
+void launch_scan_u64(const uint64_t *in, uint64_t *out, uint32_t n, uint64_t *tmp, hipStream_t s);
+size_t scan_tmp_elems(uint32_t n);
+} // namespace ym

@@ -1,0 +1,85 @@
+// yscan.hip — exclusive prefix sum over u64 (per-document sizes -> arena offsets).
+// Three launches: per-tile totals, one-workgroup scan of the tile totals, per-tile
+// rescan + add.  Tiles are 256 lanes x 8 elements, loads coalesced per lane group.
+#include "ykernels.h"
+
+namespace ym {
+constexpr uint32_t SCAN_NT = 256, SCAN_IT = 8, SCAN_TILE = SCAN_NT * SCAN_IT;
+
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t *sh, uint64_t &total) {
+  uint32_t t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  uint64_t x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    uint64_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) sh[wid] = x;
+  __syncthreads();
+  if (t == 0) {
+    uint64_t acc = 0;
+    for (uint32_t w = 0; w < SCAN_NT / 64; w++) {
+      uint64_t s = sh[w];
+      sh[w] = acc;
+      acc += s;
+    }
+    sh[SCAN_NT / 64] = acc;
+  }
+  __syncthreads();
+  total = sh[SCAN_NT / 64];
+  uint64_t r = sh[wid] + x - v;
+  __syncthreads();
+  return r;
+}
+
+__global__ void __launch_bounds__(256) k_scan_tiles(const uint64_t *in, uint32_t n, uint64_t *tile_sum) {
+  __shared__ uint64_t sh[SCAN_NT / 64 + 1];
+  uint32_t base = blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_IT;
+  uint64_t s = 0;
+  for (uint32_t i = 0; i < SCAN_IT; i++)
+    if (base + i < n) s += in[base + i];
+  uint64_t tot;
+  block_excl_scan(s, sh, tot);
+  if (threadIdx.x == 0) tile_sum[blockIdx.x] = tot;
+}
+__global__ void __launch_bounds__(256) k_scan_top(uint64_t *tile_sum, uint32_t ntiles) {
+  __shared__ uint64_t sh[SCAN_NT / 64 + 1];
+  uint64_t carry = 0;
+  for (uint32_t b0 = 0; b0 < ntiles; b0 += SCAN_NT) {
+    uint32_t i = b0 + threadIdx.x;
+    uint64_t v = i < ntiles ? tile_sum[i] : 0, tot;
+    uint64_t e = block_excl_scan(v, sh, tot);
+    if (i < ntiles) tile_sum[i] = carry + e;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) tile_sum[ntiles] = carry;
+}
+__global__ void __launch_bounds__(256) k_scan_final(const uint64_t *in, uint32_t n, const uint64_t *tile_off,
+                                                   uint64_t *out) {
+  __shared__ uint64_t sh[SCAN_NT / 64 + 1];
+  uint32_t base = blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_IT;
+  uint64_t v[SCAN_IT], s = 0;
+  for (uint32_t i = 0; i < SCAN_IT; i++) {
+    v[i] = base + i < n ? in[base + i] : 0;
+    s += v[i];
+  }
+  uint64_t tot;
+  uint64_t e = block_excl_scan(s, sh, tot) + tile_off[blockIdx.x];
+  for (uint32_t i = 0; i < SCAN_IT; i++) {
+    if (base + i < n) out[base + i] = e;
+    e += v[i];
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = tile_off[gridDim.x];
+}
+
+size_t scan_tmp_elems(uint32_t n) { return n / SCAN_TILE + 2; }
+void launch_scan_u64(const uint64_t *in, uint64_t *out, uint32_t n, uint64_t *tmp, hipStream_t s) {
+  uint32_t ntiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+  if (ntiles == 0) {
+    hipMemsetAsync(out, 0, sizeof(uint64_t), s);
+    return;
+  }
+  hipLaunchKernelGGL(k_scan_tiles, dim3(ntiles), dim3(SCAN_NT), 0, s, in, n, tmp);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_NT), 0, s, tmp, ntiles);
+  hipLaunchKernelGGL(k_scan_final, dim3(ntiles), dim3(SCAN_NT), 0, s, in, n, tmp, out);
+}
+} // namespace ym

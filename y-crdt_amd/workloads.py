@@ -1,0 +1,169 @@
+"""Synthetic Yjs v1 update logs for the BASELINE.json configs (wraps csrc/workload.c).
+
+C1  automerge-paper trace replay, one doc (tests/golden/automerge-paper.json.gz)
+C2  n docs x k ops, 1-4 clients, 80/20 insert/delete, synced replicas (seed 0xC0FFEE)
+C3  Zipf(1.5) op counts on [1, 1e4] (seed 0x5EED)
+C4  delete-heavy docs: GC'd snapshot + per-op log, 10% withheld, 5% duplicated (seed 0xDE1E7E)
+"""
+import ctypes
+import gzip
+import json
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "lib", "libywork.so")
+_lib = None
+
+
+def _L():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB):
+            raise RuntimeError(f"workload generator not built: {_LIB}")
+        L = ctypes.CDLL(_LIB)
+        P = ctypes.POINTER
+        L.yw_generate.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_uint32,
+                                  ctypes.c_uint32, ctypes.c_double, ctypes.c_int, P(ctypes.c_void_p),
+                                  P(ctypes.c_uint64), P(ctypes.c_void_p), P(ctypes.c_uint64), P(ctypes.c_void_p)]
+        L.yw_replay.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                ctypes.c_uint32, P(ctypes.c_void_p), P(ctypes.c_uint64), P(ctypes.c_void_p)]
+        L.yw_generate_ids.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_double, ctypes.c_int,
+                                      P(ctypes.c_void_p), P(ctypes.c_uint64), P(ctypes.c_void_p), P(ctypes.c_uint64),
+                                      P(ctypes.c_void_p)]
+        L.yw_doc_hash.restype = ctypes.c_uint64
+        L.yw_doc_hash.argtypes = [ctypes.c_uint64]
+        L.yw_free.argtypes = [ctypes.c_void_p]
+        _lib = L
+    return _lib
+
+
+class Batch:
+    """Arena of documents: doc d -> updates [doc_upd[d], doc_upd[d+1]) -> bytes [upd_off[u], upd_off[u+1])."""
+
+    def __init__(self, data, upd_off, doc_upd, name=""):
+        self.data, self.upd_off, self.doc_upd, self.name = data, upd_off, doc_upd, name
+
+    @property
+    def n_docs(self):
+        return len(self.doc_upd) - 1
+
+    @property
+    def n_updates(self):
+        return len(self.upd_off) - 1
+
+    @property
+    def n_bytes(self):
+        return int(self.upd_off[-1])
+
+    def doc_updates(self, d):
+        u0, u1 = int(self.doc_upd[d]), int(self.doc_upd[d + 1])
+        return [self.data[int(self.upd_off[u]):int(self.upd_off[u + 1])].tobytes() for u in range(u0, u1)]
+
+    def subset(self, docs):
+        docs = list(docs)
+        parts, offs, dus = [], [0], [0]
+        tot = 0
+        for d in docs:
+            for u in self.doc_updates(d):
+                parts.append(np.frombuffer(u, dtype=np.uint8))
+                tot += len(u)
+                offs.append(tot)
+            dus.append(len(offs) - 1)
+        data = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+        return Batch(data, np.array(offs, np.uint64), np.array(dus, np.uint64), self.name + "[subset]")
+
+
+def doc_hash(doc_id):
+    return int(_L().yw_doc_hash(int(doc_id)))
+
+
+def shard_ids(n_total, rank, world):
+    """Global doc ids owned by `rank` under doc-hash sharding: splitmix64(id) % world == rank."""
+    if world == 1:
+        return np.arange(n_total, dtype=np.uint64)
+    return np.array([i for i in range(n_total) if doc_hash(i) % world == rank], dtype=np.uint64)
+
+
+def _generate(kind, seed, n_ops, min_clients, max_clients, del_frac, threads, ids=None):
+    n_ops = np.ascontiguousarray(n_ops, dtype=np.uint32)
+    b, nb, uo, nu, du = (ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_void_p(), ctypes.c_uint64(),
+                         ctypes.c_void_p())
+    idp = None
+    if ids is not None:
+        ids = np.ascontiguousarray(ids, dtype=np.uint64)
+        assert len(ids) == len(n_ops)
+        idp = ids.ctypes.data
+    _L().yw_generate_ids(kind, seed, len(n_ops), idp, n_ops.ctypes.data, min_clients, max_clients, del_frac,
+                         threads, ctypes.byref(b), ctypes.byref(nb), ctypes.byref(uo), ctypes.byref(nu),
+                         ctypes.byref(du))
+    data = np.frombuffer(ctypes.string_at(b, nb.value), dtype=np.uint8).copy() if nb.value else np.zeros(0, np.uint8)
+    upd_off = np.ctypeslib.as_array(ctypes.cast(uo, ctypes.POINTER(ctypes.c_uint64)), (nu.value + 1,)).copy()
+    doc_upd = np.ctypeslib.as_array(ctypes.cast(du, ctypes.POINTER(ctypes.c_uint64)), (len(n_ops) + 1,)).copy()
+    for p in (b, uo, du):
+        _L().yw_free(p)
+    return data, upd_off, doc_upd
+
+
+def text_docs(n_docs, ops_per_doc, seed=0xC0FFEE, min_clients=1, max_clients=4, del_frac=0.2, threads=None,
+              ids=None):
+    """C2: n_docs synced YText docs, `ops_per_doc` single-op updates each (ids: global doc ids)."""
+    threads = threads or min(16, os.cpu_count() or 1)
+    if ids is not None:
+        n_docs = len(ids)
+    n_ops = np.full(n_docs, ops_per_doc, np.uint32) if np.isscalar(ops_per_doc) else ops_per_doc
+    return Batch(*_generate(2, seed, n_ops, min_clients, max_clients, del_frac, threads, ids), name="C2")
+
+
+def zipf_counts(n_docs, alpha=1.5, kmax=10_000, seed=0x5EED):
+    rng = np.random.default_rng(seed)
+    k = np.arange(1, kmax + 1, dtype=np.float64)
+    p = k ** (-alpha)
+    cdf = np.cumsum(p / p.sum())
+    return (np.searchsorted(cdf, rng.random(n_docs)) + 1).astype(np.uint32)
+
+
+def zipf_docs(n_docs, seed=0x5EED, threads=None, ids=None):
+    """C3: Zipf(1.5)-skewed update counts on [1, 1e4] (ids: global doc ids of this shard)."""
+    threads = threads or min(16, os.cpu_count() or 1)
+    counts = zipf_counts(n_docs, seed=seed)
+    if ids is not None:
+        counts = counts[np.asarray(ids, dtype=np.int64)]
+    return Batch(*_generate(2, seed, counts, 1, 4, 0.2, threads, ids), name="C3")
+
+
+def delete_heavy_docs(n_docs, ops_per_doc=5000, seed=0xDE1E7E, threads=None):
+    """C4: 70% deletes, GC'd snapshot + log with withheld / duplicated updates."""
+    threads = threads or min(16, os.cpu_count() or 1)
+    n_ops = np.full(n_docs, ops_per_doc, np.uint32)
+    return Batch(*_generate(4, seed, n_ops, 1, 4, 0.7, threads), name="C4")
+
+
+def trace_updates(path=None, client=1):
+    """C1: one update per transaction of an editing trace (default automerge-paper)."""
+    if path is None:
+        path = os.path.join(os.path.dirname(_HERE), "tests", "golden", "automerge-paper.json.gz")
+    with gzip.open(path) as f:
+        d = json.load(f)
+    pos, dele, ilen, ins = [], [], [], []
+    for t in d["txns"]:
+        for p in t["patches"]:
+            s = p[2].encode("utf-8")
+            pos.append(p[0])
+            dele.append(p[1])
+            ilen.append(len(s))
+            ins.append(s)
+    pos = np.array(pos, np.uint32)
+    dele = np.array(dele, np.uint32)
+    ilen = np.array(ilen, np.uint32)
+    insb = np.frombuffer(b"".join(ins) or b"\0", dtype=np.uint8)
+    b, nb, uo = ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_void_p()
+    _L().yw_replay(pos.ctypes.data, dele.ctypes.data, ilen.ctypes.data, insb.ctypes.data, len(pos), client,
+                   ctypes.byref(b), ctypes.byref(nb), ctypes.byref(uo))
+    data = np.frombuffer(ctypes.string_at(b, nb.value), dtype=np.uint8).copy()
+    upd_off = np.ctypeslib.as_array(ctypes.cast(uo, ctypes.POINTER(ctypes.c_uint64)), (len(pos) + 1,)).copy()
+    _L().yw_free(b)
+    _L().yw_free(uo)
+    return Batch(data, upd_off, np.array([0, len(pos)], np.uint64), name="C1"), d["endContent"]

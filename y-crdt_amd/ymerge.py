@@ -1,0 +1,195 @@
+"""Host-side mirror of yrs' binary-update API over the MI355X engine (C ABI).
+
+Same names, argument meaning and error behaviour as yrs/src/alt.rs:
+    merge_updates_v1(updates)                 -> bytes   (alt.rs:15-28)
+    diff_updates_v1(update, state_vector)     -> bytes   (alt.rs:73-81)
+    encode_state_vector_from_update_v1(update)-> bytes   (alt.rs:54-57)
+A decode failure raises YrsError carrying yffi's error code (yffi/src/lib.rs:1137-1174).
+
+`Engine` is the batched, multi-tenant entry point (one HIP stream per device).
+There is no CPU fallback: without the gfx950 library or a GPU, calls raise.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libymerge.so")
+
+ERRORS = {2: "InvalidVarInt", 3: "EndOfBuffer", 4: "UnexpectedValue", 5: "InvalidJSON", 6: "Other",
+          7: "NotEnoughMemory", 20: "ReferencePanic", 21: "Unsupported", 30: "DeviceError"}
+
+
+class YrsError(Exception):
+    def __init__(self, code):
+        super().__init__(f"{ERRORS.get(code, 'error')} ({code})")
+        self.code = code
+
+
+class DeviceError(RuntimeError):
+    pass
+
+
+class _Stats(ctypes.Structure):
+    _fields_ = [("n_docs", ctypes.c_uint64), ("bytes_in", ctypes.c_uint64), ("bytes_out", ctypes.c_uint64),
+                ("docs_fast", ctypes.c_uint64), ("docs_exact", ctypes.c_uint64), ("docs_error", ctypes.c_uint64),
+                ("ms_total", ctypes.c_float), ("ms_plan", ctypes.c_float), ("ms_write", ctypes.c_float),
+                ("ms_count", ctypes.c_float)]
+
+
+class _DevRes(ctypes.Structure):
+    _fields_ = [("d_out", ctypes.c_void_p), ("d_out_off", ctypes.c_void_p), ("d_status", ctypes.c_void_p),
+                ("out_bytes", ctypes.c_uint64)]
+
+
+_lib = None
+
+
+def lib():
+    """Loads the in-tree gfx950 library; raises loudly if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise DeviceError(f"HIP engine not built: {LIB_PATH} missing (run __graft_entry__.build())")
+    # torch ships its own libamdhip64.so.7 (same soname as /opt/rocm's): load it first
+    # so the engine and torch's allocator share ONE HIP runtime in this process.
+    import torch  # noqa: F401
+    L = ctypes.CDLL(LIB_PATH)
+    c = ctypes
+    vp, u64, u32 = c.c_void_p, c.c_uint64, c.c_uint32
+    L.ymerge_ctx_create.restype = vp
+    L.ymerge_ctx_create.argtypes = [c.c_int]
+    L.ymerge_ctx_destroy.argtypes = [vp]
+    L.ymerge_updates_v1_batch_device.argtypes = [vp, vp, vp, vp, u64, c.POINTER(_DevRes)]
+    L.ydiff_updates_v1_batch_device.argtypes = [vp, vp, vp, vp, vp, u64, c.POINTER(_DevRes)]
+    L.yencode_state_vector_from_update_v1_batch_device.argtypes = [vp, vp, vp, u64, c.POINTER(_DevRes)]
+    L.ymerge_result_to_host.argtypes = [vp, c.POINTER(_DevRes), u64, vp, vp, vp]
+    L.ymerge_last_stats.argtypes = [vp, c.POINTER(_Stats)]
+    L.ymerge_updates_v1.restype = vp
+    L.ymerge_updates_v1.argtypes = [c.POINTER(c.c_char_p), c.POINTER(u32), u32, c.POINTER(u32)]
+    L.ydiff_updates_v1.restype = vp
+    L.ydiff_updates_v1.argtypes = [c.c_char_p, u32, c.c_char_p, u32, c.POINTER(u32)]
+    L.yencode_state_vector_from_update_v1.restype = vp
+    L.yencode_state_vector_from_update_v1.argtypes = [c.c_char_p, u32, c.POINTER(u32)]
+    L.ybinary_destroy.argtypes = [vp, u32]
+    L.ymerge_last_error.restype = c.c_uint8
+    _lib = L
+    return L
+
+
+def _take(ptr, n):
+    if not ptr:
+        code = lib().ymerge_last_error()
+        if code == 30:
+            raise DeviceError("no usable MI355X (HIP)")
+        raise YrsError(code)
+    data = ctypes.string_at(ptr, n.value)
+    lib().ybinary_destroy(ptr, n.value)
+    return data
+
+
+def merge_updates_v1(updates):
+    """yrs::merge_updates_v1 (alt.rs:15)."""
+    ups = [bytes(u) for u in updates]
+    arr = (ctypes.c_char_p * max(1, len(ups)))(*ups)
+    lens = (ctypes.c_uint32 * max(1, len(ups)))(*[len(u) for u in ups])
+    n = ctypes.c_uint32()
+    return _take(lib().ymerge_updates_v1(arr, lens, len(ups), ctypes.byref(n)), n)
+
+
+def diff_updates_v1(update, state_vector):
+    """yrs::diff_updates_v1 (alt.rs:73)."""
+    n = ctypes.c_uint32()
+    u, s = bytes(update), bytes(state_vector)
+    return _take(lib().ydiff_updates_v1(u, len(u), s, len(s), ctypes.byref(n)), n)
+
+
+def encode_state_vector_from_update_v1(update):
+    """yrs::encode_state_vector_from_update_v1 (alt.rs:54)."""
+    n = ctypes.c_uint32()
+    u = bytes(update)
+    return _take(lib().yencode_state_vector_from_update_v1(u, len(u), ctypes.byref(n)), n)
+
+
+class DeviceResult:
+    def __init__(self, engine, res, n_docs):
+        self.engine, self.res, self.n_docs = engine, res, n_docs
+
+    @property
+    def out_bytes(self):
+        return int(self.res.out_bytes)
+
+    def to_host(self):
+        n = self.n_docs
+        out = np.empty(max(1, self.out_bytes), dtype=np.uint8)
+        off = np.empty(n + 1, dtype=np.uint64)
+        st = np.empty(max(1, n), dtype=np.uint8)
+        rc = lib().ymerge_result_to_host(self.engine._ctx, ctypes.byref(self.res), n, out.ctypes.data,
+                                         off.ctypes.data, st.ctypes.data)
+        if rc:
+            raise DeviceError(f"result copy failed ({rc})")
+        return out[: self.out_bytes], off, st[:n]
+
+
+class Engine:
+    """One HIP stream + HBM workspace on one GPU; batches of documents."""
+
+    def __init__(self, device=0):
+        self._ctx = lib().ymerge_ctx_create(device)
+        if not self._ctx:
+            raise DeviceError(f"cannot open HIP device {device}")
+        self.device = device
+
+    def close(self):
+        if self._ctx:
+            lib().ymerge_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def merge_device(self, d_bytes, d_upd_off, d_doc_upd, n_docs):
+        """Inputs are device pointers (ints) into HBM; returns a DeviceResult."""
+        res = _DevRes()
+        rc = lib().ymerge_updates_v1_batch_device(self._ctx, d_bytes, d_upd_off, d_doc_upd, n_docs,
+                                                  ctypes.byref(res))
+        if rc:
+            raise DeviceError(f"merge batch failed ({rc})")
+        return DeviceResult(self, res, n_docs)
+
+    def diff_device(self, d_bytes, d_upd_off, d_sv, d_sv_off, n_docs):
+        res = _DevRes()
+        rc = lib().ydiff_updates_v1_batch_device(self._ctx, d_bytes, d_upd_off, d_sv, d_sv_off, n_docs,
+                                                 ctypes.byref(res))
+        if rc:
+            raise DeviceError(f"diff batch failed ({rc})")
+        return DeviceResult(self, res, n_docs)
+
+    def state_vector_device(self, d_bytes, d_upd_off, n_docs):
+        res = _DevRes()
+        rc = lib().yencode_state_vector_from_update_v1_batch_device(self._ctx, d_bytes, d_upd_off, n_docs,
+                                                                    ctypes.byref(res))
+        if rc:
+            raise DeviceError(f"state-vector batch failed ({rc})")
+        return DeviceResult(self, res, n_docs)
+
+    def stats(self):
+        s = _Stats()
+        lib().ymerge_last_stats(self._ctx, ctypes.byref(s))
+        return {k: getattr(s, k) for k, _ in _Stats._fields_}
+
+    # convenience: host arrays in, host arrays out (uses torch for HBM residency)
+    def merge_host(self, data, upd_off, doc_upd):
+        import torch
+        dev = torch.device("cuda", self.device)
+        t_b = torch.from_numpy(np.ascontiguousarray(data, dtype=np.uint8)).to(dev)
+        t_u = torch.from_numpy(np.ascontiguousarray(upd_off, dtype=np.uint64).view(np.int64)).to(dev)
+        t_d = torch.from_numpy(np.ascontiguousarray(doc_upd, dtype=np.uint64).view(np.int64)).to(dev)
+        torch.cuda.synchronize(dev)
+        r = self.merge_device(t_b.data_ptr(), t_u.data_ptr(), t_d.data_ptr(), len(doc_upd) - 1)
+        return r.to_host()
