@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--docs", type=int, default=10_000, help="documents per GPU")
     ap.add_argument("--ops", type=int, default=1_000, help="updates per document")
-    ap.add_argument("--cpu-sample", type=int, default=1_000, help="docs in the CPU-baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=10_000, help="docs in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
 
@@ -85,7 +85,8 @@ def main():
     eng = ymerge.Engine(local)
 
     def step():
-        return eng.merge_device(t_b.data_ptr(), t_u.data_ptr(), t_d.data_ptr(), batch.n_docs)
+        return eng.merge_device(t_b.data_ptr(), batch.n_bytes, t_u.data_ptr(), batch.n_updates, t_d.data_ptr(),
+                                batch.n_docs)
 
     for _ in range(a.warmup):
         step()
@@ -105,8 +106,9 @@ def main():
     out_bytes = res.out_bytes
     _, _, st = res.to_host()
     n_err = int((st != 0).sum())
-    ms_kernel = float(np.mean([s["ms_write"] for s in kstats]))
-    ms_plan = float(np.mean([s["ms_plan"] for s in kstats]))
+    ms_kernel = float(np.mean([s["ms_fast"] for s in kstats]))
+    ms_exact = float(np.mean([s["ms_exact"] for s in kstats]))
+    docs_exact = int(kstats[-1]["docs_exact"])
     local_stats = torch.tensor([batch.n_docs, batch.n_bytes, out_bytes, n_err, elapsed, ms_kernel],
                                dtype=torch.float64, device=dev)
     if dist:
@@ -156,8 +158,8 @@ def main():
                    "parallelism": f"doc-hash sharding x{world}", "error_docs": int(allst[:, 3].sum())},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_seq_merge<WRITE>", "kernel_ms": ms_kernel, "plan_ms": ms_plan,
-                     "alg_bytes_per_launch": alg_bytes},
+                     "kernel": "k_fast_merge", "kernel_ms": ms_kernel, "exact_path_ms": ms_exact,
+                     "docs_exact_path": docs_exact, "alg_bytes_per_launch": alg_bytes},
         "cpu_baseline": cpu,
     }
     print(json.dumps(line))

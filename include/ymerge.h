@@ -62,21 +62,27 @@ void ymerge_ctx_destroy(ymerge_ctx *ctx);
 typedef struct {
   uint64_t n_docs, bytes_in, bytes_out;
   uint64_t docs_fast, docs_exact, docs_error;
-  float ms_total, ms_plan, ms_write, ms_count;
+  float ms_total, ms_fast, ms_exact, ms_tail;
 } ymerge_stats;
 
-/* Device-resident result, owned by the context, valid until the next batch. */
+/* Device-resident result, owned by the context, valid until the next batch.
+ * Document d's output is d_out[d_out_start[d] .. d_out_start[d] + d_out_len[d]);
+ * documents are written where their slot is (no packing pass on the hot path). */
 typedef struct {
-  uint8_t *d_out;      /* output arena */
-  uint64_t *d_out_off; /* n_docs + 1 offsets (documents with status != 0 are empty) */
-  uint8_t *d_status;   /* n_docs status codes */
-  uint64_t out_bytes;  /* arena size */
+  uint8_t *d_out;         /* output arena */
+  uint64_t *d_out_start;  /* n_docs */
+  uint64_t *d_out_len;    /* n_docs (0 when status != 0) */
+  uint8_t *d_status;      /* n_docs status codes */
+  uint64_t arena_bytes;   /* size of d_out */
+  uint64_t out_bytes;     /* sum of d_out_len */
 } ymerge_device_result;
 
-/* merge_updates_v1 over a batch whose arena/offsets already live in HBM of the
- * context's device.  Returns 0 or YMERGE_ERR_DEVICE. */
-int ymerge_updates_v1_batch_device(ymerge_ctx *ctx, const uint8_t *d_bytes, const uint64_t *d_upd_off,
-                                   const uint64_t *d_doc_upd, uint64_t n_docs, ymerge_device_result *res);
+/* merge_updates_v1 over a batch whose arena (n_bytes) and offsets (n_updates + 1,
+ * n_docs + 1) already live in HBM of the context's device.
+ * Returns 0 or YMERGE_ERR_DEVICE. */
+int ymerge_updates_v1_batch_device(ymerge_ctx *ctx, const uint8_t *d_bytes, uint64_t n_bytes,
+                                   const uint64_t *d_upd_off, uint64_t n_updates, const uint64_t *d_doc_upd,
+                                   uint64_t n_docs, ymerge_device_result *res);
 /* encode_state_vector_from_update_v1 / diff_updates_v1: one update per document
  * (d_upd_off has n_docs + 1 entries); diff also takes one encoded state vector
  * per document. */
@@ -86,7 +92,8 @@ int yencode_state_vector_from_update_v1_batch_device(ymerge_ctx *ctx, const uint
 int ydiff_updates_v1_batch_device(ymerge_ctx *ctx, const uint8_t *d_bytes, const uint64_t *d_upd_off,
                                   const uint8_t *d_sv_bytes, const uint64_t *d_sv_off, uint64_t n_docs,
                                   ymerge_device_result *res);
-/* copy the last device result to host buffers (out: out_bytes, out_off: n_docs+1, status: n_docs) */
+/* pack the last device result into host buffers: out (res->out_bytes), out_off (n_docs + 1,
+ * document d at out[out_off[d] .. out_off[d+1])), status (n_docs) */
 int ymerge_result_to_host(ymerge_ctx *ctx, const ymerge_device_result *res, uint64_t n_docs, uint8_t *out,
                           uint64_t *out_off, uint8_t *status);
 void ymerge_last_stats(ymerge_ctx *ctx, ymerge_stats *stats);

@@ -119,6 +119,42 @@ def test_c4_delete_heavy(engine, oracle):
     check_batch(engine, oracle, workloads.delete_heavy_docs(24, ops_per_doc=2000), mode=1)
 
 
+def test_exact_engine_only(oracle):
+    """Same C2/C4 inputs through the exact per-document engine alone (fast path off)."""
+    import ymerge
+    os.environ["YMERGE_FAST_THREADS"] = "0"
+    try:
+        e = ymerge.Engine(0)
+    finally:
+        del os.environ["YMERGE_FAST_THREADS"]
+    try:
+        check_batch(e, oracle, workloads.text_docs(100, 500, seed=5))
+        check_batch(e, oracle, workloads.delete_heavy_docs(6, ops_per_doc=1500, seed=9))
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("threads", ["256", "1024"])
+def test_fast_path_workgroup_sizes(oracle, threads):
+    import ymerge
+    os.environ["YMERGE_FAST_THREADS"] = threads
+    try:
+        e = ymerge.Engine(0)
+    finally:
+        del os.environ["YMERGE_FAST_THREADS"]
+    try:
+        check_batch(e, oracle, workloads.text_docs(150, 1000, seed=11))
+    finally:
+        e.close()
+
+
+def test_fast_path_coverage(engine, oracle):
+    """C2 documents must stay on the fast path (no silent exact-engine fallback)."""
+    check_batch(engine, oracle, workloads.text_docs(500, 1000, seed=21))
+    st = engine.stats()
+    assert st["docs_exact"] == 0 and st["docs_fast"] == 500
+
+
 def test_c1_automerge_trace(engine, oracle):
     b, _ = workloads.trace_updates()
     check_batch(engine, oracle, b, mode=1)

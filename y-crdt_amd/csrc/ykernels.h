@@ -14,11 +14,29 @@ struct BatchIn {
   uint32_t n_docs;
 };
 
-void launch_seq_count(const BatchIn &b, uint8_t *status, uint32_t *counts, uint64_t *need, hipStream_t s);
-void launch_seq_merge(bool write, const BatchIn &b, const uint8_t *status, const uint32_t *counts,
+// LDS capacities of the one-workgroup-per-document fast path (per document)
+struct FastCaps {
+  uint32_t in_cap, u_cap, b_cap, e_cap, r_cap;
+};
+// per-document results; path 0 = written by the fast path, 1 = needs the exact engine
+struct FastOut {
+  uint8_t *out; // output arena: document d's slot starts at 2*byte_start(d) + 64*d
+  uint64_t *out_start, *out_len;
+  uint8_t *status, *path;
+};
+size_t fast_lds_bytes(const FastCaps &c);
+void launch_fast_merge(const BatchIn &b, const FastCaps &caps, const FastOut &o, int nt, hipStream_t s);
+
+// exact per-document engine; `path` (optional) restricts it to documents with path == 1
+void launch_seq_count(const BatchIn &b, const uint8_t *path, uint8_t *status, uint32_t *counts, uint64_t *need,
+                      uint32_t *n_exact, hipStream_t s);
+void launch_seq_merge(bool write, const BatchIn &b, const uint8_t *path, const uint8_t *status, const uint32_t *counts,
                       const uint64_t *scr_off, uint32_t *scratch, uint64_t *sizes, const uint64_t *out_off,
-                      uint8_t *out, uint8_t *status_out, hipStream_t s);
+                      uint8_t *out, uint64_t out_base, uint64_t *out_start, uint64_t *out_len, uint8_t *status_out,
+                      hipStream_t s);
 // exclusive scan: out[0..n] (out[n] = total); tmp needs >= (n/2048 + 2) u64
 void launch_scan_u64(const uint64_t *in, uint64_t *out, uint32_t n, uint64_t *tmp, hipStream_t s);
 size_t scan_tmp_elems(uint32_t n);
+void launch_pack(const uint8_t *src, const uint64_t *start, const uint64_t *len, const uint64_t *pack_off,
+                 uint8_t *dst, uint32_t n_docs, hipStream_t s);
 } // namespace ym

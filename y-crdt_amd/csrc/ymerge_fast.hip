@@ -1,0 +1,932 @@
+// ymerge_fast.hip — parallel merge_updates_v1: one workgroup per document, LDS-resident.
+//
+// Stages (all inside one launch, one document per workgroup):
+//   1 stage   : coalesced copy of the document's bytes + update offsets into LDS
+//   2 decode  : lane-per-update walk (ywalk.h), counts -> block scan -> second walk
+//               writes SoA block / DeleteSet records at their scanned positions
+//   3 sort    : blocks by (client desc, clock asc, input order) — LDS bitonic,
+//               skipped when already ordered
+//   4 squash  : segmented max-scan of block ends -> keep / gap(Skip) / violation.
+//               Fast-path precondition: every block starts at or
+//               after the running end, or is fully covered with a later start, or
+//               is a byte-identical duplicate.  Otherwise the document is handed to
+//               the exact per-document engine (ymerge_seq.hip).
+//   5 DS union: entries sorted by (client, first occurrence) -> yrs' hashbrown
+//               client order; ranges sorted by (client, start) -> segmented union
+//               (join overlapping or adjacent, id_set.rs:129-164)
+//   6 encode  : prefix sums over output sizes; each lane writes its pieces into the
+//               document's output slot (canonical re-encode only where the input was
+//               not canonical).
+#include "ycodec.h"
+#include "ykernels.h"
+#include "ywalk.h"
+
+namespace ym {
+
+// ------------------------------------------------------------------ LDS layout
+// [in][uoff][block records][DS records] then a union of three phase-local regions:
+//   phase 2 (decode): per-update counts -> offsets
+//   phase 3/4/6 (blocks): sort keys, classify flags, per-position output offsets
+//   phase 5 (DeleteSet): sort keys, union flags/offsets, per-client tables
+struct FastLayout {
+  uint32_t in, uoff, bc, bk, bl, bp, bm, ec, et, rs, re, ri;
+  uint32_t cB, cE, cR;
+  uint32_t skey, sval, sE, sf, sz, sseg;
+  uint32_t dkey, dval, cend, coff, chead, dcl, dfirst, dord, dnc, dbeg, doff;
+  uint32_t misc, total;
+};
+__host__ __device__ inline uint32_t pow2ceil(uint32_t x) {
+  uint32_t p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+__host__ __device__ inline FastLayout fast_layout(const FastCaps &c) {
+  FastLayout L;
+  uint32_t o = 0;
+  auto take = [&](uint32_t bytes) {
+    uint32_t r = o;
+    o += (bytes + 15) & ~15u;
+    return r;
+  };
+  const uint32_t BS = pow2ceil(c.b_cap), RS = pow2ceil(c.r_cap > c.e_cap ? c.r_cap : c.e_cap);
+  L.in = take(c.in_cap + 16);
+  L.uoff = take(4 * (c.u_cap + 1));
+  L.bc = take(4 * c.b_cap);
+  L.bk = take(4 * c.b_cap);
+  L.bl = take(4 * c.b_cap);
+  L.bp = take(4 * c.b_cap);
+  L.bm = take(4 * c.b_cap);
+  L.ec = take(4 * c.e_cap);
+  L.et = take(4 * c.e_cap);
+  L.rs = take(4 * c.r_cap);
+  L.re = take(4 * c.r_cap);
+  L.ri = take(4 * c.r_cap);
+  L.misc = take(4 * 256);
+  const uint32_t u0 = o;
+  L.cB = take(4 * (c.u_cap + 1));
+  L.cE = take(4 * (c.u_cap + 1));
+  L.cR = take(4 * (c.u_cap + 1));
+  uint32_t end = o;
+  o = u0;
+  L.skey = take(8 * BS);
+  L.sval = take(4 * BS);
+  L.sE = take(4 * c.b_cap);
+  L.sf = take(4 * c.b_cap);
+  L.sz = take(4 * (c.b_cap + 1));
+  L.sseg = take(4 * (c.b_cap + 1));
+  if (o > end) end = o;
+  o = u0;
+  L.dkey = take(8 * RS);
+  L.dval = take(4 * RS);
+  L.cend = take(4 * (RS + 1));
+  L.coff = take(4 * (RS + 1));
+  L.chead = take(4 * (RS + 1));
+  L.dcl = take(4 * (RS + 1));
+  L.dfirst = take(4 * (RS + 1));
+  L.dord = take(4 * (RS + 1));
+  L.dnc = take(4 * (RS + 1));
+  L.dbeg = take(4 * (RS + 1));
+  L.doff = take(4 * (RS + 1));
+  if (o > end) end = o;
+  L.total = end;
+  return L;
+}
+
+// ------------------------------------------------------------------ block-wide helpers
+template <int NT> struct Blk {
+  static constexpr int NW = NT / 64;
+};
+
+// exclusive sum over per-lane values; returns the lane's exclusive prefix, *total = sum
+template <int NT> __device__ __forceinline__ uint32_t bscan_sum(uint32_t v, uint32_t *ws, uint32_t &total) {
+  uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) ws[w] = x;
+  __syncthreads();
+  if (t == 0) {
+    uint32_t acc = 0;
+    for (int i = 0; i < NT / 64; i++) {
+      uint32_t s = ws[i];
+      ws[i] = acc;
+      acc += s;
+    }
+    ws[NT / 64] = acc;
+  }
+  __syncthreads();
+  uint32_t r = ws[w] + x - v;
+  total = ws[NT / 64];
+  __syncthreads();
+  return r;
+}
+
+// segmented scan pair: (flag, value); (f1,v1)+(f2,v2) = (f1|f2, f2 ? v2 : op(v1,v2))
+struct OpMax {
+  __device__ static uint32_t f(uint32_t a, uint32_t b) { return a > b ? a : b; }
+};
+struct OpSum {
+  __device__ static uint32_t f(uint32_t a, uint32_t b) { return a + b; }
+};
+struct OpFirst {
+  __device__ static uint32_t f(uint32_t a, uint32_t) { return a; }
+};
+// Exclusive segmented scan of the per-lane aggregate (flag, v): returns (pf, pv) = combination
+// of all lanes before this lane (pf = any head before in ... ), over the whole workgroup.
+template <int NT, class Op>
+__device__ __forceinline__ void bscan_seg(uint32_t f, uint32_t v, uint32_t *ws, uint32_t &pf, uint32_t &pv) {
+  uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+  uint32_t xf = f, xv = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t yf = __shfl_up(xf, o, 64), yv = __shfl_up(xv, o, 64);
+    if (lane >= (uint32_t)o) {
+      xv = xf ? xv : Op::f(yv, xv);
+      xf = xf | yf;
+    }
+  }
+  // exclusive within wave
+  uint32_t ef = __shfl_up(xf, 1, 64), ev = __shfl_up(xv, 1, 64);
+  if (lane == 0) {
+    ef = 0;
+    ev = 0;
+  }
+  if (lane == 63) {
+    ws[2 * w] = xf;
+    ws[2 * w + 1] = xv;
+  }
+  __syncthreads();
+  if (t == 0) {
+    uint32_t af = 0, av = 0;
+    for (int i = 0; i < NT / 64; i++) {
+      uint32_t sf = ws[2 * i], sv = ws[2 * i + 1];
+      ws[2 * i] = af;
+      ws[2 * i + 1] = av;
+      av = sf ? sv : Op::f(av, sv);
+      af |= sf;
+    }
+  }
+  __syncthreads();
+  uint32_t wf = ws[2 * w], wv = ws[2 * w + 1];
+  __syncthreads();
+  // combine wave prefix (wf,wv) with in-wave exclusive (ef,ev)
+  if (lane == 0) {
+    pf = wf;
+    pv = wv;
+  } else {
+    pv = ef ? ev : Op::f(wv, ev);
+    pf = wf | ef;
+  }
+}
+
+// bitonic sort of (key64, val32) pairs, n a power of two, composite order (key, val)
+template <int NT> __device__ void bitonic(uint64_t *k, uint32_t *v, uint32_t n) {
+  for (uint32_t size = 2; size <= n; size <<= 1) {
+    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+      for (uint32_t i = threadIdx.x; i < n / 2; i += NT) {
+        uint32_t lo = 2 * i - (i & (stride - 1));
+        uint32_t hi = lo + stride;
+        bool up = ((lo & size) == 0);
+        uint64_t a = k[lo], b = k[hi];
+        uint32_t va = v[lo], vb = v[hi];
+        bool gt = a > b || (a == b && va > vb);
+        if (gt == up) {
+          k[lo] = b;
+          k[hi] = a;
+          v[lo] = vb;
+          v[hi] = va;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// ------------------------------------------------------------------ walk sinks
+struct FastCount {
+  uint32_t nb, ne, nr;
+  bool unsupported;
+  DsOrder ord;
+  __device__ void on_section(uint32_t) {}
+  __device__ int on_block(uint32_t, uint32_t, const BlockInfo &bi, uint32_t, uint32_t) {
+    if (bi.kind != BK_SKIP) nb++;
+    if (bi.unsupported) unsupported = true;
+    return 0;
+  }
+  __device__ int on_ds_begin(uint32_t) {
+    ord.begin();
+    return 0;
+  }
+  __device__ int on_ds_entry(uint32_t client, uint32_t) {
+    ne++;
+    uint32_t dead;
+    return ord.insert(client, dead);
+  }
+  __device__ void on_ds_range(uint32_t, uint32_t) { nr++; }
+  __device__ int on_ds_done() { return 0; }
+};
+
+struct FastFill {
+  uint32_t *bc, *bk, *bl, *bp, *bm, *ec, *et, *rs, *re, *ri;
+  const uint8_t *doc;
+  uint32_t doc_len, upd, ubase; // update index, byte offset of update within doc
+  uint32_t nb, ne, nr, ebase;
+  DsOrder ord;
+  __device__ void on_section(uint32_t) {}
+  __device__ int on_block(uint32_t client, uint32_t clock, const BlockInfo &bi, uint32_t bpos, uint32_t blen) {
+    if (bi.kind == BK_SKIP) return 0;
+    uint32_t pos = ubase + bpos;
+    uint32_t canon = blen;
+    if (bi.reenc) {
+      Counter cn;
+      emit_block(doc, doc_len, pos, client, clock, bi.len, 0, cn);
+      canon = (uint32_t)cn.n;
+    }
+    bc[nb] = client;
+    bk[nb] = clock;
+    bl[nb] = bi.len;
+    bp[nb] = pos | (blen << 16);
+    bm[nb] = (uint32_t)bi.kind | (bi.reenc ? 4u : 0u) | (canon << 8);
+    nb++;
+    return 0;
+  }
+  __device__ int on_ds_begin(uint32_t) {
+    ord.begin();
+    ebase = ne;
+    return 0;
+  }
+  __device__ int on_ds_entry(uint32_t client, uint32_t) {
+    uint32_t dead;
+    YM_TRY(ord.insert(client, dead));
+    if (dead != ~0u) et[ebase + dead] &= 0x7FFFFFFFu; // replaced in this update: dead
+    ec[ne] = client;
+    et[ne] = 0x80000000u | (upd << 8);
+    ne++;
+    return 0;
+  }
+  __device__ void on_ds_range(uint32_t s, uint32_t e) {
+    rs[nr] = s;
+    re[nr] = e;
+    ri[nr] = ne - 1;
+    nr++;
+  }
+  __device__ int on_ds_done() {
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < ord.hb.buckets; i++)
+      if (ord.hb.slot[i]) et[ebase + ord.hb.slot[i] - 1] |= k++;
+    return 0;
+  }
+};
+
+// ------------------------------------------------------------------ the kernel
+template <int NT>
+__global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, FastOut o) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  const FastLayout L = fast_layout(caps);
+  const uint32_t d = blockIdx.x;
+  if (d >= b.n_docs) return;
+  const uint32_t t = threadIdx.x;
+  uint32_t *misc = (uint32_t *)(smem + L.misc);
+  // misc[0] err key, [1] flags, [2..] scan workspace (NT/64*2+2 words), [64..] scalars
+  uint32_t *ws = misc + 2;
+  uint32_t *sc = misc + 64;
+
+  const uint64_t u0 = b.doc_upd[d], u1 = b.doc_upd[d + 1];
+  const uint32_t U = (uint32_t)(u1 - u0);
+  const uint64_t B0 = b.upd_off[u0], B1 = b.upd_off[u1];
+  const uint32_t nbytes = (uint32_t)(B1 - B0);
+  const uint64_t slot = 2 * B0 + 64ull * d;
+  const uint64_t cap = 2ull * nbytes + 64;
+  if (U > caps.u_cap || nbytes > caps.in_cap) {
+    if (t == 0) {
+      o.path[d] = 1;
+      o.status[d] = 0;
+      o.out_len[d] = 0;
+      o.out_start[d] = slot;
+    }
+    return;
+  }
+  // ---- 1 stage bytes (word copy + byte tail) and update offsets
+  uint8_t *in = smem + L.in;
+  {
+    const uint64_t a0 = B0 & ~3ull;
+    const uint32_t shift = (uint32_t)(B0 - a0);
+    const uint32_t nfull = (uint32_t)((B1 - a0) / 4);
+    const uint32_t *src = (const uint32_t *)(b.bytes + a0);
+    uint32_t *dst = (uint32_t *)in;
+    for (uint32_t k = t; k < nfull; k += NT) dst[k] = src[k];
+    for (uint64_t q = a0 + 4ull * nfull + t; q < B1; q += NT) in[q - a0] = b.bytes[q];
+    in += shift; // doc byte j at in[j]
+  }
+  uint32_t *uoff = (uint32_t *)(smem + L.uoff);
+  for (uint32_t i = t; i <= U; i += NT) uoff[i] = (uint32_t)(b.upd_off[u0 + i] - B0);
+  if (t == 0) {
+    misc[0] = 0xFFFFFFFFu;
+    misc[1] = 0;
+  }
+  __syncthreads();
+
+  // ---- 2a walk: counts, first error, unsupported
+  uint32_t *cB = (uint32_t *)(smem + L.cB), *cE = (uint32_t *)(smem + L.cE), *cR = (uint32_t *)(smem + L.cR);
+  {
+    FastCount s;
+    s.unsupported = false;
+    for (uint32_t i = t; i < U; i += NT) {
+      s.nb = s.ne = s.nr = 0;
+      int e = walk_update(in + uoff[i], uoff[i + 1] - uoff[i], s);
+      if (e) atomicMin(&misc[0], (i << 8) | (uint32_t)e);
+      cB[i] = s.nb;
+      cE[i] = s.ne;
+      cR[i] = s.nr;
+    }
+    if (s.unsupported) atomicOr(&misc[1], 1u);
+  }
+  __syncthreads();
+  {
+    uint32_t ek = misc[0];
+    if (ek != 0xFFFFFFFFu || misc[1]) {
+      if (t == 0) {
+        o.status[d] = (uint8_t)(ek != 0xFFFFFFFFu ? (ek & 0xFF) : E_UNSUPPORTED);
+        o.path[d] = 0;
+        o.out_len[d] = 0;
+        o.out_start[d] = slot;
+      }
+      return;
+    }
+  }
+  // ---- 2b exclusive scans of the per-update counts (contiguous chunk per lane)
+  uint32_t NB, NE, NR;
+  {
+    const uint32_t per = (U + NT - 1) / NT, j0 = t * per, j1 = j0 + per < U ? j0 + per : U;
+    uint32_t sb = 0, se = 0, sr = 0;
+    for (uint32_t j = j0; j < j1; j++) {
+      sb += cB[j];
+      se += cE[j];
+      sr += cR[j];
+    }
+    uint32_t pb = bscan_sum<NT>(sb, ws, NB);
+    uint32_t pe = bscan_sum<NT>(se, ws, NE);
+    uint32_t pr = bscan_sum<NT>(sr, ws, NR);
+    for (uint32_t j = j0; j < j1; j++) {
+      uint32_t x = cB[j], y = cE[j], z = cR[j];
+      cB[j] = pb;
+      cE[j] = pe;
+      cR[j] = pr;
+      pb += x;
+      pe += y;
+      pr += z;
+    }
+  }
+  __syncthreads();
+  if (NB > caps.b_cap || NE > caps.e_cap || NR > caps.r_cap) {
+    if (t == 0) {
+      o.path[d] = 1;
+      o.status[d] = 0;
+      o.out_len[d] = 0;
+      o.out_start[d] = slot;
+    }
+    return;
+  }
+  uint32_t *bc = (uint32_t *)(smem + L.bc), *bk = (uint32_t *)(smem + L.bk), *bl = (uint32_t *)(smem + L.bl),
+           *bp = (uint32_t *)(smem + L.bp), *bm = (uint32_t *)(smem + L.bm);
+  uint32_t *ec = (uint32_t *)(smem + L.ec), *et = (uint32_t *)(smem + L.et);
+  uint32_t *rs = (uint32_t *)(smem + L.rs), *re = (uint32_t *)(smem + L.re), *ri = (uint32_t *)(smem + L.ri);
+  // ---- 2c second walk: records at scanned positions
+  {
+    FastFill f;
+    f.bc = bc;
+    f.bk = bk;
+    f.bl = bl;
+    f.bp = bp;
+    f.bm = bm;
+    f.ec = ec;
+    f.et = et;
+    f.rs = rs;
+    f.re = re;
+    f.ri = ri;
+    f.doc = in;
+    f.doc_len = nbytes;
+    for (uint32_t i = t; i < U; i += NT) {
+      f.upd = i;
+      f.ubase = uoff[i];
+      f.nb = cB[i];
+      f.ne = cE[i];
+      f.nr = cR[i];
+      walk_update(in + uoff[i], uoff[i + 1] - uoff[i], f);
+    }
+  }
+  __syncthreads();
+
+  // ---- 3 sort blocks: key = (~client, clock), val = record index (input order)
+  uint64_t *skey = (uint64_t *)(smem + L.skey);
+  uint32_t *sval = (uint32_t *)(smem + L.sval);
+  {
+    uint32_t unsorted = 0;
+    for (uint32_t j = t; j + 1 < NB; j += NT) {
+      uint64_t ka = ((uint64_t)(~bc[j]) << 32) | bk[j], kb = ((uint64_t)(~bc[j + 1]) << 32) | bk[j + 1];
+      if (ka > kb) unsorted = 1;
+    }
+    unsorted = __syncthreads_or(unsorted);
+    uint32_t n2 = unsorted ? pow2ceil(NB) : NB;
+    for (uint32_t j = t; j < n2; j += NT) {
+      skey[j] = j < NB ? (((uint64_t)(~bc[j]) << 32) | bk[j]) : ~0ull;
+      sval[j] = j;
+    }
+    __syncthreads();
+    if (unsorted) bitonic<NT>(skey, sval, n2);
+  }
+  // ---- 4 classify: per lane a contiguous chunk of sorted positions
+  uint32_t *sE = (uint32_t *)(smem + L.sE), *sf = (uint32_t *)(smem + L.sf), *sz = (uint32_t *)(smem + L.sz);
+  const uint32_t per = (NB + NT - 1) / NT, j0 = t * per, j1 = j0 + per < NB ? j0 + per : NB;
+  {
+    // segmented exclusive max of block ends (segments = clients)
+    uint32_t lf = 0, lv = 0;
+    for (uint32_t j = j0; j < j1; j++) {
+      uint32_t r = sval[j];
+      bool head = j == 0 || bc[sval[j - 1]] != bc[r];
+      uint32_t e = bk[r] + bl[r];
+      if (head) {
+        lf = 1;
+        lv = e;
+      } else
+        lv = OpMax::f(lv, e);
+    }
+    uint32_t pf, pv;
+    bscan_seg<NT, OpMax>(lf, lv, ws, pf, pv);
+    uint32_t run = pv; // running max of ends before j within the current segment
+    uint32_t viol = 0;
+    for (uint32_t j = j0; j < j1; j++) {
+      uint32_t r = sval[j];
+      bool head = j == 0 || bc[sval[j - 1]] != bc[r];
+      uint32_t k = bk[r], e = k + bl[r];
+      uint32_t E = head ? 0 : run;
+      uint32_t flag = 0;
+      if (bl[r] == 0) viol = 1; // zero-length GC: leave to the exact engine
+      if (head || k >= E) {
+        flag = 1; // keep
+        if (!head && k > E) flag |= 2; // Skip of (k - E) before it
+      } else if (e > E) {
+        viol = 1; // partial overlap
+      }
+      sE[j] = E;
+      sf[j] = flag;
+      run = head ? e : OpMax::f(run, e);
+    }
+    viol = __syncthreads_or(viol);
+    if (viol) {
+      if (t == 0) {
+        o.path[d] = 1;
+        o.status[d] = 0;
+        o.out_len[d] = 0;
+        o.out_start[d] = slot;
+      }
+      return;
+    }
+  }
+  // dropped blocks must be covered with a later start, or byte-identical to the last kept block
+  {
+    // last kept sorted index before j (segmented "max" of kept positions)
+    uint32_t lf = 0, lv = 0;
+    for (uint32_t j = j0; j < j1; j++) {
+      uint32_t r = sval[j];
+      bool head = j == 0 || bc[sval[j - 1]] != bc[r];
+      if (head) {
+        lf = 1;
+        lv = 0;
+      }
+      if (sf[j] & 1) lv = j + 1;
+    }
+    uint32_t pf, pv;
+    bscan_seg<NT, OpMax>(lf, lv, ws, pf, pv);
+    uint32_t last = pv;
+    uint32_t viol = 0;
+    for (uint32_t j = j0; j < j1; j++) {
+      uint32_t r = sval[j];
+      bool head = j == 0 || bc[sval[j - 1]] != bc[r];
+      if (head) last = 0;
+      if (!(sf[j] & 1)) {
+        uint32_t kr = sval[last - 1];
+        if (bk[kr] == bk[r]) {
+          // same start: must be an exact duplicate (kind, length, bytes)
+          uint32_t pa = bp[kr] & 0xFFFF, la = bp[kr] >> 16, pb = bp[r] & 0xFFFF, lb = bp[r] >> 16;
+          bool same = la == lb && (bm[kr] & 3) == (bm[r] & 3) && bl[kr] == bl[r];
+          for (uint32_t q = 0; same && q < la; q++) same = in[pa + q] == in[pb + q];
+          if (!same) viol = 1;
+        }
+      } else
+        last = j + 1;
+    }
+    viol = __syncthreads_or(viol);
+    if (viol) {
+      if (t == 0) {
+        o.path[d] = 1;
+        o.status[d] = 0;
+        o.out_len[d] = 0;
+        o.out_start[d] = slot;
+      }
+      return;
+    }
+  }
+  // ---- 6a block section sizes: per client header + (Skip) + canonical block bytes
+  uint32_t blocks_size, NC;
+  uint32_t *sseg = (uint32_t *)(smem + L.sseg);
+  {
+    uint32_t nh = 0, lf = 0, lv = 0;
+    for (uint32_t j = j0; j < j1; j++) {
+      uint32_t r = sval[j];
+      bool head = j == 0 || bc[sval[j - 1]] != bc[r];
+      uint32_t c = (sf[j] & 1) + ((sf[j] >> 1) & 1);
+      if (head) {
+        nh++;
+        lf = 1;
+        lv = c;
+      } else
+        lv += c;
+    }
+    const uint32_t hpre = bscan_sum<NT>(nh, ws, NC);
+    uint32_t pf, pv;
+    bscan_seg<NT, OpSum>(lf, lv, ws, pf, pv);
+    uint32_t rank = hpre, run = pv;
+    for (uint32_t j = j0; j < j1; j++) {
+      uint32_t r = sval[j];
+      bool head = j == 0 || bc[sval[j - 1]] != bc[r];
+      uint32_t c = (sf[j] & 1) + ((sf[j] >> 1) & 1);
+      if (head) {
+        rank++;
+        run = c;
+      } else
+        run += c;
+      bool tail = j + 1 == NB || bc[sval[j + 1]] != bc[r];
+      if (tail) sseg[rank - 1] = run; // blocks emitted for this client
+    }
+    __syncthreads();
+    uint32_t ls = 0;
+    rank = hpre;
+    for (uint32_t j = j0; j < j1; j++) {
+      uint32_t r = sval[j];
+      bool head = j == 0 || bc[sval[j - 1]] != bc[r];
+      uint32_t s = 0;
+      if (head) {
+        rank++;
+        uint32_t cnt = sseg[rank - 1];
+        sf[j] |= cnt << 8;
+        s += varlen(cnt) + varlen(bc[r]) + varlen(bk[r]);
+      }
+      if (sf[j] & 2) s += 1 + varlen(bk[r] - sE[j]);
+      if (sf[j] & 1) s += bm[r] >> 8;
+      ls += s;
+    }
+    uint32_t tot;
+    const uint32_t pre = bscan_sum<NT>(ls, ws, tot);
+    const uint32_t base = varlen(NC);
+    uint32_t pos = base + pre;
+    for (uint32_t j = j0; j < j1; j++) {
+      uint32_t r = sval[j];
+      bool head = j == 0 || bc[sval[j - 1]] != bc[r];
+      uint32_t s = 0;
+      if (head) s += varlen(sf[j] >> 8) + varlen(bc[r]) + varlen(bk[r]);
+      if (sf[j] & 2) s += 1 + varlen(bk[r] - sE[j]);
+      if (sf[j] & 1) s += bm[r] >> 8;
+      sz[j] = pos;
+      pos += s;
+    }
+    blocks_size = base + tot;
+    __syncthreads();
+  }
+  // ---- 6b write the block section into the document's slot
+  uint8_t *out = o.out + slot;
+  if (blocks_size <= cap) {
+    if (t == 0) {
+      Writer w{out, 0};
+      w_var(w, NC);
+    }
+    for (uint32_t j = j0; j < j1; j++) {
+      uint32_t r = sval[j];
+      bool head = j == 0 || bc[sval[j - 1]] != bc[r];
+      Writer w{out, sz[j]};
+      if (head) {
+        w_var(w, sf[j] >> 8);
+        w_var(w, bc[r]);
+        w_var(w, bk[r]);
+      }
+      if (sf[j] & 2) {
+        w.u8(10);
+        w_var(w, bk[r] - sE[j]);
+      }
+      if (sf[j] & 1) {
+        uint32_t p = bp[r] & 0xFFFF, len = bp[r] >> 16;
+        if (bm[r] & 4) {
+          emit_block(in, nbytes, p, bc[r], bk[r], bl[r], 0, w);
+        } else {
+          for (uint32_t q = 0; q < len; q++) w.p[w.n + q] = in[p + q];
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- 5 DeleteSet: distinct clients in yrs' table order, union of ranges
+  uint64_t *dkey = (uint64_t *)(smem + L.dkey);
+  uint32_t *dval = (uint32_t *)(smem + L.dval);
+  const uint32_t RSZ = pow2ceil(caps.r_cap > caps.e_cap ? caps.r_cap : caps.e_cap);
+  uint32_t *d_client = (uint32_t *)(smem + L.dcl), *d_first = (uint32_t *)(smem + L.dfirst),
+           *d_aux = (uint32_t *)(smem + L.dord);
+  // 5a entries: key = (client, upd<<8|tpos) for live entries
+  uint32_t ne2 = pow2ceil(NE ? NE : 1);
+  for (uint32_t j = t; j < ne2; j += NT) {
+    bool live = j < NE && (et[j] & 0x80000000u);
+    dkey[j] = live ? (((uint64_t)ec[j] << 32) | (et[j] & 0x7FFFFFFFu)) : ~0ull;
+    dval[j] = j;
+  }
+  __syncthreads();
+  bitonic<NT>(dkey, dval, ne2);
+  // distinct clients: heads of runs of equal client among live keys
+  uint32_t D;
+  {
+    const uint32_t pe = (NE + NT - 1) / NT, e0 = t * pe, e1 = e0 + pe < NE ? e0 + pe : NE;
+    uint32_t nh = 0;
+    for (uint32_t j = e0; j < e1; j++)
+      if (dkey[j] != ~0ull && (j == 0 || (dkey[j] >> 32) != (dkey[j - 1] >> 32))) nh++;
+    uint32_t pre = bscan_sum<NT>(nh, ws, D);
+    for (uint32_t j = e0; j < e1; j++) {
+      if (dkey[j] != ~0ull && (j == 0 || (dkey[j] >> 32) != (dkey[j - 1] >> 32))) {
+        d_client[pre] = (uint32_t)(dkey[j] >> 32);
+        d_first[pre] = (uint32_t)dkey[j];
+        pre++;
+      }
+    }
+  }
+  __syncthreads();
+  // 5b yrs' table order (IdSet::merge inserts in first-occurrence order, hashbrown layout)
+  if (t == 0) {
+    // insertion order: sort ranks by first occurrence (insertion sort; D is small in practice)
+    uint32_t *ord = d_aux;
+    for (uint32_t i = 0; i < D; i++) {
+      uint32_t x = i, j = i;
+      while (j > 0 && d_first[ord[j - 1]] > d_first[x]) {
+        ord[j] = ord[j - 1];
+        j--;
+      }
+      ord[j] = x;
+    }
+    // emulate the table: slots hold rank+1; reuse dkey (as u32) for slots — dkey is free now
+    uint32_t *slot_arr = (uint32_t *)dkey;
+    uint32_t slot_cap = 2 * RSZ; // u32 capacity of dkey region
+    uint32_t buckets = 0, items = 0, growth = 0;
+    auto ctrl_empty = [&](uint32_t idx) -> bool {
+      if (idx < buckets) return slot_arr[idx] == 0;
+      if (buckets < 16) return idx < 16 ? true : slot_arr[idx - 16] == 0;
+      return slot_arr[idx - buckets] == 0;
+    };
+    auto find_slot = [&](uint32_t key) -> uint32_t {
+      uint32_t mask = buckets - 1, pos = key & mask, stride = 0;
+      for (;;) {
+        for (uint32_t j = 0; j < 16; j++) {
+          if (ctrl_empty(pos + j)) {
+            uint32_t index = (pos + j) & mask;
+            if (slot_arr[index] != 0)
+              for (uint32_t k = 0; k < buckets; k++)
+                if (slot_arr[k] == 0) return k;
+            return index;
+          }
+        }
+        stride += 16;
+        pos = (pos + stride) & mask;
+      }
+    };
+    uint32_t ok = 1;
+    uint32_t *tmp = dval; // resize scratch
+    for (uint32_t i = 0; i < D && ok; i++) {
+      if (growth == 0) {
+        uint64_t full = buckets ? mask_to_cap(buckets - 1) : 0;
+        uint64_t need = items + 1;
+        uint64_t nb = cap_to_buckets(need > full + 1 ? need : full + 1);
+        if (nb > slot_cap / 2) {
+          ok = 0;
+          break;
+        }
+        uint32_t ob = buckets;
+        for (uint32_t q = 0; q < ob; q++) tmp[q] = slot_arr[q];
+        buckets = (uint32_t)nb;
+        for (uint32_t q = 0; q < buckets; q++) slot_arr[q] = 0;
+        for (uint32_t q = 0; q < ob; q++)
+          if (tmp[q]) slot_arr[find_slot(d_client[tmp[q] - 1])] = tmp[q];
+        growth = (uint32_t)mask_to_cap(buckets - 1) - items;
+      }
+      uint32_t rk = ord[i];
+      slot_arr[find_slot(d_client[rk])] = rk + 1;
+      items++;
+      growth--;
+    }
+    // iteration order -> ord (rank list)
+    uint32_t k = 0;
+    for (uint32_t q = 0; q < buckets && ok; q++)
+      if (slot_arr[q]) ord[k++] = slot_arr[q] - 1;
+    sc[1] = ok;
+  }
+  __syncthreads();
+  if (!sc[1]) {
+    if (t == 0) {
+      o.path[d] = 1;
+      o.status[d] = 0;
+      o.out_len[d] = 0;
+      o.out_start[d] = slot;
+    }
+    return;
+  }
+  // 5c ranges of live entries sorted by (client, start)
+  uint32_t nr2 = pow2ceil(NR ? NR : 1);
+  for (uint32_t j = t; j < nr2; j += NT) {
+    bool live = j < NR && (et[ri[j]] & 0x80000000u);
+    dkey[j] = live ? (((uint64_t)ec[ri[j]] << 32) | rs[j]) : ~0ull;
+    dval[j] = j;
+  }
+  __syncthreads();
+  {
+    uint32_t unsorted = 0;
+    for (uint32_t j = t; j + 1 < nr2; j += NT)
+      if (dkey[j] > dkey[j + 1] || (dkey[j] == dkey[j + 1] && dval[j] > dval[j + 1])) unsorted = 1;
+    unsorted = __syncthreads_or(unsorted);
+    if (unsorted) bitonic<NT>(dkey, dval, nr2);
+  }
+  // live count
+  uint32_t NL;
+  {
+    uint32_t c = 0;
+    for (uint32_t j = t; j < NR; j += NT) c += dkey[j] != ~0ull;
+    bscan_sum<NT>(c, ws, NL);
+  }
+  // 5d segmented union over sorted live ranges: comp heads, comp end, comp size at comp tails
+  uint32_t *cmp_end = (uint32_t *)(smem + L.cend);
+  uint32_t *cmp_off = (uint32_t *)(smem + L.coff);
+  uint32_t *cmp_head = (uint32_t *)(smem + L.chead);
+  const uint32_t pr = (NL + NT - 1) / NT, r0 = t * pr, r1 = r0 + pr < NL ? r0 + pr : NL;
+  {
+    uint32_t lf = 0, lv = 0;
+    for (uint32_t j = r0; j < r1; j++) {
+      bool chead = j == 0 || (dkey[j] >> 32) != (dkey[j - 1] >> 32);
+      uint32_t e = re[dval[j]];
+      if (chead) {
+        lf = 1;
+        lv = e;
+      } else
+        lv = OpMax::f(lv, e);
+    }
+    uint32_t pf, pv;
+    bscan_seg<NT, OpMax>(lf, lv, ws, pf, pv);
+    uint32_t run = pv;
+    for (uint32_t j = r0; j < r1; j++) {
+      bool chead = j == 0 || (dkey[j] >> 32) != (dkey[j - 1] >> 32);
+      uint32_t s0 = (uint32_t)dkey[j], e = re[dval[j]];
+      uint32_t h = chead ? 3u : (s0 > run ? 1u : 0u); // bit0 component head, bit1 client head
+      cmp_head[j] = h;
+      run = chead ? e : OpMax::f(run, e);
+      cmp_end[j] = run; // inclusive running max within client
+    }
+  }
+  __syncthreads();
+  // component start propagated to its tail; component size at tails
+  uint32_t ds_comp_total;
+  {
+    uint32_t lf = 0, lv = 0;
+    for (uint32_t j = r0; j < r1; j++) {
+      if (cmp_head[j] & 1) {
+        lf = 1;
+        lv = (uint32_t)dkey[j];
+      }
+    }
+    uint32_t pf, pv;
+    bscan_seg<NT, OpFirst>(lf, lv, ws, pf, pv);
+    uint32_t cs = pv;
+    uint32_t ls = 0;
+    for (uint32_t j = r0; j < r1; j++) {
+      if (cmp_head[j] & 1) cs = (uint32_t)dkey[j];
+      bool tail = j + 1 == NL || (cmp_head[j + 1] & 1);
+      uint32_t s = tail ? varlen(cs) + varlen(cmp_end[j] - cs) : 0;
+      ls += s;
+    }
+    uint32_t pre = bscan_sum<NT>(ls, ws, ds_comp_total);
+    // offsets of component bytes within the concatenation (client order = sorted order)
+    cs = pv;
+    uint32_t pos = pre;
+    for (uint32_t j = r0; j < r1; j++) {
+      if (cmp_head[j] & 1) cs = (uint32_t)dkey[j];
+      bool tail = j + 1 == NL || (cmp_head[j + 1] & 1);
+      uint32_t s = tail ? varlen(cs) + varlen(cmp_end[j] - cs) : 0;
+      cmp_off[j] = pos;
+      pos += s;
+      // stash component start for the writer in the key's low half (no longer needed as key)
+      if (tail) dkey[j] = (dkey[j] & 0xFFFFFFFF00000000ull) | cs;
+    }
+    if (t == 0) cmp_off[NL] = ds_comp_total;
+  }
+  __syncthreads();
+  // 5e per distinct client (rank r, ascending client): range segment, #components, bytes
+  // d_aux[0..D) holds iteration order; compute per-rank [rb, re) by binary search
+  uint32_t *r_beg = (uint32_t *)(smem + L.dbeg);
+  uint32_t *r_ncomp = (uint32_t *)(smem + L.dnc);
+  uint32_t *r_off = (uint32_t *)(smem + L.doff);
+  for (uint32_t r = t; r < D; r += NT) {
+    uint32_t c = d_client[r];
+    uint32_t lo = 0, hi = NL;
+    while (lo < hi) {
+      uint32_t mid = (lo + hi) / 2;
+      if ((uint32_t)(dkey[mid] >> 32) < c) lo = mid + 1;
+      else hi = mid;
+    }
+    uint32_t a = lo;
+    hi = NL;
+    while (lo < hi) {
+      uint32_t mid = (lo + hi) / 2;
+      if ((uint32_t)(dkey[mid] >> 32) <= c) lo = mid + 1;
+      else hi = mid;
+    }
+    uint32_t bnd = lo, nc = 0;
+    for (uint32_t j = a; j < bnd; j++) nc += cmp_head[j] & 1;
+    r_beg[r] = a;
+    r_ncomp[r] = nc;
+    r_off[r] = bnd; // end, temporarily
+  }
+  __syncthreads();
+  // client byte sizes in iteration order -> offsets (single lane; D is small)
+  if (t == 0) {
+    uint32_t pos = varlen(D);
+    for (uint32_t i = 0; i < D; i++) {
+      uint32_t r = d_aux[i];
+      uint32_t a = r_beg[r], bnd = r_off[r];
+      uint32_t bytes = cmp_off[bnd] - cmp_off[a];
+      uint32_t hdr = varlen(d_client[r]) + varlen(r_ncomp[r]);
+      r_off[r] = pos; // header position of client r
+      pos += hdr + bytes;
+    }
+    sc[2] = pos;
+  }
+  __syncthreads();
+  const uint32_t ds_size = sc[2];
+  const uint64_t total = (uint64_t)blocks_size + ds_size;
+  if (total > cap) {
+    if (t == 0) {
+      o.path[d] = 1;
+      o.status[d] = 0;
+      o.out_len[d] = 0;
+      o.out_start[d] = slot;
+    }
+    return;
+  }
+  uint8_t *dso = out + blocks_size;
+  if (t == 0) {
+    Writer w{dso, 0};
+    w_var(w, D);
+  }
+  for (uint32_t r = t; r < D; r += NT) {
+    Writer w{dso, r_off[r]};
+    w_var(w, d_client[r]);
+    w_var(w, r_ncomp[r]);
+  }
+  for (uint32_t j = r0; j < r1; j++) {
+    bool tail = j + 1 == NL || (cmp_head[j + 1] & 1);
+    if (!tail) continue;
+    uint32_t c = (uint32_t)(dkey[j] >> 32);
+    // rank of c (binary search over d_client, ascending)
+    uint32_t lo = 0, hi = D;
+    while (lo < hi) {
+      uint32_t mid = (lo + hi) / 2;
+      if (d_client[mid] < c) lo = mid + 1;
+      else hi = mid;
+    }
+    uint32_t r = lo;
+    uint32_t hdr = varlen(c) + varlen(r_ncomp[r]);
+    Writer w{dso, r_off[r] + hdr + (cmp_off[j] - cmp_off[r_beg[r]])};
+    uint32_t cs = (uint32_t)dkey[j];
+    w_var(w, cs);
+    w_var(w, cmp_end[j] - cs);
+  }
+  if (t == 0) {
+    o.path[d] = 0;
+    o.status[d] = 0;
+    o.out_len[d] = total;
+    o.out_start[d] = slot;
+  }
+}
+
+size_t fast_lds_bytes(const FastCaps &c) { return fast_layout(c).total; }
+
+void launch_fast_merge(const BatchIn &b, const FastCaps &caps, const FastOut &o, int nt, hipStream_t s) {
+  if (!b.n_docs) return;
+  size_t lds = fast_lds_bytes(caps);
+  if (nt == 1024) {
+    hipFuncSetAttribute((const void *)k_fast_merge<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_fast_merge<1024>, dim3(b.n_docs), dim3(1024), lds, s, b, caps, o);
+  } else if (nt == 512) {
+    hipFuncSetAttribute((const void *)k_fast_merge<512>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_fast_merge<512>, dim3(b.n_docs), dim3(512), lds, s, b, caps, o);
+  } else {
+    hipFuncSetAttribute((const void *)k_fast_merge<256>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_fast_merge<256>, dim3(b.n_docs), dim3(256), lds, s, b, caps, o);
+  }
+}
+
+} // namespace ym

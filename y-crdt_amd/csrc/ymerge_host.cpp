@@ -50,10 +50,13 @@ struct ymerge_ctx {
   int device = 0;
   hipStream_t s = nullptr;
   DevBuf in_bytes, in_upd_off, in_doc_upd, in_sv, in_sv_off;
-  DevBuf status, counts, need, scr_off, scratch, sizes, out_off, out, scan_tmp;
+  DevBuf status, path, out_start, out_len, pack_off, counts, need, scr_off, scratch, sizes, spill_off, scan_tmp;
+  DevBuf arena, packed, counter;
   uint64_t *h_pinned = nullptr;
   hipEvent_t ev[6];
   ymerge_stats stats{};
+  ym::FastCaps caps{32768, 2048, 2048, 1024, 1024};
+  int fast_threads = 512;
   std::mutex mu;
 };
 
@@ -66,6 +69,9 @@ static bool ctx_init(ymerge_ctx *c, int device) {
   if (hipHostMalloc((void **)&c->h_pinned, 64 * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess) return false;
   for (auto &e : c->ev)
     if (hipEventCreate(&e) != hipSuccess) return false;
+  // YMERGE_FAST_THREADS: workgroup size of the fast path (256/512/1024); 0 routes every
+  // document through the exact engine (used by the parity tests to cover both engines)
+  if (const char *v = getenv("YMERGE_FAST_THREADS")) c->fast_threads = atoi(v);
   return true;
 }
 
@@ -82,8 +88,9 @@ extern "C" void ymerge_ctx_destroy(ymerge_ctx *c) {
   if (!c) return;
   hipSetDevice(c->device);
   if (c->s) hipStreamSynchronize(c->s);
-  for (DevBuf *b : {&c->in_bytes, &c->in_upd_off, &c->in_doc_upd, &c->in_sv, &c->in_sv_off, &c->status, &c->counts,
-                    &c->need, &c->scr_off, &c->scratch, &c->sizes, &c->out_off, &c->out, &c->scan_tmp})
+  for (DevBuf *b : {&c->in_bytes, &c->in_upd_off, &c->in_doc_upd, &c->in_sv, &c->in_sv_off, &c->status, &c->path,
+                    &c->out_start, &c->out_len, &c->pack_off, &c->counts, &c->need, &c->scr_off, &c->scratch,
+                    &c->sizes, &c->spill_off, &c->scan_tmp, &c->arena, &c->packed, &c->counter})
     b->release();
   if (c->h_pinned) hipHostFree(c->h_pinned);
   for (auto &e : c->ev)
@@ -92,72 +99,112 @@ extern "C" void ymerge_ctx_destroy(ymerge_ctx *c) {
   delete c;
 }
 
-static bool read_u64(ymerge_ctx *c, const uint64_t *d_src, uint64_t &v) {
-  if (hipMemcpyAsync(c->h_pinned, d_src, sizeof(uint64_t), hipMemcpyDeviceToHost, c->s) != hipSuccess) return false;
+static bool read_words(ymerge_ctx *c, const void *d_src, size_t bytes, uint64_t *dst) {
+  if (hipMemcpyAsync(c->h_pinned, d_src, bytes, hipMemcpyDeviceToHost, c->s) != hipSuccess) return false;
   if (hipStreamSynchronize(c->s) != hipSuccess) return false;
-  v = c->h_pinned[0];
+  memcpy(dst, c->h_pinned, bytes);
   return true;
 }
 
-static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, const uint64_t *d_upd_off, const uint64_t *d_doc_upd,
-                        uint64_t n_docs, ymerge_device_result *res) {
+// grow `b` to `bytes` keeping its first `keep` bytes (device-to-device copy)
+static bool ensure_keep(ymerge_ctx *c, DevBuf &b, size_t bytes, size_t keep) {
+  if (bytes <= b.cap && b.p) return true;
+  DevBuf nb;
+  if (!nb.ensure(bytes)) return false;
+  if (keep && b.p && hipMemcpyAsync(nb.p, b.p, keep, hipMemcpyDeviceToDevice, c->s) != hipSuccess) return false;
+  if (hipStreamSynchronize(c->s) != hipSuccess) return false;
+  b.release();
+  b = nb;
+  return true;
+}
+
+// One batch: fast path for every document, exact engine for the documents it hands over.
+static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes, const uint64_t *d_upd_off,
+                        const uint64_t *d_doc_upd, uint64_t n_docs, ymerge_device_result *res) {
   if (hipSetDevice(c->device) != hipSuccess) return YMERGE_ERR_DEVICE;
   if (n_docs > 0xFFFFFFFFull) return YMERGE_ERR_OTHER;
-  uint32_t n = (uint32_t)n_docs;
+  const uint32_t n = (uint32_t)n_docs;
   ym::BatchIn b{d_bytes, d_upd_off, d_doc_upd, n};
-  size_t nn = (size_t)n + 1;
-  if (!c->status.ensure(nn) || !c->counts.ensure(4 * nn * 4) || !c->need.ensure(nn * 8) ||
-      !c->scr_off.ensure(nn * 8) || !c->sizes.ensure(nn * 8) || !c->out_off.ensure(nn * 8) ||
-      !c->scan_tmp.ensure(ym::scan_tmp_elems(n) * 8 + 64))
+  const size_t nn = (size_t)n + 1;
+  const uint64_t slots = 2 * n_bytes + 64 * (uint64_t)n_docs;
+  if (!c->status.ensure(nn) || !c->path.ensure(nn) || !c->out_start.ensure(nn * 8) || !c->out_len.ensure(nn * 8) ||
+      !c->pack_off.ensure(nn * 8) || !c->counts.ensure(4 * nn * 4) || !c->need.ensure(nn * 8) ||
+      !c->scr_off.ensure(nn * 8) || !c->sizes.ensure(nn * 8) || !c->spill_off.ensure(nn * 8) ||
+      !c->scan_tmp.ensure(ym::scan_tmp_elems(n) * 8 + 64) || !c->counter.ensure(64) ||
+      !ensure_keep(c, c->arena, slots + slots / 8 + 4096, 0))
     return YMERGE_ERR_DEVICE;
+  uint8_t *arena = c->arena.as<uint8_t>();
+  uint64_t *ostart = c->out_start.as<uint64_t>(), *olen = c->out_len.as<uint64_t>();
+  uint8_t *status = c->status.as<uint8_t>(), *path = c->path.as<uint8_t>();
+  hipMemsetAsync(c->counter.p, 0, 64, c->s);
   hipEventRecord(c->ev[0], c->s);
-  ym::launch_seq_count(b, c->status.as<uint8_t>(), c->counts.as<uint32_t>(), c->need.as<uint64_t>(), c->s);
-  ym::launch_scan_u64(c->need.as<uint64_t>(), c->scr_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
+  ym::FastOut fo{arena, ostart, olen, status, path};
+  if (c->fast_threads)
+    ym::launch_fast_merge(b, c->caps, fo, c->fast_threads, c->s);
+  else
+    hipMemsetAsync(path, 1, n, c->s);
   hipEventRecord(c->ev[1], c->s);
-  uint64_t words = 0;
-  if (!read_u64(c, c->scr_off.as<uint64_t>() + n, words)) return YMERGE_ERR_DEVICE;
-  if (!c->scratch.ensure((size_t)words * 4 + 64)) return YMERGE_ERR_DEVICE;
-  hipEventRecord(c->ev[2], c->s);
-  ym::launch_seq_merge(false, b, c->status.as<uint8_t>(), c->counts.as<uint32_t>(), c->scr_off.as<uint64_t>(),
-                       c->scratch.as<uint32_t>(), c->sizes.as<uint64_t>(), nullptr, nullptr, c->status.as<uint8_t>(),
+  // exact engine for documents the fast path handed over (path == 1)
+  ym::launch_seq_count(b, path, status, c->counts.as<uint32_t>(), c->need.as<uint64_t>(), c->counter.as<uint32_t>(),
                        c->s);
-  ym::launch_scan_u64(c->sizes.as<uint64_t>(), c->out_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
+  ym::launch_scan_u64(c->need.as<uint64_t>(), c->scr_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
+  hipMemcpyAsync(c->h_pinned + 8, c->scr_off.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, c->s);
+  hipMemcpyAsync(c->h_pinned + 9, c->counter.p, 4, hipMemcpyDeviceToHost, c->s);
+  if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
+  const uint64_t words = c->h_pinned[8];
+  const uint32_t n_exact = (uint32_t)(c->h_pinned[9] & 0xFFFFFFFFu);
+  if (n_exact) {
+    if (!c->scratch.ensure((size_t)words * 4 + 64)) return YMERGE_ERR_DEVICE;
+    ym::launch_seq_merge(false, b, path, status, c->counts.as<uint32_t>(), c->scr_off.as<uint64_t>(),
+                         c->scratch.as<uint32_t>(), c->sizes.as<uint64_t>(), nullptr, nullptr, 0, nullptr, nullptr,
+                         status, c->s);
+    ym::launch_scan_u64(c->sizes.as<uint64_t>(), c->spill_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
+    uint64_t spill = 0;
+    if (!read_words(c, c->spill_off.as<uint64_t>() + n, 8, &spill)) return YMERGE_ERR_DEVICE;
+    if (!ensure_keep(c, c->arena, slots + spill + 4096, slots)) return YMERGE_ERR_DEVICE;
+    arena = c->arena.as<uint8_t>();
+    ym::launch_seq_merge(true, b, path, status, c->counts.as<uint32_t>(), c->scr_off.as<uint64_t>(),
+                         c->scratch.as<uint32_t>(), nullptr, c->spill_off.as<uint64_t>(), arena, slots, ostart, olen,
+                         nullptr, c->s);
+  }
+  hipEventRecord(c->ev[2], c->s);
+  // total output bytes (and packed offsets for host copies)
+  ym::launch_scan_u64(olen, c->pack_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
   hipEventRecord(c->ev[3], c->s);
   uint64_t total = 0;
-  if (!read_u64(c, c->out_off.as<uint64_t>() + n, total)) return YMERGE_ERR_DEVICE;
-  if (!c->out.ensure((size_t)total + 64)) return YMERGE_ERR_DEVICE;
-  hipEventRecord(c->ev[4], c->s);
-  ym::launch_seq_merge(true, b, c->status.as<uint8_t>(), c->counts.as<uint32_t>(), c->scr_off.as<uint64_t>(),
-                       c->scratch.as<uint32_t>(), nullptr, c->out_off.as<uint64_t>(), c->out.as<uint8_t>(), nullptr,
-                       c->s);
-  hipEventRecord(c->ev[5], c->s);
-  if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
+  if (!read_words(c, c->pack_off.as<uint64_t>() + n, 8, &total)) return YMERGE_ERR_DEVICE;
   if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
-  float t01 = 0, t23 = 0, t45 = 0, t05 = 0;
+  float t01 = 0, t12 = 0, t23 = 0, t03 = 0;
   hipEventElapsedTime(&t01, c->ev[0], c->ev[1]);
+  hipEventElapsedTime(&t12, c->ev[1], c->ev[2]);
   hipEventElapsedTime(&t23, c->ev[2], c->ev[3]);
-  hipEventElapsedTime(&t45, c->ev[4], c->ev[5]);
-  hipEventElapsedTime(&t05, c->ev[0], c->ev[5]);
+  hipEventElapsedTime(&t03, c->ev[0], c->ev[3]);
   c->stats = ymerge_stats{};
   c->stats.n_docs = n_docs;
+  c->stats.bytes_in = n_bytes;
   c->stats.bytes_out = total;
-  c->stats.docs_exact = n_docs;
-  c->stats.ms_count = t01;
-  c->stats.ms_plan = t23;
-  c->stats.ms_write = t45;
-  c->stats.ms_total = t05;
-  res->d_out = c->out.as<uint8_t>();
-  res->d_out_off = c->out_off.as<uint64_t>();
-  res->d_status = c->status.as<uint8_t>();
+  c->stats.docs_exact = n_exact;
+  c->stats.docs_fast = n_docs - n_exact;
+  c->stats.ms_fast = t01;
+  c->stats.ms_exact = t12;
+  c->stats.ms_tail = t23;
+  c->stats.ms_total = t03;
+  res->d_out = arena;
+  res->d_out_start = ostart;
+  res->d_out_len = olen;
+  res->d_status = status;
+  res->arena_bytes = c->arena.cap;
   res->out_bytes = total;
   return 0;
 }
 
-extern "C" int ymerge_updates_v1_batch_device(ymerge_ctx *c, const uint8_t *d_bytes, const uint64_t *d_upd_off,
-                                              const uint64_t *d_doc_upd, uint64_t n_docs, ymerge_device_result *res) {
+extern "C" int ymerge_updates_v1_batch_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
+                                              const uint64_t *d_upd_off, uint64_t n_updates, const uint64_t *d_doc_upd,
+                                              uint64_t n_docs, ymerge_device_result *res) {
   if (!c || !res) return YMERGE_ERR_OTHER;
+  (void)n_updates;
   std::lock_guard<std::mutex> g(c->mu);
-  return merge_device(c, d_bytes, d_upd_off, d_doc_upd, n_docs, res);
+  return merge_device(c, d_bytes, n_bytes, d_upd_off, d_doc_upd, n_docs, res);
 }
 
 extern "C" int yencode_state_vector_from_update_v1_batch_device(ymerge_ctx *, const uint8_t *, const uint64_t *,
@@ -169,20 +216,28 @@ extern "C" int ydiff_updates_v1_batch_device(ymerge_ctx *, const uint8_t *, cons
   return YMERGE_ERR_UNSUPPORTED;
 }
 
+static int pack_to_host(ymerge_ctx *c, const ymerge_device_result *res, uint64_t n_docs, uint8_t *out,
+                        uint64_t *out_off, uint8_t *status) {
+  const uint32_t n = (uint32_t)n_docs;
+  if (!c->packed.ensure(res->out_bytes + 64)) return YMERGE_ERR_DEVICE;
+  ym::launch_pack(res->d_out, res->d_out_start, res->d_out_len, c->pack_off.as<uint64_t>(),
+                  c->packed.as<uint8_t>(), n, c->s);
+  if (out && res->out_bytes &&
+      hipMemcpyAsync(out, c->packed.p, res->out_bytes, hipMemcpyDeviceToHost, c->s) != hipSuccess)
+    return YMERGE_ERR_DEVICE;
+  if (out_off && hipMemcpyAsync(out_off, c->pack_off.p, (n_docs + 1) * 8, hipMemcpyDeviceToHost, c->s) != hipSuccess)
+    return YMERGE_ERR_DEVICE;
+  if (status && n_docs && hipMemcpyAsync(status, res->d_status, n_docs, hipMemcpyDeviceToHost, c->s) != hipSuccess)
+    return YMERGE_ERR_DEVICE;
+  return hipStreamSynchronize(c->s) == hipSuccess ? 0 : YMERGE_ERR_DEVICE;
+}
+
 extern "C" int ymerge_result_to_host(ymerge_ctx *c, const ymerge_device_result *res, uint64_t n_docs, uint8_t *out,
                                      uint64_t *out_off, uint8_t *status) {
   if (!c || !res) return YMERGE_ERR_OTHER;
   std::lock_guard<std::mutex> g(c->mu);
   hipSetDevice(c->device);
-  if (out && res->out_bytes &&
-      hipMemcpyAsync(out, res->d_out, res->out_bytes, hipMemcpyDeviceToHost, c->s) != hipSuccess)
-    return YMERGE_ERR_DEVICE;
-  if (out_off &&
-      hipMemcpyAsync(out_off, res->d_out_off, (n_docs + 1) * 8, hipMemcpyDeviceToHost, c->s) != hipSuccess)
-    return YMERGE_ERR_DEVICE;
-  if (status && n_docs && hipMemcpyAsync(status, res->d_status, n_docs, hipMemcpyDeviceToHost, c->s) != hipSuccess)
-    return YMERGE_ERR_DEVICE;
-  return hipStreamSynchronize(c->s) == hipSuccess ? 0 : YMERGE_ERR_DEVICE;
+  return pack_to_host(c, res, n_docs, out, out_off, status);
 }
 
 extern "C" void ymerge_last_stats(ymerge_ctx *c, ymerge_stats *st) {
@@ -205,8 +260,8 @@ extern "C" int ymerge_updates_v1_batch(ymerge_ctx *c, const uint8_t *bytes, cons
       hipMemcpyAsync(c->in_doc_upd.p, doc_upd, (n_docs + 1) * 8, hipMemcpyHostToDevice, c->s) != hipSuccess)
     return YMERGE_ERR_DEVICE;
   ymerge_device_result dr{};
-  int st = merge_device(c, c->in_bytes.as<uint8_t>(), c->in_upd_off.as<uint64_t>(), c->in_doc_upd.as<uint64_t>(),
-                        n_docs, &dr);
+  int st = merge_device(c, c->in_bytes.as<uint8_t>(), nbytes, c->in_upd_off.as<uint64_t>(),
+                        c->in_doc_upd.as<uint64_t>(), n_docs, &dr);
   if (st) return st;
   auto *r = (ymerge_batch_result *)calloc(1, sizeof(ymerge_batch_result));
   r->n_docs = n_docs;
@@ -214,12 +269,10 @@ extern "C" int ymerge_updates_v1_batch(ymerge_ctx *c, const uint8_t *bytes, cons
   r->out = (uint8_t *)malloc(dr.out_bytes + 1);
   r->out_off = (uint64_t *)malloc((n_docs + 1) * 8);
   r->status = (uint8_t *)malloc(n_docs + 1);
-  hipMemcpyAsync(r->out, dr.d_out, dr.out_bytes, hipMemcpyDeviceToHost, c->s);
-  hipMemcpyAsync(r->out_off, dr.d_out_off, (n_docs + 1) * 8, hipMemcpyDeviceToHost, c->s);
-  hipMemcpyAsync(r->status, dr.d_status, n_docs, hipMemcpyDeviceToHost, c->s);
-  if (hipStreamSynchronize(c->s) != hipSuccess) {
+  st = pack_to_host(c, &dr, n_docs, r->out, r->out_off, r->status);
+  if (st) {
     ymerge_batch_result_destroy(r);
-    return YMERGE_ERR_DEVICE;
+    return st;
   }
   *out = r;
   return 0;

@@ -8,101 +8,10 @@
 //   output size, WRITE=true writes at out_off[d].
 #include "ycodec.h"
 #include "yseq.h"
+#include "ywalk.h"
 #include "ykernels.h"
 
 namespace ym {
-
-// ------------------------------------------------------------------ update walk
-// Sink interface: on_section, on_block, on_ds_entry, on_ds_range, on_ds_done.
-struct TrackClients {
-  uint32_t client[8], count[8];
-  uint32_t n;
-  __device__ void reset() { n = 0; }
-  // returns blocks already recorded for `client` in this update (exact for <= 8 clients)
-  __device__ uint32_t *slot(uint32_t c) {
-    for (uint32_t i = 0; i < n; i++)
-      if (client[i] == c) return &count[i];
-    if (n < 8) {
-      client[n] = c;
-      count[n] = 0;
-      return &count[n++];
-    }
-    return nullptr;
-  }
-};
-
-template <class S> __device__ int walk_update(const uint8_t *p, uint32_t n, S &s) {
-  Cur c{p, n, 0};
-  bool cn;
-  uint32_t ncl;
-  YM_TRY(rd_var_u32(c, ncl, cn));
-  if (ncl && cap_to_buckets(ncl) * 41ull > ALLOC_LIMIT) return E_NEM; // try_reserve, (u64, VecDeque) = 40 B
-  TrackClients tc;
-  tc.reset();
-  for (uint32_t i = 0; i < ncl; i++) {
-    uint32_t nb, client, clock;
-    YM_TRY(rd_var_u32(c, nb, cn));
-    YM_TRY(rd_var_u32(c, client, cn));
-    YM_TRY(rd_var_u32(c, clock, cn));
-    uint32_t *cnt = tc.slot(client);
-    uint64_t existing = cnt ? *cnt : 0;
-    if ((existing + nb) * 32ull > ALLOC_LIMIT) return E_NEM; // VecDeque<BlockCarrier>::try_reserve
-    s.on_section(client);
-    for (uint32_t j = 0; j < nb; j++) {
-      uint32_t bpos = c.i;
-      BlockInfo bi;
-      YM_TRY(parse_block(c, bi));
-      if (bi.kind == BK_ITEM && bi.len == 0) continue; // Item::new -> None
-      if ((uint64_t)clock + bi.len > 0xFFFFFFFFull) return E_PANIC;
-      YM_TRY(s.on_block(client, clock, bi, bpos, c.i - bpos));
-      if (cnt) (*cnt)++;
-      clock += bi.len;
-    }
-  }
-  uint32_t nds;
-  YM_TRY(rd_var_u32(c, nds, cn));
-  YM_TRY(s.on_ds_begin(nds));
-  for (uint32_t i = 0; i < nds; i++) {
-    uint32_t client, nr;
-    YM_TRY(rd_var_u32(c, client, cn));
-    YM_TRY(rd_var_u32(c, nr, cn));
-    YM_TRY(s.on_ds_entry(client, nr));
-    for (uint32_t k = 0; k < nr; k++) {
-      uint32_t st, ln;
-      YM_TRY(rd_var_u32(c, st, cn));
-      YM_TRY(rd_var_u32(c, ln, cn));
-      if ((uint64_t)st + ln > 0xFFFFFFFFull) return E_PANIC;
-      s.on_ds_range(st, st + ln);
-    }
-  }
-  return s.on_ds_done();
-}
-
-// DS table order of one update: HashMap::insert per entry in stream order
-struct DsOrder {
-  SmallHB<64> hb;
-  uint32_t n;
-  __device__ void begin() {
-    hb.init_empty();
-    n = 0;
-  }
-  // returns local index of a replaced (now dead) entry, ~0u if none; <0 error
-  __device__ int insert(uint32_t client, uint32_t &dead) {
-    if (n >= 64) return E_UNSUPPORTED; // device limit: <= 64 DeleteSet entries per update
-    bool existed;
-    int e = hb.insert(client, n, existed);
-    if (e == -2) return E_UNSUPPORTED;
-    dead = ~0u;
-    if (existed) {
-      dead = (uint32_t)e;
-      for (uint32_t i = 0; i < hb.buckets; i++)
-        if (hb.slot[i] == e + 1) hb.slot[i] = (uint16_t)(n + 1);
-      hb.keys[n] = client;
-    }
-    n++;
-    return 0;
-  }
-};
 
 struct CountSink {
   uint32_t NB = 0, NBALL = 0, NE = 0, NR = 0;
@@ -128,9 +37,15 @@ struct CountSink {
   __device__ int on_ds_done() { return 0; }
 };
 
-__global__ void k_seq_count(BatchIn b, uint8_t *status, uint32_t *counts, uint64_t *need_words) {
+__global__ void k_seq_count(BatchIn b, const uint8_t *path, uint8_t *status, uint32_t *counts,
+                            uint64_t *need_words, uint32_t *n_exact) {
   uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= b.n_docs) return;
+  if (path && path[d] != 1) {
+    need_words[d] = 0;
+    return;
+  }
+  if (path) atomicAdd(n_exact, 1u);
   uint64_t u0 = b.doc_upd[d], u1 = b.doc_upd[d + 1];
   CountSink s;
   int st = 0;
@@ -660,13 +575,22 @@ __device__ int seq_fill(SeqCtx &x, const BatchIn &b, uint64_t u0) {
 }
 
 template <bool WRITE>
-__global__ void k_seq_merge(BatchIn b, const uint8_t *status, const uint32_t *counts, const uint64_t *scr_off,
-                            uint32_t *scratch, uint64_t *sizes, const uint64_t *out_off, uint8_t *out,
+__global__ void k_seq_merge(BatchIn b, const uint8_t *path, const uint8_t *status, const uint32_t *counts,
+                            const uint64_t *scr_off, uint32_t *scratch, uint64_t *sizes, const uint64_t *out_off,
+                            uint8_t *out, uint64_t out_base, uint64_t *out_start, uint64_t *out_len,
                             uint8_t *status_out) {
   uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= b.n_docs) return;
+  if (path && path[d] != 1) {
+    if (!WRITE) sizes[d] = 0;
+    return;
+  }
   if (status[d]) {
     if (!WRITE) sizes[d] = 0;
+    if (WRITE && out_len) {
+      out_len[d] = 0;
+      out_start[d] = out_base + out_off[d];
+    }
     return;
   }
   SeqCtx x;
@@ -682,9 +606,13 @@ __global__ void k_seq_merge(BatchIn b, const uint8_t *status, const uint32_t *co
   int err = seq_fill(x, b, u0);
   if (!err) err = seq_merge_blocks(x);
   if (WRITE) {
-    Writer w{out + out_off[d], 0};
+    Writer w{out + out_base + out_off[d], 0};
     if (!err) err = seq_encode_blocks(x, w);
     if (!err) err = seq_encode_ds(x, w);
+    if (out_len) {
+      out_start[d] = out_base + out_off[d];
+      out_len[d] = w.n;
+    }
   } else {
     Counter c;
     if (!err) err = seq_encode_blocks(x, c);
@@ -698,20 +626,22 @@ __global__ void k_seq_merge(BatchIn b, const uint8_t *status, const uint32_t *co
 
 // ------------------------------------------------------------------ launchers
 namespace ym {
-void launch_seq_count(const BatchIn &b, uint8_t *status, uint32_t *counts, uint64_t *need, hipStream_t s) {
+void launch_seq_count(const BatchIn &b, const uint8_t *path, uint8_t *status, uint32_t *counts, uint64_t *need,
+                      uint32_t *n_exact, hipStream_t s) {
   uint32_t nb = (b.n_docs + 63) / 64;
-  if (nb) hipLaunchKernelGGL(k_seq_count, dim3(nb), dim3(64), 0, s, b, status, counts, need);
+  if (nb) hipLaunchKernelGGL(k_seq_count, dim3(nb), dim3(64), 0, s, b, path, status, counts, need, n_exact);
 }
-void launch_seq_merge(bool write, const BatchIn &b, const uint8_t *status, const uint32_t *counts,
+void launch_seq_merge(bool write, const BatchIn &b, const uint8_t *path, const uint8_t *status, const uint32_t *counts,
                       const uint64_t *scr_off, uint32_t *scratch, uint64_t *sizes, const uint64_t *out_off,
-                      uint8_t *out, uint8_t *status_out, hipStream_t s) {
+                      uint8_t *out, uint64_t out_base, uint64_t *out_start, uint64_t *out_len, uint8_t *status_out,
+                      hipStream_t s) {
   uint32_t nb = (b.n_docs + 63) / 64;
   if (!nb) return;
   if (write)
-    hipLaunchKernelGGL(k_seq_merge<true>, dim3(nb), dim3(64), 0, s, b, status, counts, scr_off, scratch, sizes,
-                       out_off, out, status_out);
+    hipLaunchKernelGGL(k_seq_merge<true>, dim3(nb), dim3(64), 0, s, b, path, status, counts, scr_off, scratch, sizes,
+                       out_off, out, out_base, out_start, out_len, status_out);
   else
-    hipLaunchKernelGGL(k_seq_merge<false>, dim3(nb), dim3(64), 0, s, b, status, counts, scr_off, scratch, sizes,
-                       out_off, out, status_out);
+    hipLaunchKernelGGL(k_seq_merge<false>, dim3(nb), dim3(64), 0, s, b, path, status, counts, scr_off, scratch,
+                       sizes, out_off, out, out_base, out_start, out_len, status_out);
 }
 } // namespace ym

@@ -83,3 +83,22 @@ void launch_scan_u64(const uint64_t *in, uint64_t *out, uint32_t n, uint64_t *tm
   hipLaunchKernelGGL(k_scan_final, dim3(ntiles), dim3(SCAN_NT), 0, s, in, n, tmp, out);
 }
 } // namespace ym
+
+namespace ym {
+// pack per-document outputs (start, len) into a contiguous arena at pack_off[d]
+__global__ void __launch_bounds__(256) k_pack(const uint8_t *src, const uint64_t *start, const uint64_t *len,
+                                             const uint64_t *pack_off, uint8_t *dst, uint32_t n_docs) {
+  for (uint32_t d = blockIdx.x; d < n_docs; d += gridDim.x) {
+    const uint8_t *s = src + start[d];
+    uint8_t *o = dst + pack_off[d];
+    uint64_t n = len[d];
+    for (uint64_t i = threadIdx.x; i < n; i += 256) o[i] = s[i];
+  }
+}
+void launch_pack(const uint8_t *src, const uint64_t *start, const uint64_t *len, const uint64_t *pack_off,
+                 uint8_t *dst, uint32_t n_docs, hipStream_t s) {
+  if (!n_docs) return;
+  uint32_t g = n_docs < 8192 ? n_docs : 8192;
+  hipLaunchKernelGGL(k_pack, dim3(g), dim3(256), 0, s, src, start, len, pack_off, dst, n_docs);
+}
+} // namespace ym

@@ -34,13 +34,13 @@ class DeviceError(RuntimeError):
 class _Stats(ctypes.Structure):
     _fields_ = [("n_docs", ctypes.c_uint64), ("bytes_in", ctypes.c_uint64), ("bytes_out", ctypes.c_uint64),
                 ("docs_fast", ctypes.c_uint64), ("docs_exact", ctypes.c_uint64), ("docs_error", ctypes.c_uint64),
-                ("ms_total", ctypes.c_float), ("ms_plan", ctypes.c_float), ("ms_write", ctypes.c_float),
-                ("ms_count", ctypes.c_float)]
+                ("ms_total", ctypes.c_float), ("ms_fast", ctypes.c_float), ("ms_exact", ctypes.c_float),
+                ("ms_tail", ctypes.c_float)]
 
 
 class _DevRes(ctypes.Structure):
-    _fields_ = [("d_out", ctypes.c_void_p), ("d_out_off", ctypes.c_void_p), ("d_status", ctypes.c_void_p),
-                ("out_bytes", ctypes.c_uint64)]
+    _fields_ = [("d_out", ctypes.c_void_p), ("d_out_start", ctypes.c_void_p), ("d_out_len", ctypes.c_void_p),
+                ("d_status", ctypes.c_void_p), ("arena_bytes", ctypes.c_uint64), ("out_bytes", ctypes.c_uint64)]
 
 
 _lib = None
@@ -62,7 +62,7 @@ def lib():
     L.ymerge_ctx_create.restype = vp
     L.ymerge_ctx_create.argtypes = [c.c_int]
     L.ymerge_ctx_destroy.argtypes = [vp]
-    L.ymerge_updates_v1_batch_device.argtypes = [vp, vp, vp, vp, u64, c.POINTER(_DevRes)]
+    L.ymerge_updates_v1_batch_device.argtypes = [vp, vp, u64, vp, u64, vp, u64, c.POINTER(_DevRes)]
     L.ydiff_updates_v1_batch_device.argtypes = [vp, vp, vp, vp, vp, u64, c.POINTER(_DevRes)]
     L.yencode_state_vector_from_update_v1_batch_device.argtypes = [vp, vp, vp, u64, c.POINTER(_DevRes)]
     L.ymerge_result_to_host.argtypes = [vp, c.POINTER(_DevRes), u64, vp, vp, vp]
@@ -153,11 +153,11 @@ class Engine:
         except Exception:
             pass
 
-    def merge_device(self, d_bytes, d_upd_off, d_doc_upd, n_docs):
+    def merge_device(self, d_bytes, n_bytes, d_upd_off, n_updates, d_doc_upd, n_docs):
         """Inputs are device pointers (ints) into HBM; returns a DeviceResult."""
         res = _DevRes()
-        rc = lib().ymerge_updates_v1_batch_device(self._ctx, d_bytes, d_upd_off, d_doc_upd, n_docs,
-                                                  ctypes.byref(res))
+        rc = lib().ymerge_updates_v1_batch_device(self._ctx, d_bytes, n_bytes, d_upd_off, n_updates, d_doc_upd,
+                                                  n_docs, ctypes.byref(res))
         if rc:
             raise DeviceError(f"merge batch failed ({rc})")
         return DeviceResult(self, res, n_docs)
@@ -191,5 +191,6 @@ class Engine:
         t_u = torch.from_numpy(np.ascontiguousarray(upd_off, dtype=np.uint64).view(np.int64)).to(dev)
         t_d = torch.from_numpy(np.ascontiguousarray(doc_upd, dtype=np.uint64).view(np.int64)).to(dev)
         torch.cuda.synchronize(dev)
-        r = self.merge_device(t_b.data_ptr(), t_u.data_ptr(), t_d.data_ptr(), len(doc_upd) - 1)
+        r = self.merge_device(t_b.data_ptr(), int(upd_off[-1]), t_u.data_ptr(), len(upd_off) - 1, t_d.data_ptr(),
+                              len(doc_upd) - 1)
         return r.to_host()
