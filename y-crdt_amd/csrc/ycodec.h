@@ -532,6 +532,7 @@ struct BlockInfo {
   uint8_t kind, ref, info;
   bool reenc;       // canonical re-encoding differs from the input bytes
   bool unsupported; // Embed / Format
+  bool enc_panic;   // yrs panics when it re-encodes this block (String split off a char boundary)
   uint32_t len;     // clock length (0 => dropped Item)
   uint32_t canon;   // canonical encoded size (valid after measure)
 };
@@ -594,6 +595,7 @@ __device__ int parse_block(Cur &c, BlockInfo &bi) {
   bi.info = info;
   bi.reenc = false;
   bi.unsupported = false;
+  bi.enc_panic = false;
   if (info == 10 || info == 0) {
     bi.kind = info == 10 ? BK_SKIP : BK_GC;
     bi.ref = 0;
@@ -660,12 +662,19 @@ __device__ int parse_block(Cur &c, BlockInfo &bi) {
     return 0;
   }
   case 3: YM_TRY(rd_var_u32(c, v, cn)); bi.reenc |= !cn; YM_TRY(rd_skip(c, v)); bi.len = 1; return 0;
-  case 4:
+  case 4: {
     YM_TRY(rd_var_u32(c, v, cn));
     bi.reenc |= !cn;
     YM_TRY(rd_skip(c, v));
-    bi.len = str_len16(c.p + c.i - v, v);
+    const uint8_t *s = c.p + c.i - v;
+    bi.len = str_len16(s, v);
+    if (bi.len > 1) { // encode_slice splits at len UTF-16 units (block.rs:1718-1729)
+      uint32_t bo;
+      if (str_split16(s, v, bi.len, bo)) bi.enc_panic = true;
+      else if (bo != v) bi.reenc = true;
+    }
     return 0;
+  }
   case 5:
     YM_TRY(rd_var_u32(c, v, cn));
     YM_TRY(rd_skip(c, v));

@@ -240,7 +240,7 @@ struct FastFill {
     if (bi.kind == BK_SKIP) return 0;
     uint32_t pos = ubase + bpos;
     uint32_t canon = blen;
-    if (bi.reenc) {
+    if (bi.reenc && !bi.enc_panic) {
       Counter cn;
       emit_block(doc, doc_len, pos, client, clock, bi.len, 0, cn);
       canon = (uint32_t)cn.n;
@@ -249,7 +249,7 @@ struct FastFill {
     bk[nb] = clock;
     bl[nb] = bi.len;
     bp[nb] = pos | (blen << 16);
-    bm[nb] = (uint32_t)bi.kind | (bi.reenc ? 4u : 0u) | (canon << 8);
+    bm[nb] = (uint32_t)bi.kind | (bi.reenc ? 4u : 0u) | (bi.enc_panic ? 8u : 0u) | (canon << 8);
     nb++;
     return 0;
   }
@@ -524,6 +524,22 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
       if (t == 0) {
         o.path[d] = 1;
         o.status[d] = 0;
+        o.out_len[d] = 0;
+        o.out_start[d] = slot;
+      }
+      return;
+    }
+  }
+  // yrs panics while encoding a kept String block that is not valid UTF-8
+  {
+    uint32_t pan = 0;
+    for (uint32_t j = j0; j < j1; j++)
+      if ((sf[j] & 1) && (bm[sval[j]] & 8)) pan = 1;
+    pan = __syncthreads_or(pan);
+    if (pan) {
+      if (t == 0) {
+        o.path[d] = 0;
+        o.status[d] = E_PANIC;
         o.out_len[d] = 0;
         o.out_start[d] = slot;
       }
