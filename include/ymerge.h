@@ -97,6 +97,8 @@ int ydiff_updates_v1_batch_device(ymerge_ctx *ctx, const uint8_t *d_bytes, const
 int ymerge_result_to_host(ymerge_ctx *ctx, const ymerge_device_result *res, uint64_t n_docs, uint8_t *out,
                           uint64_t *out_off, uint8_t *status);
 void ymerge_last_stats(ymerge_ctx *ctx, ymerge_stats *stats);
+/* diagnostic builds (env YMERGE_STAMPS=1): per-document s_memtime phase stamps, 16 per doc */
+int ymerge_debug_stamps(ymerge_ctx *ctx, uint64_t n_docs, uint64_t *dst);
 
 /* ---------------------------------------------------------------- batched, host memory */
 typedef struct {

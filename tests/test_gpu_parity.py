@@ -158,3 +158,66 @@ def test_fast_path_coverage(engine, oracle):
 def test_c1_automerge_trace(engine, oracle):
     b, _ = workloads.trace_updates()
     check_batch(engine, oracle, b, mode=1)
+
+
+def _var(x):
+    out = bytearray()
+    while True:
+        b, x = x & 0x7F, x >> 7
+        if x:
+            out.append(b | 0x80)
+        else:
+            out.append(b)
+            return bytes(out)
+
+
+def _ds_update(entries):
+    """A v1 update with no blocks and the given DeleteSet [(client, [(start, len)])]."""
+    b = bytearray(_var(0)) + _var(len(entries))
+    for c, rs in entries:
+        b += _var(c) + _var(len(rs))
+        for s, n in rs:
+            b += _var(s) + _var(n)
+    return bytes(b)
+
+
+def ds_heavy_docs(seed):
+    """Documents whose updates carry many DeleteSet entries (around the 14-entry
+    in-register table and the former 64-entry limit), with repeated clients inside
+    one update (HashMap::insert replacement, id_set.rs decode)."""
+    rng = np.random.default_rng(seed)
+    docs = []
+    for n_ent in (2, 3, 13, 14, 15, 40, 56, 57, 64, 65, 120, 300):
+        for rep in range(3):
+            ups = []
+            for _ in range(4):
+                ents = []
+                for _ in range(n_ent):
+                    if rng.random() < 0.3:
+                        c = int(rng.integers(0, max(4, n_ent // 2)))
+                    else:
+                        c = int(rng.integers(0, 2 ** 32))
+                    rs = [(int(rng.integers(0, 1000)), int(rng.integers(1, 20))) for _ in range(rng.integers(1, 3))]
+                    ents.append((c, rs))
+                ups.append(_ds_update(ents))
+            if rep:
+                ups.append(bytes(ALT_MERGE_1[rep - 1]))
+            docs.append(ups)
+    return docs
+
+
+def test_ds_heavy_updates(engine, oracle):
+    check_batch(engine, oracle, batch_of(ds_heavy_docs(31)))
+
+
+def test_ds_heavy_updates_exact_engine(oracle):
+    import ymerge
+    os.environ["YMERGE_FAST_THREADS"] = "0"
+    try:
+        e = ymerge.Engine(0)
+    finally:
+        del os.environ["YMERGE_FAST_THREADS"]
+    try:
+        check_batch(e, oracle, batch_of(ds_heavy_docs(32)))
+    finally:
+        e.close()

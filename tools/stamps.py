@@ -1,0 +1,37 @@
+"""Diagnostic: per-phase cycle shares of k_fast_merge (s_memtime stamps, separate
+instantiation enabled by YMERGE_STAMPS=1; never used for timed numbers)."""
+import ctypes
+import os
+import sys
+
+os.environ["YMERGE_STAMPS"] = "1"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "y-crdt_amd"))
+import numpy as np  # noqa: E402
+import workloads  # noqa: E402
+import ymerge  # noqa: E402
+
+NAMES = ["stage", "walk1", "scan", "walk2", "sort", "classify", "sizes", "write", "ds_sort", "ds_order",
+         "ds_rsort", "ds_union", "ds_write"]
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
+    threads = os.environ.get("YMERGE_FAST_THREADS", "512")
+    b = workloads.text_docs(n, 1000)
+    e = ymerge.Engine(0)
+    e.merge_host(b.data, b.upd_off, b.doc_upd)
+    L = ymerge.lib()
+    L.ymerge_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+    st = np.zeros((n, 16), np.uint64)
+    assert L.ymerge_debug_stamps(e._ctx, n, st.ctypes.data) == 0
+    ok = st[:, 13] > 0
+    d = np.diff(st[ok][:, :14].astype(np.int64), axis=1)
+    tot = d.sum(axis=1).mean()
+    print(f"threads/WG {threads}: {ok.sum()} fast docs, mean {tot:.0f} cycles per doc")
+    for i, nm in enumerate(NAMES):
+        print(f"  {nm:10s} {d[:, i].mean():10.0f} cycles  {100 * d[:, i].mean() / tot:5.1f}%")
+
+
+if __name__ == "__main__":
+    main()

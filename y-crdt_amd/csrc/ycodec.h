@@ -31,6 +31,7 @@ enum : int {
 constexpr uint64_t ALLOC_LIMIT = 1ull << 36;
 constexpr int ANY_MAX_DEPTH = 64;
 
+#define YM_INLINE __device__ __attribute__((always_inline)) inline
 #define YM_TRY(x)                                                                                  \
   do {                                                                                             \
     int _e = (x);                                                                                  \
@@ -239,7 +240,7 @@ __device__ __forceinline__ uint64_t f32_to_f64_bits(uint32_t b) {
   return sign | ((uint64_t)(ex - 127 + 1023) << 52) | ((uint64_t)m << 29);
 }
 // Any::encode number (any.rs:136-154)
-template <class W> __device__ void num_encode(W &w, uint64_t bits) {
+template <class W> YM_INLINE void num_encode(W &w, uint64_t bits) {
   uint64_t sign = bits >> 63;
   int ex = (int)((bits >> 52) & 0x7FF);
   uint64_t frac = bits & ((1ull << 52) - 1);
@@ -307,7 +308,7 @@ struct AnyFrame {
   uint32_t map_start; // cursor index of the first key (maps) or ~0u (arrays)
   uint32_t nkeys;
 };
-__device__ int any_skip(Cur &c); // forward
+__device__ __noinline__ int any_skip(Cur &c); // forward
 __device__ __forceinline__ bool bytes_eq(const uint8_t *a, const uint8_t *b, uint32_t n) {
   for (uint32_t i = 0; i < n; i++)
     if (a[i] != b[i]) return false;
@@ -328,7 +329,7 @@ __device__ __forceinline__ bool map_key_dup(const Cur &c, uint32_t map_start, ui
   }
   return false;
 }
-template <bool CHECK_DUPS = true, class W> __device__ int any_walk(Cur &c, W &w, bool &reenc) {
+template <bool CHECK_DUPS = true, class W> __device__ __noinline__ int any_walk(Cur &c, W &w, bool &reenc) {
   AnyFrame st[ANY_MAX_DEPTH];
   int depth = 0;
   for (;;) {
@@ -479,7 +480,7 @@ template <bool CHECK_DUPS = true, class W> __device__ int any_walk(Cur &c, W &w,
   }
 }
 // skip one already-validated Any value
-__device__ int any_skip(Cur &c) {
+__device__ __noinline__ int any_skip(Cur &c) {
   uint64_t rem[ANY_MAX_DEPTH];
   uint8_t ismap[ANY_MAX_DEPTH];
   int depth = 0;
@@ -541,7 +542,7 @@ struct DocOpts {
   uint32_t cid_pos, cid_len;
 };
 // Options::decode (doc.rs:840-872): last value per key wins; map order irrelevant for the fields
-__device__ __forceinline__ void doc_opts_parse(Cur a, DocOpts &o) {
+YM_INLINE void doc_opts_parse(Cur a, DocOpts &o) {
   o.skip_gc = false;
   o.auto_load = false;
   o.has_cid = false;
@@ -587,8 +588,145 @@ __device__ __forceinline__ void doc_opts_parse(Cur a, DocOpts &o) {
   }
 }
 
+// Cold content kinds (JSON, Binary, Embed, Format, Type, Any, Doc, Move): out of line, cursor
+// position passed and returned by value so the hot walk keeps its cursor in registers.
+struct SlowRes {
+  int err;
+  uint32_t pos, len;
+  bool reenc, unsupported;
+};
+__device__ __noinline__ SlowRes parse_content_slow(const uint8_t *p, uint32_t n, uint32_t pos, uint8_t ref,
+                                                   bool reenc_in) {
+  Cur c{p, n, pos};
+  BlockInfo bi;
+  bi.reenc = reenc_in;
+  bi.unsupported = false;
+  bi.enc_panic = false;
+  bi.len = 0;
+  bool cn;
+  uint32_t v;
+  SlowRes r{0, 0, 0, false, false};
+  r.err = [&]() -> int {
+  switch (ref) {
+    case 1: YM_TRY(rd_var_u32(c, bi.len, cn)); bi.reenc |= !cn; return 0;
+    case 2: {
+      uint32_t L;
+      YM_TRY(rd_var_u32(c, L, cn));
+      int32_t remaining = (int32_t)L;
+      if (remaining < 0) return E_NEM;
+      bi.reenc = true; // re-emitted count is the element count (L + 1)
+      uint32_t cnt = 0;
+      while (remaining >= 0) {
+        YM_TRY(rd_var_u32(c, v, cn));
+        YM_TRY(rd_skip(c, v));
+        cnt++;
+        remaining--;
+      }
+      bi.len = cnt;
+      return 0;
+    }
+    case 3: YM_TRY(rd_var_u32(c, v, cn)); bi.reenc |= !cn; YM_TRY(rd_skip(c, v)); bi.len = 1; return 0;
+    case 4: {
+      YM_TRY(rd_var_u32(c, v, cn));
+      bi.reenc |= !cn;
+      YM_TRY(rd_skip(c, v));
+      const uint8_t *s = c.p + c.i - v;
+      bi.len = str_len16(s, v);
+      if (bi.len > 1) { // encode_slice splits at len UTF-16 units (block.rs:1718-1729)
+        uint32_t bo;
+        if (str_split16(s, v, bi.len, bo)) bi.enc_panic = true;
+        else if (bo != v) bi.reenc = true;
+      }
+      return 0;
+    }
+    case 5:
+      YM_TRY(rd_var_u32(c, v, cn));
+      YM_TRY(rd_skip(c, v));
+      bi.len = 1;
+      bi.unsupported = true;
+      return 0;
+    case 6:
+      YM_TRY(rd_var_u32(c, v, cn));
+      YM_TRY(rd_skip(c, v));
+      YM_TRY(rd_var_u32(c, v, cn));
+      YM_TRY(rd_skip(c, v));
+      bi.len = 1;
+      bi.unsupported = true;
+      return 0;
+    case 7: {
+      uint8_t tr;
+      YM_TRY(rd_u8(c, tr));
+      bi.len = 1;
+      switch (tr) {
+      case 0: case 1: case 2: case 4: case 5: case 6: case 9: case 15: return 0;
+      case 3:
+        YM_TRY(rd_var_u32(c, v, cn));
+        bi.reenc |= !cn;
+        return rd_skip(c, v);
+      case 7: {
+        uint8_t f;
+        uint64_t c64;
+        YM_TRY(rd_u8(c, f));
+        YM_TRY(rd_var_u64(c, c64, cn));
+        YM_TRY(rd_var_u32(c, v, cn));
+        if (f & 1) {
+          YM_TRY(rd_var_u64(c, c64, cn));
+          YM_TRY(rd_var_u32(c, v, cn));
+        }
+        bi.reenc = true;
+        return 0;
+      }
+      default: return E_UNEXPECTED;
+      }
+    }
+    case 8: {
+      uint32_t n;
+      YM_TRY(rd_var_u32(c, n, cn));
+      bi.reenc |= !cn;
+      if ((uint64_t)n * 24 > ALLOC_LIMIT) return E_NEM;
+      Counter cnt;
+      for (uint32_t k = 0; k < n; k++) YM_TRY(any_walk(c, cnt, bi.reenc));
+      bi.len = n;
+      return 0;
+    }
+    case 9: {
+      YM_TRY(rd_var_u32(c, v, cn));
+      YM_TRY(rd_skip(c, v));
+      Counter cnt;
+      bool r;
+      YM_TRY(any_walk<false>(c, cnt, r));
+      bi.reenc = true;
+      bi.len = 1;
+      return 0;
+    }
+    case 11: {
+      int64_t f;
+      uint64_t c64;
+      YM_TRY(rd_var_i64(c, f));
+      if (f < INT32_MIN || f > INT32_MAX) return E_VARINT;
+      YM_TRY(rd_var_u64(c, c64, cn));
+      YM_TRY(rd_var_u32(c, v, cn));
+      if (!(f & 1)) {
+        YM_TRY(rd_var_u64(c, c64, cn));
+        YM_TRY(rd_var_u32(c, v, cn));
+      }
+      bi.reenc = true;
+      bi.len = 1;
+      return 0;
+    }
+    default: return E_UNEXPECTED;
+    }
+  
+  }();
+  r.pos = c.i;
+  r.len = bi.len;
+  r.reenc = bi.reenc;
+  r.unsupported = bi.unsupported;
+  return r;
+}
+
 // Parses one block (Update::decode_block, update.rs:433-488) starting at c.i.
-__device__ int parse_block(Cur &c, BlockInfo &bi) {
+YM_INLINE int parse_block(Cur &c, BlockInfo &bi) {
   uint8_t info;
   bool cn;
   YM_TRY(rd_u8(c, info));
@@ -643,30 +781,27 @@ __device__ int parse_block(Cur &c, BlockInfo &bi) {
   if (want != info) bi.reenc = true;
   uint8_t ref = info & 15;
   bi.ref = ref;
-  switch (ref) {
-  case 1: YM_TRY(rd_var_u32(c, bi.len, cn)); bi.reenc |= !cn; return 0;
-  case 2: {
-    uint32_t L;
-    YM_TRY(rd_var_u32(c, L, cn));
-    int32_t remaining = (int32_t)L;
-    if (remaining < 0) return E_NEM;
-    bi.reenc = true; // re-emitted count is the element count (L + 1)
-    uint32_t cnt = 0;
-    while (remaining >= 0) {
-      YM_TRY(rd_var_u32(c, v, cn));
-      YM_TRY(rd_skip(c, v));
-      cnt++;
-      remaining--;
-    }
-    bi.len = cnt;
+  if (ref == 1) {
+    YM_TRY(rd_var_u32(c, bi.len, cn));
+    bi.reenc |= !cn;
     return 0;
   }
-  case 3: YM_TRY(rd_var_u32(c, v, cn)); bi.reenc |= !cn; YM_TRY(rd_skip(c, v)); bi.len = 1; return 0;
-  case 4: {
+  if (ref == 4) {
     YM_TRY(rd_var_u32(c, v, cn));
     bi.reenc |= !cn;
     YM_TRY(rd_skip(c, v));
     const uint8_t *s = c.p + c.i - v;
+    if (v == 1) {
+      bi.len = 1;
+      return 0;
+    }
+    // ASCII fast check: UTF-16 length = byte length and the full split is the whole string
+    bool ascii = true;
+    for (uint32_t q = 0; q < v; q++) ascii &= s[q] < 0x80;
+    if (ascii) {
+      bi.len = v;
+      return 0;
+    }
     bi.len = str_len16(s, v);
     if (bi.len > 1) { // encode_slice splits at len UTF-16 units (block.rs:1718-1729)
       uint32_t bo;
@@ -675,83 +810,13 @@ __device__ int parse_block(Cur &c, BlockInfo &bi) {
     }
     return 0;
   }
-  case 5:
-    YM_TRY(rd_var_u32(c, v, cn));
-    YM_TRY(rd_skip(c, v));
-    bi.len = 1;
-    bi.unsupported = true;
-    return 0;
-  case 6:
-    YM_TRY(rd_var_u32(c, v, cn));
-    YM_TRY(rd_skip(c, v));
-    YM_TRY(rd_var_u32(c, v, cn));
-    YM_TRY(rd_skip(c, v));
-    bi.len = 1;
-    bi.unsupported = true;
-    return 0;
-  case 7: {
-    uint8_t tr;
-    YM_TRY(rd_u8(c, tr));
-    bi.len = 1;
-    switch (tr) {
-    case 0: case 1: case 2: case 4: case 5: case 6: case 9: case 15: return 0;
-    case 3:
-      YM_TRY(rd_var_u32(c, v, cn));
-      bi.reenc |= !cn;
-      return rd_skip(c, v);
-    case 7: {
-      uint8_t f;
-      uint64_t c64;
-      YM_TRY(rd_u8(c, f));
-      YM_TRY(rd_var_u64(c, c64, cn));
-      YM_TRY(rd_var_u32(c, v, cn));
-      if (f & 1) {
-        YM_TRY(rd_var_u64(c, c64, cn));
-        YM_TRY(rd_var_u32(c, v, cn));
-      }
-      bi.reenc = true;
-      return 0;
-    }
-    default: return E_UNEXPECTED;
-    }
-  }
-  case 8: {
-    uint32_t n;
-    YM_TRY(rd_var_u32(c, n, cn));
-    bi.reenc |= !cn;
-    if ((uint64_t)n * 24 > ALLOC_LIMIT) return E_NEM;
-    Counter cnt;
-    for (uint32_t k = 0; k < n; k++) YM_TRY(any_walk(c, cnt, bi.reenc));
-    bi.len = n;
-    return 0;
-  }
-  case 9: {
-    YM_TRY(rd_var_u32(c, v, cn));
-    YM_TRY(rd_skip(c, v));
-    Counter cnt;
-    bool r;
-    YM_TRY(any_walk<false>(c, cnt, r));
-    bi.reenc = true;
-    bi.len = 1;
-    return 0;
-  }
-  case 11: {
-    int64_t f;
-    uint64_t c64;
-    YM_TRY(rd_var_i64(c, f));
-    if (f < INT32_MIN || f > INT32_MAX) return E_VARINT;
-    YM_TRY(rd_var_u64(c, c64, cn));
-    YM_TRY(rd_var_u32(c, v, cn));
-    if (!(f & 1)) {
-      YM_TRY(rd_var_u64(c, c64, cn));
-      YM_TRY(rd_var_u32(c, v, cn));
-    }
-    bi.reenc = true;
-    bi.len = 1;
-    return 0;
-  }
-  default: return E_UNEXPECTED;
-  }
+  SlowRes r = parse_content_slow(c.p, c.n, c.i, ref, bi.reenc);
+  if (r.err) return r.err;
+  c.i = r.pos;
+  bi.len = r.len;
+  bi.reenc = r.reenc;
+  bi.unsupported = r.unsupported;
+  return 0;
 }
 
 // ------------------------------------------------------------------ block emit
@@ -759,7 +824,7 @@ __device__ int parse_block(Cur &c, BlockInfo &bi) {
 // (slice.rs:199-251): for off > 0 the origin becomes (client, clock + off - 1).
 // `len` is the decoded clock length of the original block.
 template <class W>
-__device__ int emit_block(const uint8_t *p, uint32_t n, uint32_t pos, uint64_t client, uint32_t clock,
+__device__ __noinline__ int emit_block(const uint8_t *p, uint32_t n, uint32_t pos, uint64_t client, uint32_t clock,
                           uint32_t len, uint32_t off, W &w) {
   Cur c{p, n, pos};
   uint8_t info;

@@ -23,6 +23,7 @@ struct FastOut {
   uint8_t *out; // output arena: document d's slot starts at 2*byte_start(d) + 64*d
   uint64_t *out_start, *out_len;
   uint8_t *status, *path;
+  uint64_t *stamps; // diagnostic build only: s_memtime per phase (16 per document)
 };
 size_t fast_lds_bytes(const FastCaps &c);
 void launch_fast_merge(const BatchIn &b, const FastCaps &caps, const FastOut &o, int nt, hipStream_t s);

@@ -32,7 +32,7 @@ struct FastLayout {
   uint32_t in, uoff, bc, bk, bl, bp, bm, ec, et, rs, re, ri;
   uint32_t cB, cE, cR;
   uint32_t skey, sval, sE, sf, sz, sseg;
-  uint32_t dkey, dval, cend, coff, chead, dcl, dfirst, dord, dnc, dbeg, doff;
+  uint32_t dkey, dval, cend, coff, chead, dcl, dfirst, dord, dnc, dbeg, doff, dtab;
   uint32_t misc, total;
 };
 __host__ __device__ inline uint32_t pow2ceil(uint32_t x) {
@@ -40,6 +40,7 @@ __host__ __device__ inline uint32_t pow2ceil(uint32_t x) {
   while (p < x) p <<= 1;
   return p;
 }
+constexpr uint32_t BTAB = 64; // client table of the counting sort (<= 8 distinct clients used)
 __host__ __device__ inline FastLayout fast_layout(const FastCaps &c) {
   FastLayout L;
   uint32_t o = 0;
@@ -61,7 +62,7 @@ __host__ __device__ inline FastLayout fast_layout(const FastCaps &c) {
   L.rs = take(4 * c.r_cap);
   L.re = take(4 * c.r_cap);
   L.ri = take(4 * c.r_cap);
-  L.misc = take(4 * 256);
+  L.misc = take(4 * 256 + 8 * BTAB);
   const uint32_t u0 = o;
   L.cB = take(4 * (c.u_cap + 1));
   L.cE = take(4 * (c.u_cap + 1));
@@ -81,12 +82,13 @@ __host__ __device__ inline FastLayout fast_layout(const FastCaps &c) {
   L.cend = take(4 * (RS + 1));
   L.coff = take(4 * (RS + 1));
   L.chead = take(4 * (RS + 1));
-  L.dcl = take(4 * (RS + 1));
-  L.dfirst = take(4 * (RS + 1));
-  L.dord = take(4 * (RS + 1));
-  L.dnc = take(4 * (RS + 1));
-  L.dbeg = take(4 * (RS + 1));
-  L.doff = take(4 * (RS + 1));
+  L.dcl = take(4 * (c.e_cap + 1)); // per distinct client (D <= NE)
+  L.dfirst = take(4 * (c.e_cap + 1)); // per distinct client (D <= NE)
+  L.dord = take(4 * (c.e_cap + 1)); // per distinct client (D <= NE)
+  L.dnc = take(4 * (c.e_cap + 1)); // per distinct client (D <= NE)
+  L.dbeg = take(4 * (c.e_cap + 1)); // per distinct client (D <= NE)
+  L.doff = take(4 * (c.e_cap + 1)); // per distinct client (D <= NE)
+  L.dtab = take(8 * (2 * pow2ceil(c.e_cap) > RS ? 2 * pow2ceil(c.e_cap) : RS));
   if (o > end) end = o;
   L.total = end;
   return L;
@@ -123,6 +125,34 @@ template <int NT> __device__ __forceinline__ uint32_t bscan_sum(uint32_t v, uint
   __syncthreads();
   return r;
 }
+
+template <int NT> __device__ __forceinline__ uint64_t bscan_sum64(uint64_t v, uint64_t *ws64, uint64_t &total) {
+  uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+  uint64_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint64_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) ws64[w] = x;
+  __syncthreads();
+  if (t == 0) {
+    uint64_t acc = 0;
+    for (int i = 0; i < NT / 64; i++) {
+      uint64_t s = ws64[i];
+      ws64[i] = acc;
+      acc += s;
+    }
+    ws64[NT / 64] = acc;
+  }
+  __syncthreads();
+  uint64_t r = ws64[w] + x - v;
+  total = ws64[NT / 64];
+  __syncthreads();
+  return r;
+}
+
+__device__ __forceinline__ uint32_t mix32(uint32_t c) { return c * 0x9E3779B9u; }
 
 // segmented scan pair: (flag, value); (f1,v1)+(f2,v2) = (f1|f2, f2 ? v2 : op(v1,v2))
 struct OpMax {
@@ -183,7 +213,7 @@ __device__ __forceinline__ void bscan_seg(uint32_t f, uint32_t v, uint32_t *ws, 
 }
 
 // bitonic sort of (key64, val32) pairs, n a power of two, composite order (key, val)
-template <int NT> __device__ void bitonic(uint64_t *k, uint32_t *v, uint32_t n) {
+template <int NT> YM_INLINE void bitonic(uint64_t *k, uint32_t *v, uint32_t n) {
   for (uint32_t size = 2; size <= n; size <<= 1) {
     for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
       for (uint32_t i = threadIdx.x; i < n / 2; i += NT) {
@@ -208,25 +238,23 @@ template <int NT> __device__ void bitonic(uint64_t *k, uint32_t *v, uint32_t n) 
 // ------------------------------------------------------------------ walk sinks
 struct FastCount {
   uint32_t nb, ne, nr;
-  bool unsupported;
-  DsOrder ord;
-  __device__ void on_section(uint32_t) {}
-  __device__ int on_block(uint32_t, uint32_t, const BlockInfo &bi, uint32_t, uint32_t) {
+  bool unsupported, big_ds;
+  YM_INLINE void on_section(uint32_t) {}
+  YM_INLINE int on_block(uint32_t, uint32_t, const BlockInfo &bi, uint32_t, uint32_t) {
     if (bi.kind != BK_SKIP) nb++;
     if (bi.unsupported) unsupported = true;
     return 0;
   }
-  __device__ int on_ds_begin(uint32_t) {
-    ord.begin();
+  YM_INLINE int on_ds_begin(uint32_t nds) {
+    if (nds > DS_SMALL) big_ds = true; // table emulation beyond 16 buckets: exact engine
     return 0;
   }
-  __device__ int on_ds_entry(uint32_t client, uint32_t) {
+  YM_INLINE int on_ds_entry(uint32_t, uint32_t) {
     ne++;
-    uint32_t dead;
-    return ord.insert(client, dead);
+    return 0;
   }
-  __device__ void on_ds_range(uint32_t, uint32_t) { nr++; }
-  __device__ int on_ds_done() { return 0; }
+  YM_INLINE void on_ds_range(uint32_t, uint32_t) { nr++; }
+  YM_INLINE int on_ds_done() { return 0; }
 };
 
 struct FastFill {
@@ -234,9 +262,8 @@ struct FastFill {
   const uint8_t *doc;
   uint32_t doc_len, upd, ubase; // update index, byte offset of update within doc
   uint32_t nb, ne, nr, ebase;
-  DsOrder ord;
-  __device__ void on_section(uint32_t) {}
-  __device__ int on_block(uint32_t client, uint32_t clock, const BlockInfo &bi, uint32_t bpos, uint32_t blen) {
+  YM_INLINE void on_section(uint32_t) {}
+  YM_INLINE int on_block(uint32_t client, uint32_t clock, const BlockInfo &bi, uint32_t bpos, uint32_t blen) {
     if (bi.kind == BK_SKIP) return 0;
     uint32_t pos = ubase + bpos;
     uint32_t canon = blen;
@@ -253,36 +280,47 @@ struct FastFill {
     nb++;
     return 0;
   }
-  __device__ int on_ds_begin(uint32_t) {
-    ord.begin();
+  YM_INLINE int on_ds_begin(uint32_t) {
     ebase = ne;
     return 0;
   }
-  __device__ int on_ds_entry(uint32_t client, uint32_t) {
-    uint32_t dead;
-    YM_TRY(ord.insert(client, dead));
-    if (dead != ~0u) et[ebase + dead] &= 0x7FFFFFFFu; // replaced in this update: dead
+  YM_INLINE int on_ds_entry(uint32_t client, uint32_t) {
     ec[ne] = client;
     et[ne] = 0x80000000u | (upd << 8);
     ne++;
     return 0;
   }
-  __device__ void on_ds_range(uint32_t s, uint32_t e) {
+  YM_INLINE void on_ds_range(uint32_t s, uint32_t e) {
     rs[nr] = s;
     re[nr] = e;
     ri[nr] = ne - 1;
     nr++;
   }
-  __device__ int on_ds_done() {
-    uint32_t k = 0;
-    for (uint32_t i = 0; i < ord.hb.buckets; i++)
-      if (ord.hb.slot[i]) et[ebase + ord.hb.slot[i] - 1] |= k++;
+  YM_INLINE int on_ds_done() {
+    uint32_t n = ne - ebase;
+    if (n >= 2) { // (n <= DS_SMALL here: walk 1 handed larger tables to the exact engine)
+      ds_small_order(ec + ebase, n, et + ebase);
+      for (uint32_t i = 0; i < n; i++) {
+        uint32_t p = et[ebase + i];
+        et[ebase + i] = (p == DS_DEAD ? 0u : 0x80000000u | p) | (upd << 8);
+      }
+    }
     return 0;
   }
 };
 
 // ------------------------------------------------------------------ the kernel
-template <int NT>
+// Diagnostic build only (STAMPS=true, env YMERGE_STAMPS): lane 0 records s_memtime at
+// phase boundaries into o.stamps[doc * 16 + k]; never part of a timed run.
+#define YM_STAMP(k)                                                                                \
+  do {                                                                                             \
+    if (STAMPS) {                                                                                  \
+      __syncthreads();                                                                             \
+      if (threadIdx.x == 0) o.stamps[(size_t)blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
+    }                                                                                              \
+  } while (0)
+
+template <int NT, bool STAMPS>
 __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, FastOut o) {
   extern __shared__ __align__(16) uint8_t smem[];
   const FastLayout L = fast_layout(caps);
@@ -309,6 +347,7 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
     }
     return;
   }
+  YM_STAMP(0);
   // ---- 1 stage bytes (word copy + byte tail) and update offsets
   uint8_t *in = smem + L.in;
   {
@@ -329,11 +368,12 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
   }
   __syncthreads();
 
+  YM_STAMP(1);
   // ---- 2a walk: counts, first error, unsupported
   uint32_t *cB = (uint32_t *)(smem + L.cB), *cE = (uint32_t *)(smem + L.cE), *cR = (uint32_t *)(smem + L.cR);
   {
     FastCount s;
-    s.unsupported = false;
+    s.unsupported = s.big_ds = false;
     for (uint32_t i = t; i < U; i += NT) {
       s.nb = s.ne = s.nr = 0;
       int e = walk_update(in + uoff[i], uoff[i + 1] - uoff[i], s);
@@ -342,12 +382,22 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
       cE[i] = s.ne;
       cR[i] = s.nr;
     }
-    if (s.unsupported) atomicOr(&misc[1], 1u);
+    if (s.unsupported || s.big_ds) atomicOr(&misc[1], (s.unsupported ? 1u : 0u) | (s.big_ds ? 2u : 0u));
   }
   __syncthreads();
   {
     uint32_t ek = misc[0];
-    if (ek != 0xFFFFFFFFu || misc[1]) {
+    const uint32_t fl = misc[1];
+    if (ek == 0xFFFFFFFFu && (fl & 2)) { // an update with > DS_SMALL DeleteSet entries
+      if (t == 0) {
+        o.path[d] = 1;
+        o.status[d] = 0;
+        o.out_len[d] = 0;
+        o.out_start[d] = slot;
+      }
+      return;
+    }
+    if (ek != 0xFFFFFFFFu || fl) {
       if (t == 0) {
         o.status[d] = (uint8_t)(ek != 0xFFFFFFFFu ? (ek & 0xFF) : E_UNSUPPORTED);
         o.path[d] = 0;
@@ -357,6 +407,7 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
       return;
     }
   }
+  YM_STAMP(2);
   // ---- 2b exclusive scans of the per-update counts (contiguous chunk per lane)
   uint32_t NB, NE, NR;
   {
@@ -394,6 +445,7 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
            *bp = (uint32_t *)(smem + L.bp), *bm = (uint32_t *)(smem + L.bm);
   uint32_t *ec = (uint32_t *)(smem + L.ec), *et = (uint32_t *)(smem + L.et);
   uint32_t *rs = (uint32_t *)(smem + L.rs), *re = (uint32_t *)(smem + L.re), *ri = (uint32_t *)(smem + L.ri);
+  YM_STAMP(3);
   // ---- 2c second walk: records at scanned positions
   {
     FastFill f;
@@ -420,23 +472,118 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
   }
   __syncthreads();
 
-  // ---- 3 sort blocks: key = (~client, clock), val = record index (input order)
+  YM_STAMP(4);
+  // ---- 3 sort blocks by (client desc, clock asc, input order).
+  // Stable counting sort by client rank (<= 32 distinct clients: LDS table), then a
+  // per-client clock-order check; LDS bitonic only when that check fails.
   uint64_t *skey = (uint64_t *)(smem + L.skey);
   uint32_t *sval = (uint32_t *)(smem + L.sval);
   {
-    uint32_t unsorted = 0;
-    for (uint32_t j = t; j + 1 < NB; j += NT) {
-      uint64_t ka = ((uint64_t)(~bc[j]) << 32) | bk[j], kb = ((uint64_t)(~bc[j + 1]) << 32) | bk[j + 1];
-      if (ka > kb) unsorted = 1;
-    }
-    unsorted = __syncthreads_or(unsorted);
-    uint32_t n2 = unsorted ? pow2ceil(NB) : NB;
-    for (uint32_t j = t; j < n2; j += NT) {
-      skey[j] = j < NB ? (((uint64_t)(~bc[j]) << 32) | bk[j]) : ~0ull;
-      sval[j] = j;
-    }
+    uint64_t *btab = (uint64_t *)(misc + 256); // [BTAB] (client << 32 | rank), ~0 = empty
+    for (uint32_t i = t; i < BTAB; i += NT) btab[i] = ~0ull;
+    if (t == 0) sc[3] = 0;
     __syncthreads();
-    if (unsorted) bitonic<NT>(skey, sval, n2);
+    const uint32_t per0 = (NB + NT - 1) / NT, k0 = t * per0, k1 = k0 + per0 < NB ? k0 + per0 : NB;
+    uint32_t overflow = 0;
+    for (uint32_t k = k0; k < k1; k++) {
+      uint32_t c = bc[k];
+      if (k > k0 && bc[k - 1] == c) continue;
+      uint32_t h = mix32(c) >> 26; // 64 slots
+      for (uint32_t probe = 0;; probe++) {
+        if (probe == BTAB) {
+          overflow = 1;
+          break;
+        }
+        uint64_t cur = btab[h];
+        if (cur == ~0ull) {
+          uint64_t prev = atomicCAS((unsigned long long *)&btab[h], ~0ull, ((uint64_t)c << 32));
+          if (prev == ~0ull) {
+            atomicAdd(&sc[3], 1u);
+            break;
+          }
+          cur = prev;
+        }
+        if ((uint32_t)(cur >> 32) == c) break;
+        h = (h + 1) & (BTAB - 1);
+      }
+    }
+    overflow = __syncthreads_or(overflow);
+    const uint32_t ncl = sc[3];
+    bool counting = !overflow && ncl <= 8 && NB <= 65535;
+    if (counting) {
+      // rank = number of distinct clients greater than this one (lane per table slot)
+      uint64_t mine = t < BTAB ? btab[t] : ~0ull;
+      uint32_t r = 0;
+      if (mine != ~0ull)
+        for (uint32_t j = 0; j < BTAB; j++) {
+          uint64_t o2 = btab[j];
+          r += (o2 != ~0ull && (uint32_t)(o2 >> 32) > (uint32_t)(mine >> 32));
+        }
+      __syncthreads();
+      if (mine != ~0ull) btab[t] = (mine & 0xFFFFFFFF00000000ull) | r;
+      __syncthreads();
+      auto rank_of = [&](uint32_t c) -> uint32_t {
+        uint32_t h = mix32(c) >> 26;
+        while ((uint32_t)(btab[h] >> 32) != c) h = (h + 1) & (BTAB - 1);
+        return (uint32_t)btab[h];
+      };
+      // Two packed 64-bit scans (ranks 0-3, 4-7; 16-bit counters, NB <= 65535), kept in
+      // registers: P0/P1 field r = next sorted position of this lane's rank-r blocks.
+      uint64_t P0 = 0, P1 = 0;
+      for (uint32_t k = k0; k < k1; k++) {
+        uint32_t r = rank_of(bc[k]);
+        uint64_t inc = 1ull << (16 * (r & 3));
+        if (r < 4) P0 += inc;
+        else P1 += inc;
+      }
+      uint64_t T0, T1;
+      P0 = bscan_sum64<NT>(P0, (uint64_t *)(misc + 2), T0);
+      P1 = bscan_sum64<NT>(P1, (uint64_t *)(misc + 2), T1);
+      {
+        // add rank starts (exclusive sum of rank totals) into every field
+        uint64_t S0 = 0, S1 = 0;
+        uint32_t start = 0;
+#pragma unroll
+        for (uint32_t r = 0; r < 8; r++) {
+          uint64_t T = r < 4 ? T0 : T1;
+          uint32_t tot = (uint32_t)((T >> (16 * (r & 3))) & 0xFFFF);
+          if (r < 4) S0 |= (uint64_t)start << (16 * r);
+          else S1 |= (uint64_t)start << (16 * (r - 4));
+          start += tot;
+        }
+        P0 += S0;
+        P1 += S1;
+      }
+      for (uint32_t k = k0; k < k1; k++) {
+        uint32_t r = rank_of(bc[k]);
+        uint32_t sh = 16 * (r & 3);
+        uint32_t pos;
+        if (r < 4) {
+          pos = (uint32_t)((P0 >> sh) & 0xFFFF);
+          P0 += 1ull << sh;
+        } else {
+          pos = (uint32_t)((P1 >> sh) & 0xFFFF);
+          P1 += 1ull << sh;
+        }
+        sval[pos] = k;
+        skey[pos] = ((uint64_t)(~bc[k]) << 32) | bk[k];
+      }
+      __syncthreads();
+      // clock order within each client run
+      uint32_t bad = 0;
+      for (uint32_t j = t; j + 1 < NB; j += NT)
+        if (skey[j] > skey[j + 1]) bad = 1;
+      counting = !__syncthreads_or(bad);
+    }
+    if (!counting) {
+      uint32_t n2 = pow2ceil(NB);
+      for (uint32_t j = t; j < n2; j += NT) {
+        skey[j] = j < NB ? (((uint64_t)(~bc[j]) << 32) | bk[j]) : ~0ull;
+        sval[j] = j;
+      }
+      __syncthreads();
+      bitonic<NT>(skey, sval, n2);
+    }
   }
   // ---- 4 classify: per lane a contiguous chunk of sorted positions
   uint32_t *sE = (uint32_t *)(smem + L.sE), *sf = (uint32_t *)(smem + L.sf), *sz = (uint32_t *)(smem + L.sz);
@@ -546,6 +693,7 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
       return;
     }
   }
+  YM_STAMP(6);
   // ---- 6a block section sizes: per client header + (Skip) + canonical block bytes
   uint32_t blocks_size, NC;
   uint32_t *sseg = (uint32_t *)(smem + L.sseg);
@@ -612,6 +760,7 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
     blocks_size = base + tot;
     __syncthreads();
   }
+  YM_STAMP(7);
   // ---- 6b write the block section into the document's slot
   uint8_t *out = o.out + slot;
   if (blocks_size <= cap) {
@@ -635,7 +784,9 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
       if (sf[j] & 1) {
         uint32_t p = bp[r] & 0xFFFF, len = bp[r] >> 16;
         if (bm[r] & 4) {
-          emit_block(in, nbytes, p, bc[r], bk[r], bl[r], 0, w);
+          Writer w2 = w; // only the out-of-line re-encode takes a Writer by reference
+          emit_block(in, nbytes, p, bc[r], bk[r], bl[r], 0, w2);
+          w.n = w2.n;
         } else {
           for (uint32_t q = 0; q < len; q++) w.p[w.n + q] = in[p + q];
         }
@@ -644,38 +795,58 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
   }
   __syncthreads();
 
+  YM_STAMP(8);
   // ---- 5 DeleteSet: distinct clients in yrs' table order, union of ranges
   uint64_t *dkey = (uint64_t *)(smem + L.dkey);
   uint32_t *dval = (uint32_t *)(smem + L.dval);
   const uint32_t RSZ = pow2ceil(caps.r_cap > caps.e_cap ? caps.r_cap : caps.e_cap);
   uint32_t *d_client = (uint32_t *)(smem + L.dcl), *d_first = (uint32_t *)(smem + L.dfirst),
            *d_aux = (uint32_t *)(smem + L.dord);
-  // 5a entries: key = (client, upd<<8|tpos) for live entries
-  uint32_t ne2 = pow2ceil(NE ? NE : 1);
-  for (uint32_t j = t; j < ne2; j += NT) {
-    bool live = j < NE && (et[j] & 0x80000000u);
-    dkey[j] = live ? (((uint64_t)ec[j] << 32) | (et[j] & 0x7FFFFFFFu)) : ~0ull;
-    dval[j] = j;
-  }
+  // 5a distinct clients of live entries and their first occurrence (upd << 8 | tpos):
+  //    LDS open-addressing table, 64-bit CAS insert, atomicMin on a hit
+  uint64_t *dtab = (uint64_t *)(smem + L.dtab);
+  const uint32_t TS = 2 * pow2ceil(caps.e_cap); // table slots (>= 2 * NE)
+  for (uint32_t j = t; j < TS; j += NT) dtab[j] = ~0ull;
   __syncthreads();
-  bitonic<NT>(dkey, dval, ne2);
-  // distinct clients: heads of runs of equal client among live keys
-  uint32_t D;
-  {
-    const uint32_t pe = (NE + NT - 1) / NT, e0 = t * pe, e1 = e0 + pe < NE ? e0 + pe : NE;
-    uint32_t nh = 0;
-    for (uint32_t j = e0; j < e1; j++)
-      if (dkey[j] != ~0ull && (j == 0 || (dkey[j] >> 32) != (dkey[j - 1] >> 32))) nh++;
-    uint32_t pre = bscan_sum<NT>(nh, ws, D);
-    for (uint32_t j = e0; j < e1; j++) {
-      if (dkey[j] != ~0ull && (j == 0 || (dkey[j] >> 32) != (dkey[j - 1] >> 32))) {
-        d_client[pre] = (uint32_t)(dkey[j] >> 32);
-        d_first[pre] = (uint32_t)dkey[j];
-        pre++;
+  for (uint32_t j = t; j < NE; j += NT) {
+    if (!(et[j] & 0x80000000u)) continue;
+    const uint32_t c = ec[j];
+    const uint64_t v = ((uint64_t)c << 32) | (et[j] & 0x7FFFFFFFu);
+    uint32_t h = mix32(c) & (TS - 1);
+    for (;;) {
+      uint64_t cur = dtab[h];
+      if (cur == ~0ull) {
+        cur = atomicCAS((unsigned long long *)&dtab[h], ~0ull, (unsigned long long)v);
+        if (cur == ~0ull) break;
       }
+      if ((uint32_t)(cur >> 32) == c) {
+        atomicMin((unsigned long long *)&dtab[h], (unsigned long long)v);
+        break;
+      }
+      h = (h + 1) & (TS - 1);
     }
   }
   __syncthreads();
+  // compact the occupied slots, then order them by client (rank sort: D is small)
+  uint32_t D;
+  {
+    const uint32_t pt = TS / NT ? TS / NT : 1, s0 = t * pt, s1 = s0 + pt < TS ? s0 + pt : TS;
+    uint32_t nh = 0;
+    for (uint32_t j = s0; j < s1; j++) nh += dtab[j] != ~0ull;
+    uint32_t pre = bscan_sum<NT>(nh, ws, D);
+    for (uint32_t j = s0; j < s1; j++)
+      if (dtab[j] != ~0ull) dkey[pre++] = dtab[j];
+  }
+  __syncthreads();
+  for (uint32_t j = t; j < D; j += NT) {
+    const uint64_t kj = dkey[j];
+    uint32_t r = 0;
+    for (uint32_t q = 0; q < D; q++) r += dkey[q] < kj; // clients are distinct
+    d_client[r] = (uint32_t)(kj >> 32);
+    d_first[r] = (uint32_t)kj;
+  }
+  __syncthreads();
+  YM_STAMP(9);
   // 5b yrs' table order (IdSet::merge inserts in first-occurrence order, hashbrown layout)
   if (t == 0) {
     // insertion order: sort ranks by first occurrence (insertion sort; D is small in practice)
@@ -753,20 +924,38 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
     }
     return;
   }
-  // 5c ranges of live entries sorted by (client, start)
-  uint32_t nr2 = pow2ceil(NR ? NR : 1);
-  for (uint32_t j = t; j < nr2; j += NT) {
-    bool live = j < NR && (et[ri[j]] & 0x80000000u);
-    dkey[j] = live ? (((uint64_t)ec[ri[j]] << 32) | rs[j]) : ~0ull;
-    dval[j] = j;
-  }
-  __syncthreads();
+  YM_STAMP(10);
+  // 5c ranges of live entries sorted by (client, start, index): rank sort, every lane
+  //    counts the smaller keys with LDS broadcast reads (no barrier stages)
   {
+    uint64_t *tkey = dtab; // >= NR slots
     uint32_t unsorted = 0;
-    for (uint32_t j = t; j + 1 < nr2; j += NT)
-      if (dkey[j] > dkey[j + 1] || (dkey[j] == dkey[j + 1] && dval[j] > dval[j + 1])) unsorted = 1;
+    for (uint32_t j = t; j < NR; j += NT) {
+      bool live = et[ri[j]] & 0x80000000u;
+      tkey[j] = live ? (((uint64_t)ec[ri[j]] << 32) | rs[j]) : ~0ull;
+    }
+    __syncthreads();
+    for (uint32_t j = t; j + 1 < NR; j += NT)
+      if (tkey[j] > tkey[j + 1]) unsorted = 1;
     unsorted = __syncthreads_or(unsorted);
-    if (unsorted) bitonic<NT>(dkey, dval, nr2);
+    if (unsorted) {
+      for (uint32_t j = t; j < NR; j += NT) {
+        const uint64_t kj = tkey[j];
+        uint32_t r = 0;
+        for (uint32_t q = 0; q < NR; q++) { // uniform trip count: one broadcast read per step
+          const uint64_t kq = tkey[q];
+          r += (kq < kj) | ((kq == kj) & (q < j));
+        }
+        dkey[r] = kj;
+        dval[r] = j;
+      }
+    } else {
+      for (uint32_t j = t; j < NR; j += NT) {
+        dkey[j] = tkey[j];
+        dval[j] = j;
+      }
+    }
+    __syncthreads();
   }
   // live count
   uint32_t NL;
@@ -775,6 +964,7 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
     for (uint32_t j = t; j < NR; j += NT) c += dkey[j] != ~0ull;
     bscan_sum<NT>(c, ws, NL);
   }
+  YM_STAMP(11);
   // 5d segmented union over sorted live ranges: comp heads, comp end, comp size at comp tails
   uint32_t *cmp_end = (uint32_t *)(smem + L.cend);
   uint32_t *cmp_off = (uint32_t *)(smem + L.coff);
@@ -840,6 +1030,7 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
     if (t == 0) cmp_off[NL] = ds_comp_total;
   }
   __syncthreads();
+  YM_STAMP(12);
   // 5e per distinct client (rank r, ascending client): range segment, #components, bytes
   // d_aux[0..D) holds iteration order; compute per-rank [rb, re) by binary search
   uint32_t *r_beg = (uint32_t *)(smem + L.dbeg);
@@ -926,23 +1117,31 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
     o.out_len[d] = total;
     o.out_start[d] = slot;
   }
+  YM_STAMP(13);
 }
 
 size_t fast_lds_bytes(const FastCaps &c) { return fast_layout(c).total; }
 
+template <int NT> static void launch_nt(const BatchIn &b, const FastCaps &caps, const FastOut &o, size_t lds,
+                                        hipStream_t s) {
+  if (o.stamps) {
+    hipFuncSetAttribute((const void *)k_fast_merge<NT, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((k_fast_merge<NT, true>), dim3(b.n_docs), dim3(NT), lds, s, b, caps, o);
+  } else {
+    hipFuncSetAttribute((const void *)k_fast_merge<NT, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((k_fast_merge<NT, false>), dim3(b.n_docs), dim3(NT), lds, s, b, caps, o);
+  }
+}
+
 void launch_fast_merge(const BatchIn &b, const FastCaps &caps, const FastOut &o, int nt, hipStream_t s) {
   if (!b.n_docs) return;
   size_t lds = fast_lds_bytes(caps);
-  if (nt == 1024) {
-    hipFuncSetAttribute((const void *)k_fast_merge<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(k_fast_merge<1024>, dim3(b.n_docs), dim3(1024), lds, s, b, caps, o);
-  } else if (nt == 512) {
-    hipFuncSetAttribute((const void *)k_fast_merge<512>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(k_fast_merge<512>, dim3(b.n_docs), dim3(512), lds, s, b, caps, o);
-  } else {
-    hipFuncSetAttribute((const void *)k_fast_merge<256>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(k_fast_merge<256>, dim3(b.n_docs), dim3(256), lds, s, b, caps, o);
-  }
+  if (nt == 1024)
+    launch_nt<1024>(b, caps, o, lds, s);
+  else if (nt == 512)
+    launch_nt<512>(b, caps, o, lds, s);
+  else
+    launch_nt<256>(b, caps, o, lds, s);
 }
 
 } // namespace ym

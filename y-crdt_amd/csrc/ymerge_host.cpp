@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -51,11 +52,12 @@ struct ymerge_ctx {
   hipStream_t s = nullptr;
   DevBuf in_bytes, in_upd_off, in_doc_upd, in_sv, in_sv_off;
   DevBuf status, path, out_start, out_len, pack_off, counts, need, scr_off, scratch, sizes, spill_off, scan_tmp;
-  DevBuf arena, packed, counter;
+  DevBuf arena, packed, counter, stamps;
+  bool want_stamps = false;
   uint64_t *h_pinned = nullptr;
   hipEvent_t ev[6];
   ymerge_stats stats{};
-  ym::FastCaps caps{32768, 2048, 2048, 1024, 1024};
+  ym::FastCaps caps{32768, 2048, 2048, 512, 1024}; // bytes, updates, blocks, DS entries, DS ranges
   int fast_threads = 512;
   std::mutex mu;
 };
@@ -72,6 +74,14 @@ static bool ctx_init(ymerge_ctx *c, int device) {
   // YMERGE_FAST_THREADS: workgroup size of the fast path (256/512/1024); 0 routes every
   // document through the exact engine (used by the parity tests to cover both engines)
   if (const char *v = getenv("YMERGE_FAST_THREADS")) c->fast_threads = atoi(v);
+  if (const char *v = getenv("YMERGE_STAMPS")) c->want_stamps = atoi(v) != 0;
+  // the fast kernel's LDS layout must fit one workgroup (160 KB on gfx950)
+  int lds_max = 0;
+  if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess) return false;
+  if (ym::fast_lds_bytes(c->caps) > (size_t)lds_max) {
+    fprintf(stderr, "ymerge: fast-path LDS layout %zu B exceeds %d B\n", ym::fast_lds_bytes(c->caps), lds_max);
+    return false;
+  }
   return true;
 }
 
@@ -138,7 +148,13 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   uint8_t *status = c->status.as<uint8_t>(), *path = c->path.as<uint8_t>();
   hipMemsetAsync(c->counter.p, 0, 64, c->s);
   hipEventRecord(c->ev[0], c->s);
-  ym::FastOut fo{arena, ostart, olen, status, path};
+  uint64_t *stamps = nullptr;
+  if (c->want_stamps) {
+    if (!c->stamps.ensure(nn * 16 * 8)) return YMERGE_ERR_DEVICE;
+    hipMemsetAsync(c->stamps.p, 0, nn * 16 * 8, c->s);
+    stamps = c->stamps.as<uint64_t>();
+  }
+  ym::FastOut fo{arena, ostart, olen, status, path, stamps};
   if (c->fast_threads)
     ym::launch_fast_merge(b, c->caps, fo, c->fast_threads, c->s);
   else
@@ -238,6 +254,14 @@ extern "C" int ymerge_result_to_host(ymerge_ctx *c, const ymerge_device_result *
   std::lock_guard<std::mutex> g(c->mu);
   hipSetDevice(c->device);
   return pack_to_host(c, res, n_docs, out, out_off, status);
+}
+
+// diagnostic: copy per-document phase stamps (16 x u64 per document) of the last batch
+extern "C" int ymerge_debug_stamps(ymerge_ctx *c, uint64_t n_docs, uint64_t *dst) {
+  if (!c || !c->want_stamps || !c->stamps.p) return YMERGE_ERR_OTHER;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipMemcpy(dst, c->stamps.p, n_docs * 16 * 8, hipMemcpyDeviceToHost) != hipSuccess) return YMERGE_ERR_DEVICE;
+  return 0;
 }
 
 extern "C" void ymerge_last_stats(ymerge_ctx *c, ymerge_stats *st) {

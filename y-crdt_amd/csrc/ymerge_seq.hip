@@ -16,25 +16,20 @@ namespace ym {
 struct CountSink {
   uint32_t NB = 0, NBALL = 0, NE = 0, NR = 0;
   bool unsupported = false;
-  DsOrder ord;
-  __device__ void on_section(uint32_t) {}
-  __device__ int on_block(uint32_t, uint32_t, const BlockInfo &bi, uint32_t, uint32_t) {
+  YM_INLINE void on_section(uint32_t) {}
+  YM_INLINE int on_block(uint32_t, uint32_t, const BlockInfo &bi, uint32_t, uint32_t) {
     NBALL++;
     if (bi.kind != BK_SKIP) NB++;
     if (bi.unsupported) unsupported = true;
     return 0;
   }
-  __device__ int on_ds_begin(uint32_t) {
-    ord.begin();
+  YM_INLINE int on_ds_begin(uint32_t) { return 0; }
+  YM_INLINE int on_ds_entry(uint32_t, uint32_t) {
+    NE++;
     return 0;
   }
-  __device__ int on_ds_entry(uint32_t client, uint32_t) {
-    NE++;
-    uint32_t dead;
-    return ord.insert(client, dead);
-  }
-  __device__ void on_ds_range(uint32_t, uint32_t) { NR++; }
-  __device__ int on_ds_done() { return 0; }
+  YM_INLINE void on_ds_range(uint32_t, uint32_t) { NR++; }
+  YM_INLINE int on_ds_done() { return 0; }
 };
 
 __global__ void k_seq_count(BatchIn b, const uint8_t *path, uint8_t *status, uint32_t *counts,
@@ -126,14 +121,37 @@ __device__ inline SeqMem seq_carve(uint32_t *w, uint32_t U, uint32_t NB, uint32_
   return m;
 }
 
+// Per-update table order for updates with more than DS_SMALL DeleteSet entries: the
+// same HashMap::insert restatement as ds_small_order, over the document's global
+// table scratch (used again only by the later DeleteSet merge).
+__device__ __noinline__ void ds_large_order(SeqMem &m, uint32_t ebase, uint32_t n) {
+  GHB t{m.hb_slot, m.hb_keys, m.hb_cap, 0, 0, 0};
+  uint32_t *pos = m.e_tpos + ebase;
+  for (uint32_t i = 0; i < n; i++) {
+    uint32_t c = m.e_client[ebase + i];
+    pos[i] = 0;
+    t.reserve(1, m.hb_tmp); // n <= NE: 4 NE + 64 slots always suffice
+    int e = t.find(c);
+    if (e >= 0) {
+      pos[e] = DS_DEAD;
+      for (uint32_t s = 0; s < t.buckets; s++)
+        if (t.slot[s] == (uint32_t)e + 1) t.slot[s] = i + 1;
+      t.keys[i] = c;
+    } else
+      t.place(c, i);
+  }
+  uint32_t k = 0;
+  for (uint32_t s = 0; s < t.buckets; s++)
+    if (t.slot[s]) pos[t.slot[s] - 1] = k++;
+}
+
 struct FillSink {
   SeqMem *m;
   uint32_t upd, nb, ne, nr, ebase;
-  DsOrder ord;
   const uint8_t *doc_base;
   const uint8_t *upd_base;
-  __device__ void on_section(uint32_t) {}
-  __device__ int on_block(uint32_t client, uint32_t clock, const BlockInfo &bi, uint32_t bpos, uint32_t) {
+  YM_INLINE void on_section(uint32_t) {}
+  YM_INLINE int on_block(uint32_t client, uint32_t clock, const BlockInfo &bi, uint32_t bpos, uint32_t) {
     if (bi.kind == BK_SKIP) return 0;
     m->b_client[nb] = client;
     m->b_clock[nb] = clock;
@@ -144,15 +162,11 @@ struct FillSink {
     nb++;
     return 0;
   }
-  __device__ int on_ds_begin(uint32_t) {
-    ord.begin();
+  YM_INLINE int on_ds_begin(uint32_t) {
     ebase = ne;
     return 0;
   }
-  __device__ int on_ds_entry(uint32_t client, uint32_t nrng) {
-    uint32_t dead;
-    YM_TRY(ord.insert(client, dead));
-    if (dead != ~0u) m->e_live[ebase + dead] = 0;
+  YM_INLINE int on_ds_entry(uint32_t client, uint32_t nrng) {
     m->e_client[ne] = client;
     m->e_upd[ne] = upd;
     m->e_live[ne] = 1;
@@ -161,17 +175,21 @@ struct FillSink {
     ne++;
     return 0;
   }
-  __device__ void on_ds_range(uint32_t s, uint32_t e) {
+  YM_INLINE void on_ds_range(uint32_t s, uint32_t e) {
     m->r_start[nr] = s;
     m->r_end[nr] = e;
     m->r_entry[nr] = ne - 1;
     nr++;
   }
-  __device__ int on_ds_done() {
-    // table iteration order -> tpos of the surviving entries
-    uint32_t k = 0;
-    for (uint32_t i = 0; i < ord.hb.buckets; i++)
-      if (ord.hb.slot[i]) m->e_tpos[ebase + ord.hb.slot[i] - 1] = k++;
+  YM_INLINE int on_ds_done() {
+    uint32_t n = ne - ebase;
+    if (n == 1) m->e_tpos[ebase] = 0;
+    else if (n >= 2) {
+      if (n <= DS_SMALL) ds_small_order(m->e_client + ebase, n, m->e_tpos + ebase);
+      else ds_large_order(*m, ebase, n);
+      for (uint32_t i = 0; i < n; i++)
+        if (m->e_tpos[ebase + i] == DS_DEAD) m->e_live[ebase + i] = 0;
+    }
     return 0;
   }
 };

@@ -10,9 +10,9 @@ namespace ym {
 struct TrackClients {
   uint32_t client[8], count[8];
   uint32_t n;
-  __device__ void reset() { n = 0; }
+  YM_INLINE void reset() { n = 0; }
   // returns blocks already recorded for `client` in this update (exact for <= 8 clients)
-  __device__ uint32_t *slot(uint32_t c) {
+  YM_INLINE uint32_t *slot(uint32_t c) {
     for (uint32_t i = 0; i < n; i++)
       if (client[i] == c) return &count[i];
     if (n < 8) {
@@ -24,7 +24,7 @@ struct TrackClients {
   }
 };
 
-template <class S> __device__ int walk_update(const uint8_t *p, uint32_t n, S &s) {
+template <class S> YM_INLINE int walk_update(const uint8_t *p, uint32_t n, S &s) {
   Cur c{p, n, 0};
   bool cn;
   uint32_t ncl;
@@ -37,7 +37,7 @@ template <class S> __device__ int walk_update(const uint8_t *p, uint32_t n, S &s
     YM_TRY(rd_var_u32(c, nb, cn));
     YM_TRY(rd_var_u32(c, client, cn));
     YM_TRY(rd_var_u32(c, clock, cn));
-    uint32_t *cnt = tc.slot(client);
+    uint32_t *cnt = ncl > 1 ? tc.slot(client) : nullptr;
     uint64_t existing = cnt ? *cnt : 0;
     if ((existing + nb) * 32ull > ALLOC_LIMIT) return E_NEM; // VecDeque<BlockCarrier>::try_reserve
     s.on_section(client);
@@ -72,29 +72,33 @@ template <class S> __device__ int walk_update(const uint8_t *p, uint32_t n, S &s
 }
 
 // DS table order of one update: HashMap::insert per entry in stream order
-struct DsOrder {
-  SmallHB<64> hb;
-  uint32_t n;
-  __device__ void begin() {
-    hb.init_empty();
-    n = 0;
-  }
-  // returns local index of a replaced (now dead) entry, ~0u if none; <0 error
-  __device__ int insert(uint32_t client, uint32_t &dead) {
-    if (n >= 64) return E_UNSUPPORTED; // device limit: <= 64 DeleteSet entries per update
+// Per-update DeleteSet table order.  IdSet decoding inserts every (client, ranges)
+// entry of one update into a std HashMap (id_set.rs:411-426, HashMap::insert:
+// reserve(1), replace in place on a repeated client); the DeleteSet merge later
+// iterates that table (update.rs:542-548).  ds_small_order restates the table for
+// one update with at most DS_SMALL entries (16 buckets suffice) and reports, per
+// entry in stream order, its iteration position or DS_DEAD if a later entry with
+// the same client replaced it.  Cold path: single-entry updates never call it.
+constexpr uint32_t DS_SMALL = 14;
+constexpr uint32_t DS_DEAD = 0xFFFFFFFFu;
+__device__ __noinline__ void ds_small_order(const uint32_t *clients, uint32_t n, uint32_t *pos_out) {
+  SmallHB<16> hb;
+  hb.init_empty();
+  for (uint32_t i = 0; i < n; i++) {
+    uint32_t c = clients[i];
+    pos_out[i] = 0;
     bool existed;
-    int e = hb.insert(client, n, existed);
-    if (e == -2) return E_UNSUPPORTED;
-    dead = ~0u;
+    int e = hb.insert(c, i, existed);
     if (existed) {
-      dead = (uint32_t)e;
-      for (uint32_t i = 0; i < hb.buckets; i++)
-        if (hb.slot[i] == e + 1) hb.slot[i] = (uint16_t)(n + 1);
-      hb.keys[n] = client;
+      pos_out[e] = DS_DEAD;
+      for (uint32_t s = 0; s < hb.buckets; s++)
+        if (hb.slot[s] == e + 1) hb.slot[s] = (uint16_t)(i + 1);
+      hb.keys[i] = c;
     }
-    n++;
-    return 0;
   }
-};
+  uint32_t k = 0;
+  for (uint32_t s = 0; s < hb.buckets; s++)
+    if (hb.slot[s]) pos_out[hb.slot[s] - 1] = k++;
+}
 
 } // namespace ym
