@@ -109,6 +109,13 @@ typedef struct {
 } ymerge_batch_result;
 int ymerge_updates_v1_batch(ymerge_ctx *ctx, const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_updates,
                             const uint64_t *doc_upd, uint64_t n_docs, ymerge_batch_result **res);
+/* diff_updates_v1 over a batch: document d = one update bytes[upd_off[d] .. upd_off[d+1]) and one
+ * encoded remote state vector sv[sv_off[d] .. sv_off[d+1]) (sync-step-2 serving, yrs/src/alt.rs:73-81) */
+int ydiff_updates_v1_batch(ymerge_ctx *ctx, const uint8_t *bytes, const uint64_t *upd_off, const uint8_t *sv,
+                           const uint64_t *sv_off, uint64_t n_docs, ymerge_batch_result **res);
+/* encode_state_vector_from_update_v1 over a batch (yrs/src/alt.rs:54-57) */
+int yencode_state_vector_from_update_v1_batch(ymerge_ctx *ctx, const uint8_t *bytes, const uint64_t *upd_off,
+                                              uint64_t n_docs, ymerge_batch_result **res);
 void ymerge_batch_result_destroy(ymerge_batch_result *res);
 
 #ifdef __cplusplus

@@ -35,6 +35,7 @@ def _load():
     lib.yo_merge_batch.argtypes = [vp, vp, vp, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
                                    P(u8p), vp, vp]
     lib.yo_diff_batch.argtypes = [vp, vp, vp, vp, ctypes.c_size_t, ctypes.c_int, P(u8p), vp, vp]
+    lib.yo_sv_batch.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_int, P(u8p), vp, vp]
     return lib
 
 
@@ -136,6 +137,22 @@ def diff_batch(ubytes, u_off, svbytes, sv_off, threads=1):
     status = np.zeros(max(1, n_docs), dtype=np.uint8)
     lib().yo_diff_batch(ubytes.ctypes.data, u_off.ctypes.data, svbytes.ctypes.data, sv_off.ctypes.data,
                         n_docs, threads, ctypes.byref(out), out_off.ctypes.data, status.ctypes.data)
+    total = int(out_off[-1])
+    arena = ctypes.string_at(out, total) if total else b""
+    lib().yo_free(out)
+    return arena, out_off, status[:n_docs]
+
+
+def sv_batch(ubytes, u_off, threads=1):
+    """encode_state_vector_from_update_v1 per document (one update each)."""
+    ubytes = np.ascontiguousarray(ubytes, dtype=np.uint8)
+    u_off = np.ascontiguousarray(u_off, dtype=np.uint64)
+    n_docs = len(u_off) - 1
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    out_off = np.zeros(n_docs + 1, dtype=np.uint64)
+    status = np.zeros(max(1, n_docs), dtype=np.uint8)
+    lib().yo_sv_batch(ubytes.ctypes.data, u_off.ctypes.data, n_docs, threads, ctypes.byref(out),
+                      out_off.ctypes.data, status.ctypes.data)
     total = int(out_off[-1])
     arena = ctypes.string_at(out, total) if total else b""
     lib().yo_free(out)

@@ -1734,7 +1734,10 @@ static void *worker(void *arg) {
     if (d0 >= j->n_docs) break;
     for (size_t d = d0; d < d0 + 4 && d < j->n_docs; d++) {
       int st;
-      if (j->is_diff) {
+      if (j->is_diff == 2) {
+        st = yo_encode_state_vector_from_update_v1(j->bytes + j->upd_off[d], j->upd_off[d + 1] - j->upd_off[d],
+                                                   &j->outs[d], &j->lens[d]);
+      } else if (j->is_diff) {
         st = yo_diff_updates_v1(j->bytes + j->upd_off[d], j->upd_off[d + 1] - j->upd_off[d],
                                 j->svbytes + j->sv_off[d], j->sv_off[d + 1] - j->sv_off[d], &j->outs[d],
                                 &j->lens[d]);
@@ -1808,6 +1811,18 @@ int yo_diff_batch(const uint8_t *ubytes, const uint64_t *u_off, const uint8_t *s
   j.sv_off = sv_off;
   j.n_docs = n_docs;
   j.is_diff = 1;
+  j.status = status;
+  return run_batch(&j, threads, out, out_off);
+}
+
+int yo_sv_batch(const uint8_t *ubytes, const uint64_t *u_off, size_t n_docs, int threads, uint8_t **out,
+                uint64_t *out_off, uint8_t *status) {
+  job_t j;
+  memset(&j, 0, sizeof(j));
+  j.bytes = ubytes;
+  j.upd_off = u_off;
+  j.n_docs = n_docs;
+  j.is_diff = 2;
   j.status = status;
   return run_batch(&j, threads, out, out_off);
 }

@@ -58,6 +58,9 @@ int yo_diff_batch(const uint8_t *ubytes, const uint64_t *u_off, const uint8_t *s
                   const uint64_t *sv_off, size_t n_docs, int threads, uint8_t **out,
                   uint64_t *out_off, uint8_t *status);
 
+int yo_sv_batch(const uint8_t *ubytes, const uint64_t *u_off, size_t n_docs, int threads, uint8_t **out,
+                uint64_t *out_off, uint8_t *status);
+
 #ifdef __cplusplus
 }
 #endif

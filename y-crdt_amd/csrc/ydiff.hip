@@ -1,0 +1,637 @@
+// ydiff.hip — batched diff_updates_v1 and encode_state_vector_from_update_v1 on gfx950.
+//
+// Reference semantics:
+//   diff_updates_v1                    yrs/src/alt.rs:73-81 -> StateVector::decode
+//                                      (state_vector.rs:111-124), Update::decode_v1
+//                                      (update.rs:714-749), Update::encode_diff (update.rs:490-535),
+//                                      IdSet::encode (id_set.rs:401-410), IdRange::encode
+//                                      (id_set.rs:256-266: squash a clone when !is_squashed)
+//   encode_state_vector_from_update_v1 yrs/src/alt.rs:54-57 -> Update::state_vector
+//                                      (update.rs:107-114; BlockRange::last_id +1 quirk,
+//                                      block.rs:1150-1152), StateVector::encode (state_vector.rs:126-134)
+//
+// Two kernels per batch (one update per document):
+//   k_plan  — one lane per document walks its update once through a register window
+//             (ywin.h): validation in stream order, per-client state (remote clock, first
+//             block past the remote clock, section byte ranges), DeleteSet table order
+//             (hashbrown emulation, GHB), squash of unsquashed ranges; emits a short list of
+//             output ops with their sizes.  The small-capacity pass runs over every document
+//             with a fixed per-document scratch; documents that overflow it are re-planned in
+//             a second pass whose scratch is sized from the document length.
+//   k_exec  — one wavefront per document: wave prefix scan of the op sizes, header / re-encode
+//             ops lane-parallel, verbatim byte ranges (most of the output) copied by all 64
+//             lanes with coalesced accesses.
+#include "ycodec.h"
+#include "yseq.h"
+#include "ywin.h"
+#include "ywalk.h"
+#include "ykernels.h"
+
+namespace ym {
+
+enum : uint32_t { OP_VARS = 1, OP_COPY = 2, OP_EMIT = 3, OP_WALK = 4, OP_DSQ = 5, OP_DSS = 6 };
+constexpr uint32_t OPW = 8;  // words per op: kind, size, p0..p4, out offset
+constexpr uint32_t CLW = 12; // words per client entry
+constexpr uint32_t SECW = 5; // words per section record
+constexpr uint32_t DEW = 8;  // words per DeleteSet entry
+constexpr uint32_t PLAN_OVF = 0xFFFF;
+
+struct PlanLayout {
+  uint32_t BC, BE;
+  uint32_t ct_slot, ct_keys, ct_tmp, cl, sec, dt_slot, dt_keys, dt_tmp, de, sq, s2_slot, s2_keys, s2_tmp, s2_val,
+      ops, words;
+};
+__host__ __device__ inline uint32_t buckets_for(uint64_t cap) {
+  if (cap < 8) return cap < 4 ? 4 : 8;
+  uint64_t adj = cap * 8 / 7, b = 1;
+  while (b < adj) b <<= 1;
+  return (uint32_t)b;
+}
+__host__ __device__ inline PlanLayout plan_layout(const PlanCaps &c) {
+  PlanLayout L;
+  uint32_t o = 2; // [0] n ops, [1] reserved
+  auto take = [&](uint32_t w) {
+    uint32_t r = o;
+    o += (w + 1) & ~1u;
+    return r;
+  };
+  L.BC = buckets_for(c.C);
+  L.BE = buckets_for(c.E);
+  L.ct_slot = take(L.BC);
+  L.ct_keys = take(c.C);
+  L.ct_tmp = take(L.BC > c.C ? L.BC : c.C);
+  L.cl = take(CLW * c.C);
+  L.sec = take(SECW * c.C);
+  L.dt_slot = take(L.BE);
+  L.dt_keys = take(c.E);
+  L.dt_tmp = take(L.BE);
+  L.de = take(DEW * c.E);
+  L.sq = take(2 * c.R);
+  L.s2_slot = take(L.BC);
+  L.s2_keys = take(c.C);
+  L.s2_tmp = take(L.BC);
+  L.s2_val = take(c.C);
+  L.ops = take(OPW * c.O);
+  L.words = o;
+  return L;
+}
+// capacities that can never overflow for a successfully decoded update of `len` bytes:
+// a client section takes >= 3 bytes, a DeleteSet entry >= 2, a range >= 2.
+__host__ __device__ inline PlanCaps big_caps(uint64_t len) {
+  PlanCaps c;
+  c.C = (uint32_t)(len / 3 + 2);
+  c.E = (uint32_t)(len / 2 + 2);
+  c.R = (uint32_t)(len / 2 + 2);
+  c.O = 3 * c.C + 2 * c.E + 4;
+  return c;
+}
+__host__ __device__ inline PlanCaps small_caps() { return PlanCaps{8, 8, 64, 3 * 8 + 2 * 8 + 4}; }
+uint64_t plan_small_words() { return plan_layout(small_caps()).words; }
+__host__ __device__ inline uint64_t plan_big_words(uint64_t len) { return plan_layout(big_caps(len)).words; }
+
+// canonical size of a validated block re-encoded with ItemSlice offset `off`
+__device__ __forceinline__ int block_size(const WCur &c, uint32_t pos, uint32_t blen, const BlockInfo &bi,
+                                          uint32_t client, uint32_t clock, uint32_t off, uint32_t &sz) {
+  if (bi.kind != BK_ITEM) {
+    sz = off == 0 && !bi.reenc ? blen : 1 + varlen(bi.len - off);
+    return 0;
+  }
+  if (off == 0 && !bi.reenc) {
+    sz = blen;
+    return bi.enc_panic ? E_PANIC : 0;
+  }
+  Counter cn;
+  int e = emit_block(c.p, c.n, pos, client, clock, bi.len, off, cn);
+  sz = (uint32_t)cn.n;
+  return e;
+}
+
+// remote clock of `client` in an encoded state vector (last entry wins: HashMap::insert)
+__device__ __forceinline__ uint32_t sv_lookup(const uint8_t *sv, uint32_t n, uint32_t client) {
+  WCur s;
+  wc_init(s, sv, n);
+  bool cn;
+  uint32_t len, clk, r = 0;
+  uint64_t c;
+  if (wc_var_u32(s, len, cn)) return 0;
+  for (uint32_t i = 0; i < len; i++) {
+    if (wc_var_u64(s, c, cn) || wc_var_u32(s, clk, cn)) return r;
+    if (c == (uint64_t)client) r = clk;
+  }
+  return r;
+}
+
+struct OpW {
+  uint32_t *ops;
+  uint32_t n, cap;
+  __device__ bool put(uint32_t kind, uint32_t size, uint32_t a = 0, uint32_t b = 0, uint32_t c = 0, uint32_t d = 0,
+                      uint32_t e = 0) {
+    if (n >= cap) return false;
+    uint32_t *o = ops + (size_t)OPW * n++;
+    o[0] = kind;
+    o[1] = size;
+    o[2] = a;
+    o[3] = b;
+    o[4] = c;
+    o[5] = d;
+    o[6] = e;
+    o[7] = 0;
+    return true;
+  }
+};
+__device__ __forceinline__ uint32_t vars_size(uint32_t k, uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t s = varlen(a);
+  if (k > 1) s += varlen(b);
+  if (k > 2) s += varlen(c);
+  return s;
+}
+
+// Plans one document.  Returns PLAN_OVF when the scratch capacities are exceeded (the
+// document is re-planned with big capacities), otherwise the yrs status (0 = ok).
+template <bool DIFF>
+__device__ uint32_t plan_doc(const uint8_t *up, uint32_t un, const uint8_t *svp, uint32_t svn, uint32_t *scr,
+                             const PlanCaps &cap, uint64_t &out_size) {
+  const PlanLayout L = plan_layout(cap);
+  bool cn;
+  // ---- remote state vector (decoded before the update, alt.rs:77-78)
+  if (DIFF) {
+    WCur s;
+    wc_init(s, svp, svn);
+    uint32_t len, clk;
+    uint64_t c;
+    YM_TRY(wc_var_u32(s, len, cn));
+    if (len && (uint64_t)buckets_for(len) * 17ull > ALLOC_LIMIT) return E_PANIC; // with_capacity
+    for (uint32_t i = 0; i < len; i++) {
+      YM_TRY(wc_var_u64(s, c, cn));
+      YM_TRY(wc_var_u32(s, clk, cn));
+    }
+  }
+  // ---- update: client sections
+  WCur c;
+  wc_init(c, up, un);
+  uint32_t ncl;
+  YM_TRY(wc_var_u32(c, ncl, cn));
+  if (ncl && (uint64_t)buckets_for(ncl) * 41ull > ALLOC_LIMIT) return E_NEM; // try_reserve
+  GHB ct{scr + L.ct_slot, scr + L.ct_keys, L.BC, 0, 0, 0};
+  if (ncl && !ct.reserve(ncl, scr + L.ct_tmp)) return PLAN_OVF;
+  uint32_t *cl = scr + L.cl, *sec = scr + L.sec;
+  uint32_t nsec = 0;
+  uint32_t pending = 0; // first encode-time error (yrs encodes only after a full decode)
+  bool unsupported = false;
+  for (uint32_t i = 0; i < ncl; i++) {
+    uint32_t nb, client, clock;
+    YM_TRY(wc_var_u32(c, nb, cn));
+    YM_TRY(wc_var_u32(c, client, cn));
+    YM_TRY(wc_var_u32(c, clock, cn));
+    int e = ct.find(client);
+    if (e < 0) { // entry(..).or_default: capacity reserved up front
+      e = (int)ct.items;
+      if (!ct.reserve(1, scr + L.ct_tmp)) return PLAN_OVF;
+      ct.place(client, (uint32_t)e);
+      uint32_t *s = cl + CLW * e;
+      for (uint32_t k = 0; k < CLW; k++) s[k] = 0;
+      if (DIFF) s[4] = sv_lookup(svp, svn, client);
+    }
+    uint32_t *st = cl + CLW * e;
+    uint32_t nstored = st[0], lkind = st[1], lclock = st[2], llen = st[3];
+    const uint32_t remote = st[4];
+    uint32_t found = st[5], count = st[10];
+    if (((uint64_t)nstored + nb) * 32ull > ALLOC_LIMIT) return E_NEM;
+    if (nsec >= cap.C) return PLAN_OVF;
+    uint32_t kb = 0xFFFFFFFFu, pure = 1, ssize = 0;
+    for (uint32_t j = 0; j < nb; j++) {
+      const uint32_t bpos = c.i;
+      BlockInfo bi;
+      YM_TRY(wparse_block(c, bi));
+      if (bi.kind == BK_ITEM && bi.len == 0) { // Item::new -> None: dropped
+        if (kb != 0xFFFFFFFFu) pure = 0;
+        continue;
+      }
+      if ((uint64_t)clock + bi.len > 0xFFFFFFFFull) return E_PANIC;
+      unsupported |= bi.unsupported;
+      nstored++;
+      lkind = bi.kind;
+      lclock = clock;
+      llen = bi.len;
+      if (DIFF) {
+        const uint32_t blen = c.i - bpos;
+        if (!found) {
+          if (bi.kind != BK_SKIP && clock + bi.len > remote) {
+            found = 1;
+            const uint32_t off = remote > clock ? remote - clock : 0;
+            uint32_t sz = 0;
+            if (!bi.unsupported) {
+              int ee = block_size(c, bpos, blen, bi, client, clock, off, sz);
+              if (ee && !pending) pending = (uint32_t)ee;
+            }
+            st[6] = bpos;
+            st[7] = clock;
+            st[8] = bi.len;
+            st[9] = off;
+            st[11] = sz;
+            count = 1;
+            kb = c.i;
+          }
+        } else {
+          if (kb == 0xFFFFFFFFu) kb = bpos;
+          count++;
+          uint32_t sz = blen;
+          if (bi.reenc || bi.enc_panic) {
+            pure = 0;
+            if (!bi.unsupported) {
+              int ee = block_size(c, bpos, blen, bi, client, clock, 0, sz);
+              if (ee && !pending) pending = (uint32_t)ee;
+            }
+          }
+          ssize += sz;
+        }
+      }
+      clock += bi.len;
+    }
+    if (kb == 0xFFFFFFFFu) kb = c.i;
+    uint32_t *sr = sec + SECW * nsec++;
+    sr[0] = (uint32_t)e;
+    sr[1] = kb;
+    sr[2] = c.i;
+    sr[3] = pure;
+    sr[4] = ssize;
+    st[0] = nstored;
+    st[1] = lkind | 0x100;
+    st[2] = lclock;
+    st[3] = llen;
+    st[5] = found;
+    st[10] = count;
+  }
+  // ---- DeleteSet (IdSet::decode: HashMap::insert per entry, id_set.rs:412-426)
+  uint32_t nds;
+  YM_TRY(wc_var_u32(c, nds, cn));
+  GHB dt{scr + L.dt_slot, scr + L.dt_keys, L.BE, 0, 0, 0};
+  uint32_t *de = scr + L.de, *sq = scr + L.sq;
+  uint32_t nsq = 0;
+  for (uint32_t i = 0; i < nds; i++) {
+    uint32_t client, n;
+    YM_TRY(wc_var_u32(c, client, cn));
+    const uint32_t cpos = c.i;
+    YM_TRY(wc_var_u32(c, n, cn));
+    bool canon = cn, squashed = true;
+    uint32_t prev_e = 0, sz = varlen(n);
+    for (uint32_t k = 0; k < n; k++) {
+      uint32_t s0, ln;
+      YM_TRY(wc_var_u32(c, s0, cn));
+      canon &= cn;
+      YM_TRY(wc_var_u32(c, ln, cn));
+      canon &= cn;
+      if ((uint64_t)s0 + ln > 0xFFFFFFFFull) return E_PANIC;
+      if (k > 0 && s0 < prev_e) squashed = false;
+      prev_e = s0 + ln;
+      sz += varlen(s0) + varlen(ln);
+    }
+    if (!DIFF) continue;
+    if (i >= cap.E) return PLAN_OVF;
+    if (!dt.reserve(1, scr + L.dt_tmp)) return PLAN_OVF;
+    int e = dt.find(client);
+    if (e >= 0) { // replaced in place: the slot now names entry i
+      for (uint32_t s = 0; s < dt.buckets; s++)
+        if (dt.slot[s] == (uint32_t)e + 1) dt.slot[s] = i + 1;
+      dt.keys[i] = client;
+    } else {
+      dt.place(client, i);
+    }
+    uint32_t *r = de + DEW * i;
+    r[0] = client;
+    r[1] = cpos;
+    r[2] = c.i;
+    r[3] = n;
+    r[4] = (squashed ? 1u : 0u) | (canon ? 2u : 0u);
+    if (!squashed) {
+      // IdRange::squash of a clone: stable sort by start, join overlapping or adjacent
+      if (nsq + n > cap.R) return PLAN_OVF;
+      uint32_t *v = sq + 2 * nsq;
+      WCur q;
+      wc_init(q, up, un);
+      q.i = cpos;
+      uint32_t dummy;
+      wc_var_u32(q, dummy, cn);
+      for (uint32_t k = 0; k < n; k++) {
+        uint32_t s0, ln;
+        wc_var_u32(q, s0, cn);
+        wc_var_u32(q, ln, cn);
+        // insertion into the sorted prefix (stable: after equal starts)
+        uint32_t j = k;
+        while (j > 0 && v[2 * (j - 1)] > s0) {
+          v[2 * j] = v[2 * (j - 1)];
+          v[2 * j + 1] = v[2 * (j - 1) + 1];
+          j--;
+        }
+        v[2 * j] = s0;
+        v[2 * j + 1] = s0 + ln;
+      }
+      uint32_t m = 0;
+      for (uint32_t k = 0; k < n; k++) {
+        uint32_t s0 = v[2 * k], e0 = v[2 * k + 1];
+        if (m > 0 && !(v[2 * (m - 1)] > e0 || s0 > v[2 * (m - 1) + 1])) {
+          if (s0 < v[2 * (m - 1)]) v[2 * (m - 1)] = s0;
+          if (e0 > v[2 * (m - 1) + 1]) v[2 * (m - 1) + 1] = e0;
+        } else {
+          v[2 * m] = s0;
+          v[2 * m + 1] = e0;
+          m++;
+        }
+      }
+      sz = varlen(m);
+      for (uint32_t k = 0; k < m; k++) sz += varlen(v[2 * k]) + varlen(v[2 * k + 1] - v[2 * k]);
+      r[5] = nsq;
+      r[6] = m;
+      nsq += m;
+    }
+    r[7] = varlen(client) + sz;
+  }
+  // ---- output plan
+  OpW ow{scr + L.ops, 0, cap.O};
+  uint64_t total = 0;
+  if (DIFF) {
+    if (unsupported) return E_UNSUPPORTED;
+    if (pending) return pending;
+    // clients with content, descending (encode_diff sorts by client id)
+    uint32_t *ord = scr + L.ct_tmp;
+    uint32_t nf = 0;
+    for (uint32_t e = 0; e < ct.items; e++)
+      if (cl[CLW * e + 5]) {
+        const uint32_t k = ct.keys[e];
+        uint32_t j = nf++;
+        while (j > 0 && ct.keys[ord[j - 1]] < k) {
+          ord[j] = ord[j - 1];
+          j--;
+        }
+        ord[j] = e;
+      }
+    if (!ow.put(OP_VARS, varlen(nf), 1, nf)) return PLAN_OVF;
+    total += varlen(nf);
+    for (uint32_t q = 0; q < nf; q++) {
+      const uint32_t e = ord[q];
+      const uint32_t *st = cl + CLW * e;
+      const uint32_t client = ct.keys[e];
+      const uint32_t hclock = st[7] + st[9];
+      uint32_t hs = vars_size(3, st[10], client, hclock);
+      if (!ow.put(OP_VARS, hs, 3, st[10], client, hclock)) return PLAN_OVF;
+      if (!ow.put(OP_EMIT, st[11], st[6], st[7], st[8], st[9], client)) return PLAN_OVF;
+      total += hs + st[11];
+      for (uint32_t s = 0; s < nsec; s++) {
+        const uint32_t *sr = sec + SECW * s;
+        if (sr[0] != e || sr[1] >= sr[2]) continue;
+        bool ok = sr[3] ? ow.put(OP_COPY, sr[2] - sr[1], sr[1]) : ow.put(OP_WALK, sr[4], sr[1], sr[2], 0, 0, client);
+        if (!ok) return PLAN_OVF;
+        total += sr[3] ? sr[2] - sr[1] : sr[4];
+      }
+    }
+    // DeleteSet in table order
+    if (!ow.put(OP_VARS, varlen(dt.items), 1, dt.items)) return PLAN_OVF;
+    total += varlen(dt.items);
+    for (uint32_t s = 0; s < dt.buckets; s++) {
+      if (!dt.slot[s]) continue;
+      const uint32_t *r = de + DEW * (dt.slot[s] - 1);
+      const uint32_t vs = varlen(r[0]);
+      bool ok = ow.put(OP_VARS, vs, 1, r[0]);
+      if (r[4] & 1) {
+        ok = ok && ((r[4] & 2) ? ow.put(OP_COPY, r[2] - r[1], r[1]) : ow.put(OP_DSS, r[7] - vs, r[1], r[3]));
+      } else {
+        ok = ok && ow.put(OP_DSQ, r[7] - vs, r[5], r[6]);
+      }
+      if (!ok) return PLAN_OVF;
+      total += r[7];
+    }
+  } else {
+    // Update::state_vector: iterate the decoded client table, set_max into a fresh table
+    GHB s2{scr + L.s2_slot, scr + L.s2_keys, L.BC, 0, 0, 0};
+    uint32_t *val = scr + L.s2_val;
+    for (uint32_t s = 0; s < ct.buckets; s++) {
+      if (!ct.slot[s]) continue;
+      const uint32_t e = ct.slot[s] - 1;
+      const uint32_t *st = cl + CLW * e;
+      if (st[0] == 0) return E_PANIC; // blocks[blocks.len() - 1] on an empty deque
+      // last_id().clock + 1: Item -> clock + len; GC / Skip -> clock + len + 1 (block.rs:1150-1152)
+      const uint32_t v = st[2] + st[3] + ((st[1] & 0xFF) != BK_ITEM ? 1u : 0u);
+      const uint32_t key = ct.keys[e];
+      int f = s2.find(key);
+      if (f < 0) {
+        f = (int)s2.items;
+        if (!s2.reserve(1, scr + L.s2_tmp)) return PLAN_OVF;
+        s2.place(key, (uint32_t)f);
+        val[f] = 0;
+      }
+      if (v > val[f]) val[f] = v;
+    }
+    if (!ow.put(OP_VARS, varlen(s2.items), 1, s2.items)) return PLAN_OVF;
+    total += varlen(s2.items);
+    for (uint32_t s = 0; s < s2.buckets; s++) {
+      if (!s2.slot[s]) continue;
+      const uint32_t e = s2.slot[s] - 1;
+      const uint32_t k = s2.keys[e], v = val[e];
+      const uint32_t sz = varlen(k) + varlen(v);
+      if (!ow.put(OP_VARS, sz, 2, k, v)) return PLAN_OVF;
+      total += sz;
+    }
+  }
+  scr[0] = ow.n;
+  out_size = total;
+  return 0;
+}
+
+// Validation only (first error in stream order), for documents whose section count
+// exceeds even the big capacities: such an update cannot decode (a section takes
+// >= 3 bytes), so only its error code is needed.
+struct NullSink {
+  YM_INLINE void on_section(uint32_t) {}
+  YM_INLINE int on_block(uint32_t, uint32_t, const BlockInfo &, uint32_t, uint32_t) { return 0; }
+  YM_INLINE int on_ds_begin(uint32_t) { return 0; }
+  YM_INLINE int on_ds_entry(uint32_t, uint32_t) { return 0; }
+  YM_INLINE void on_ds_range(uint32_t, uint32_t) {}
+  YM_INLINE int on_ds_done() { return 0; }
+};
+template <bool DIFF>
+__device__ __noinline__ uint32_t validate_doc(const uint8_t *up, uint32_t un, const uint8_t *svp, uint32_t svn) {
+  if (DIFF) {
+    Cur s{svp, svn, 0};
+    bool cn;
+    uint32_t len, clk;
+    uint64_t c;
+    YM_TRY(rd_var_u32(s, len, cn));
+    if (len && (uint64_t)buckets_for(len) * 17ull > ALLOC_LIMIT) return E_PANIC;
+    for (uint32_t i = 0; i < len; i++) {
+      YM_TRY(rd_var_u64(s, c, cn));
+      YM_TRY(rd_var_u32(s, clk, cn));
+    }
+  }
+  NullSink ns;
+  int e = walk_update(up, un, ns);
+  return e ? (uint32_t)e : (uint32_t)E_OTHER;
+}
+
+template <bool DIFF>
+__global__ void __launch_bounds__(64) k_plan(DiffBatch b, PlanScratch ps, int pass) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= b.n_docs) return;
+  if (pass == 1 && !ps.big[d]) return;
+  const uint64_t o0 = b.upd_off[d], o1 = b.upd_off[d + 1];
+  const uint8_t *up = b.bytes + o0;
+  const uint32_t un = (uint32_t)(o1 - o0);
+  const uint8_t *svp = nullptr;
+  uint32_t svn = 0;
+  if (DIFF) {
+    svp = b.sv + b.sv_off[d];
+    svn = (uint32_t)(b.sv_off[d + 1] - b.sv_off[d]);
+  }
+  uint32_t *scr;
+  PlanCaps cap;
+  if (pass == 0) {
+    cap = small_caps();
+    scr = ps.small + (size_t)d * ps.small_words;
+  } else {
+    cap = big_caps(un);
+    scr = ps.bigscr + ps.big_off[d];
+  }
+  uint64_t sz = 0;
+  uint32_t st = plan_doc<DIFF>(up, un, svp, svn, scr, cap, sz);
+  if (st == PLAN_OVF && pass == 1) st = validate_doc<DIFF>(up, un, svp, svn);
+  if (st == PLAN_OVF) {
+    // only the small pass can overflow (big capacities hold every decodable update)
+    ps.big[d] = pass == 0 ? 1 : 0;
+    ps.status[d] = pass == 0 ? 0 : E_OTHER;
+    ps.size[d] = 0;
+    if (pass == 0) atomicAdd(ps.n_big, 1u);
+    return;
+  }
+  if (pass == 0) ps.big[d] = 0;
+  ps.status[d] = (uint8_t)st;
+  ps.size[d] = st ? 0 : sz;
+}
+
+__global__ void k_big_need(const uint64_t *upd_off, const uint8_t *big, uint32_t n, uint64_t *need) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= n) return;
+  need[d] = big[d] ? (plan_big_words(upd_off[d + 1] - upd_off[d]) + 1) & ~1ull : 0;
+}
+
+// ------------------------------------------------------------------ executor
+template <class W> __device__ __forceinline__ void walk_emit(const uint8_t *up, uint32_t un, uint32_t kb,
+                                                             uint32_t ke, uint32_t client, W &w) {
+  WCur c;
+  wc_init(c, up, un);
+  c.i = kb;
+  while (c.i < ke) {
+    const uint32_t bpos = c.i;
+    BlockInfo bi;
+    if (wparse_block(c, bi)) return;
+    if (bi.kind == BK_ITEM && bi.len == 0) continue;
+    if (!bi.reenc && !bi.enc_panic) {
+      for (uint32_t q = bpos; q < c.i; q++) w.u8((uint8_t)wc_byte(c, q));
+    } else {
+      emit_block(up, un, bpos, client, 0, bi.len, 0, w);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_exec(DiffBatch b, PlanScratch ps, const uint64_t *out_off, uint8_t *out) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t d = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (d >= b.n_docs) return;
+  if (ps.status[d] || ps.size[d] == 0) return;
+  const uint64_t o0 = b.upd_off[d], o1 = b.upd_off[d + 1];
+  const uint8_t *up = b.bytes + o0;
+  const uint32_t un = (uint32_t)(o1 - o0);
+  const uint32_t *scr;
+  PlanCaps cap;
+  if (ps.big[d]) {
+    cap = big_caps(un);
+    scr = ps.bigscr + ps.big_off[d];
+  } else {
+    cap = small_caps();
+    scr = ps.small + (size_t)d * ps.small_words;
+  }
+  const PlanLayout L = plan_layout(cap);
+  uint32_t *ops = (uint32_t *)scr + L.ops;
+  const uint32_t nops = scr[0];
+  uint8_t *dst = out + out_off[d];
+  // op offsets: wave-wide exclusive scan of the sizes
+  uint32_t acc = 0;
+  for (uint32_t r = 0; r < nops; r += 64) {
+    const uint32_t k = r + lane;
+    const uint32_t sz = k < nops ? ops[OPW * k + 1] : 0;
+    uint32_t x = sz;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      uint32_t y = __shfl_up(x, o, 64);
+      if (lane >= (uint32_t)o) x += y;
+    }
+    if (k < nops) ops[OPW * k + 7] = acc + x - sz;
+    acc += __shfl(x, 63, 64);
+  }
+  // header / re-encode ops: one lane each
+  for (uint32_t k = lane; k < nops; k += 64) {
+    const uint32_t *o = ops + OPW * k;
+    Writer w{dst + o[7], 0};
+    switch (o[0]) {
+    case OP_VARS:
+      w_var(w, o[3]);
+      if (o[2] > 1) w_var(w, o[4]);
+      if (o[2] > 2) w_var(w, o[5]);
+      break;
+    case OP_EMIT: emit_block(up, un, o[2], o[6], o[3], o[4], o[5], w); break;
+    case OP_WALK: walk_emit(up, un, o[2], o[3], o[6], w); break;
+    case OP_DSQ: {
+      const uint32_t *v = scr + L.sq + 2 * o[2];
+      w_var(w, o[3]);
+      for (uint32_t q = 0; q < o[3]; q++) {
+        w_var(w, v[2 * q]);
+        w_var(w, v[2 * q + 1] - v[2 * q]);
+      }
+      break;
+    }
+    case OP_DSS: {
+      WCur c;
+      wc_init(c, up, un);
+      c.i = o[2];
+      bool cn;
+      uint32_t n, s0, ln;
+      wc_var_u32(c, n, cn);
+      w_var(w, n);
+      for (uint32_t q = 0; q < n; q++) {
+        wc_var_u32(c, s0, cn);
+        wc_var_u32(c, ln, cn);
+        w_var(w, s0);
+        w_var(w, ln);
+      }
+      break;
+    }
+    default: break;
+    }
+  }
+  // verbatim ranges: all lanes, coalesced
+  for (uint32_t k = 0; k < nops; k++) {
+    const uint32_t *o = ops + OPW * k;
+    if (o[0] != OP_COPY) continue;
+    const uint8_t *src = up + o[2];
+    uint8_t *q = dst + o[7];
+    const uint32_t len = o[1];
+    for (uint32_t j = lane; j < len; j += 64) q[j] = src[j];
+  }
+}
+
+void launch_plan(bool diff, int pass, const DiffBatch &b, const PlanScratch &ps, hipStream_t s) {
+  if (!b.n_docs) return;
+  dim3 g((b.n_docs + 63) / 64), t(64);
+  if (diff)
+    hipLaunchKernelGGL(k_plan<true>, g, t, 0, s, b, ps, pass);
+  else
+    hipLaunchKernelGGL(k_plan<false>, g, t, 0, s, b, ps, pass);
+}
+void launch_big_need(const uint64_t *upd_off, const uint8_t *big, uint32_t n, uint64_t *need, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_big_need, dim3((n + 255) / 256), dim3(256), 0, s, upd_off, big, n, need);
+}
+void launch_exec(const DiffBatch &b, const PlanScratch &ps, const uint64_t *out_off, uint8_t *out, hipStream_t s) {
+  if (!b.n_docs) return;
+  hipLaunchKernelGGL(k_exec, dim3((b.n_docs + 3) / 4), dim3(256), 0, s, b, ps, out_off, out);
+}
+
+} // namespace ym

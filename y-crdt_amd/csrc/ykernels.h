@@ -41,3 +41,30 @@ size_t scan_tmp_elems(uint32_t n);
 void launch_pack(const uint8_t *src, const uint64_t *start, const uint64_t *len, const uint64_t *pack_off,
                  uint8_t *dst, uint32_t n_docs, hipStream_t s);
 } // namespace ym
+
+namespace ym {
+// ---- diff_updates_v1 / encode_state_vector_from_update_v1 (ydiff.hip): one update per document
+struct DiffBatch {
+  const uint8_t *bytes;
+  const uint64_t *upd_off; // n_docs + 1
+  const uint8_t *sv;       // remote state vectors (diff only)
+  const uint64_t *sv_off;  // n_docs + 1 (diff only)
+  uint32_t n_docs;
+};
+struct PlanCaps {
+  uint32_t C, E, R, O; // client sections, DeleteSet entries, squash ranges, output ops
+};
+struct PlanScratch {
+  uint32_t *small;        // n_docs * small_words
+  uint64_t small_words;
+  uint32_t *bigscr;       // documents re-planned with capacities sized from their length
+  const uint64_t *big_off; // word offset per document into bigscr
+  uint8_t *big, *status;
+  uint64_t *size;
+  uint32_t *n_big;
+};
+uint64_t plan_small_words();
+void launch_plan(bool diff, int pass, const DiffBatch &b, const PlanScratch &ps, hipStream_t s);
+void launch_big_need(const uint64_t *upd_off, const uint8_t *big, uint32_t n, uint64_t *need, hipStream_t s);
+void launch_exec(const DiffBatch &b, const PlanScratch &ps, const uint64_t *out_off, uint8_t *out, hipStream_t s);
+} // namespace ym

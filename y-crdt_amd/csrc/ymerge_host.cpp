@@ -52,7 +52,7 @@ struct ymerge_ctx {
   hipStream_t s = nullptr;
   DevBuf in_bytes, in_upd_off, in_doc_upd, in_sv, in_sv_off;
   DevBuf status, path, out_start, out_len, pack_off, counts, need, scr_off, scratch, sizes, spill_off, scan_tmp;
-  DevBuf arena, packed, counter, stamps;
+  DevBuf arena, packed, counter, stamps, plan_small, plan_big;
   bool want_stamps = false;
   uint64_t *h_pinned = nullptr;
   hipEvent_t ev[6];
@@ -100,7 +100,8 @@ extern "C" void ymerge_ctx_destroy(ymerge_ctx *c) {
   if (c->s) hipStreamSynchronize(c->s);
   for (DevBuf *b : {&c->in_bytes, &c->in_upd_off, &c->in_doc_upd, &c->in_sv, &c->in_sv_off, &c->status, &c->path,
                     &c->out_start, &c->out_len, &c->pack_off, &c->counts, &c->need, &c->scr_off, &c->scratch,
-                    &c->sizes, &c->spill_off, &c->scan_tmp, &c->arena, &c->packed, &c->counter})
+                    &c->sizes, &c->spill_off, &c->scan_tmp, &c->arena, &c->packed, &c->counter, &c->stamps,
+                    &c->plan_small, &c->plan_big})
     b->release();
   if (c->h_pinned) hipHostFree(c->h_pinned);
   for (auto &e : c->ev)
@@ -223,13 +224,86 @@ extern "C" int ymerge_updates_v1_batch_device(ymerge_ctx *c, const uint8_t *d_by
   return merge_device(c, d_bytes, n_bytes, d_upd_off, d_doc_upd, n_docs, res);
 }
 
-extern "C" int yencode_state_vector_from_update_v1_batch_device(ymerge_ctx *, const uint8_t *, const uint64_t *,
-                                                                uint64_t, ymerge_device_result *) {
-  return YMERGE_ERR_UNSUPPORTED;
+// diff_updates_v1 / encode_state_vector_from_update_v1 over a batch (one update per document):
+// plan (small scratch) -> re-plan the overflowing documents with length-sized scratch ->
+// output offsets (scan) -> execute.
+static int plan_exec(ymerge_ctx *c, bool diff, const uint8_t *d_bytes, const uint64_t *d_upd_off,
+                     const uint8_t *d_sv, const uint64_t *d_sv_off, uint64_t n_docs, ymerge_device_result *res) {
+  if (hipSetDevice(c->device) != hipSuccess) return YMERGE_ERR_DEVICE;
+  if (n_docs > 0xFFFFFFFFull) return YMERGE_ERR_OTHER;
+  const uint32_t n = (uint32_t)n_docs;
+  const size_t nn = (size_t)n + 1;
+  const uint64_t sw = ym::plan_small_words();
+  if (!c->status.ensure(nn) || !c->path.ensure(nn) || !c->out_len.ensure(nn * 8) || !c->pack_off.ensure(nn * 8) ||
+      !c->need.ensure(nn * 8) || !c->spill_off.ensure(nn * 8) || !c->scan_tmp.ensure(ym::scan_tmp_elems(n) * 8 + 64) ||
+      !c->counter.ensure(64) || !c->plan_small.ensure(nn * sw * 4))
+    return YMERGE_ERR_DEVICE;
+  ym::DiffBatch b{d_bytes, d_upd_off, d_sv, d_sv_off, n};
+  ym::PlanScratch ps{c->plan_small.as<uint32_t>(), sw,       nullptr,
+                     c->spill_off.as<uint64_t>(), c->path.as<uint8_t>(), c->status.as<uint8_t>(),
+                     c->out_len.as<uint64_t>(),    c->counter.as<uint32_t>()};
+  hipMemsetAsync(c->counter.p, 0, 64, c->s);
+  hipEventRecord(c->ev[0], c->s);
+  ym::launch_plan(diff, 0, b, ps, c->s);
+  hipEventRecord(c->ev[1], c->s);
+  hipMemcpyAsync(c->h_pinned + 9, c->counter.p, 4, hipMemcpyDeviceToHost, c->s);
+  if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
+  const uint32_t n_big = (uint32_t)(c->h_pinned[9] & 0xFFFFFFFFu);
+  if (n_big) {
+    ym::launch_big_need(d_upd_off, ps.big, n, c->need.as<uint64_t>(), c->s);
+    ym::launch_scan_u64(c->need.as<uint64_t>(), c->spill_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
+    uint64_t words = 0;
+    if (!read_words(c, c->spill_off.as<uint64_t>() + n, 8, &words)) return YMERGE_ERR_DEVICE;
+    if (!c->plan_big.ensure(words * 4 + 64)) return YMERGE_ERR_DEVICE;
+    ps.bigscr = c->plan_big.as<uint32_t>();
+    ym::launch_plan(diff, 1, b, ps, c->s);
+  }
+  hipEventRecord(c->ev[2], c->s);
+  ym::launch_scan_u64(ps.size, c->pack_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
+  uint64_t total = 0;
+  if (!read_words(c, c->pack_off.as<uint64_t>() + n, 8, &total)) return YMERGE_ERR_DEVICE;
+  if (!c->arena.ensure(total + 64)) return YMERGE_ERR_DEVICE;
+  hipEventRecord(c->ev[4], c->s);
+  ym::launch_exec(b, ps, c->pack_off.as<uint64_t>(), c->arena.as<uint8_t>(), c->s);
+  hipEventRecord(c->ev[3], c->s);
+  if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
+  if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
+  float t01 = 0, t12 = 0, t43 = 0, t03 = 0;
+  hipEventElapsedTime(&t01, c->ev[0], c->ev[1]);
+  hipEventElapsedTime(&t12, c->ev[1], c->ev[2]);
+  hipEventElapsedTime(&t43, c->ev[4], c->ev[3]);
+  hipEventElapsedTime(&t03, c->ev[0], c->ev[3]);
+  c->stats = ymerge_stats{};
+  c->stats.n_docs = n_docs;
+  c->stats.bytes_out = total;
+  c->stats.docs_exact = n_big; // documents re-planned with length-sized scratch
+  c->stats.docs_fast = n_docs - n_big;
+  c->stats.ms_fast = t01;  // plan kernel (small pass)
+  c->stats.ms_exact = t12; // big re-plan pass (incl. its scan)
+  c->stats.ms_tail = t43;  // execute kernel
+  c->stats.ms_total = t03;
+  res->d_out = c->arena.as<uint8_t>();
+  res->d_out_start = c->pack_off.as<uint64_t>();
+  res->d_out_len = ps.size;
+  res->d_status = ps.status;
+  res->arena_bytes = c->arena.cap;
+  res->out_bytes = total;
+  return 0;
 }
-extern "C" int ydiff_updates_v1_batch_device(ymerge_ctx *, const uint8_t *, const uint64_t *, const uint8_t *,
-                                             const uint64_t *, uint64_t, ymerge_device_result *) {
-  return YMERGE_ERR_UNSUPPORTED;
+
+extern "C" int yencode_state_vector_from_update_v1_batch_device(ymerge_ctx *c, const uint8_t *d_bytes,
+                                                                const uint64_t *d_upd_off, uint64_t n_docs,
+                                                                ymerge_device_result *res) {
+  if (!c || !res) return YMERGE_ERR_OTHER;
+  std::lock_guard<std::mutex> g(c->mu);
+  return plan_exec(c, false, d_bytes, d_upd_off, nullptr, nullptr, n_docs, res);
+}
+extern "C" int ydiff_updates_v1_batch_device(ymerge_ctx *c, const uint8_t *d_bytes, const uint64_t *d_upd_off,
+                                             const uint8_t *d_sv, const uint64_t *d_sv_off, uint64_t n_docs,
+                                             ymerge_device_result *res) {
+  if (!c || !res) return YMERGE_ERR_OTHER;
+  std::lock_guard<std::mutex> g(c->mu);
+  return plan_exec(c, true, d_bytes, d_upd_off, d_sv, d_sv_off, n_docs, res);
 }
 
 static int pack_to_host(ymerge_ctx *c, const ymerge_device_result *res, uint64_t n_docs, uint8_t *out,
@@ -359,13 +433,103 @@ extern "C" char *ymerge_updates_v1(const char *const *updates, const uint32_t *u
   return res;
 }
 
-extern "C" char *ydiff_updates_v1(const char *, uint32_t, const char *, uint32_t, uint32_t *) {
-  g_last_error = YMERGE_ERR_UNSUPPORTED;
-  return nullptr;
+// host buffers of one (or more) documents -> device -> plan/exec -> host
+static int host_plan_exec(ymerge_ctx *c, bool diff, const uint8_t *bytes, const uint64_t *upd_off,
+                          const uint8_t *sv, const uint64_t *sv_off, uint64_t n_docs, ymerge_batch_result **out) {
+  std::lock_guard<std::mutex> g(c->mu);
+  hipSetDevice(c->device);
+  const uint64_t nbytes = upd_off[n_docs], nsv = diff ? sv_off[n_docs] : 0;
+  if (!c->in_bytes.ensure(nbytes + 16) || !c->in_upd_off.ensure((n_docs + 1) * 8) ||
+      (diff && (!c->in_sv.ensure(nsv + 16) || !c->in_sv_off.ensure((n_docs + 1) * 8))))
+    return YMERGE_ERR_DEVICE;
+  if (nbytes && hipMemcpyAsync(c->in_bytes.p, bytes, nbytes, hipMemcpyHostToDevice, c->s) != hipSuccess)
+    return YMERGE_ERR_DEVICE;
+  if (hipMemcpyAsync(c->in_upd_off.p, upd_off, (n_docs + 1) * 8, hipMemcpyHostToDevice, c->s) != hipSuccess)
+    return YMERGE_ERR_DEVICE;
+  if (diff) {
+    if (nsv && hipMemcpyAsync(c->in_sv.p, sv, nsv, hipMemcpyHostToDevice, c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
+    if (hipMemcpyAsync(c->in_sv_off.p, sv_off, (n_docs + 1) * 8, hipMemcpyHostToDevice, c->s) != hipSuccess)
+      return YMERGE_ERR_DEVICE;
+  }
+  ymerge_device_result dr{};
+  int st = plan_exec(c, diff, c->in_bytes.as<uint8_t>(), c->in_upd_off.as<uint64_t>(),
+                     diff ? c->in_sv.as<uint8_t>() : nullptr, diff ? c->in_sv_off.as<uint64_t>() : nullptr, n_docs,
+                     &dr);
+  if (st) return st;
+  auto *r = (ymerge_batch_result *)calloc(1, sizeof(ymerge_batch_result));
+  r->n_docs = n_docs;
+  r->out_bytes = dr.out_bytes;
+  r->out = (uint8_t *)malloc(dr.out_bytes + 1);
+  r->out_off = (uint64_t *)malloc((n_docs + 1) * 8);
+  r->status = (uint8_t *)malloc(n_docs + 1);
+  st = pack_to_host(c, &dr, n_docs, r->out, r->out_off, r->status);
+  if (st) {
+    ymerge_batch_result_destroy(r);
+    return st;
+  }
+  *out = r;
+  return 0;
 }
-extern "C" char *yencode_state_vector_from_update_v1(const char *, uint32_t, uint32_t *) {
-  g_last_error = YMERGE_ERR_UNSUPPORTED;
-  return nullptr;
+
+extern "C" int ydiff_updates_v1_batch(ymerge_ctx *c, const uint8_t *bytes, const uint64_t *upd_off,
+                                      const uint8_t *sv, const uint64_t *sv_off, uint64_t n_docs,
+                                      ymerge_batch_result **res) {
+  if (!c || !res) return YMERGE_ERR_OTHER;
+  return host_plan_exec(c, true, bytes, upd_off, sv, sv_off, n_docs, res);
+}
+extern "C" int yencode_state_vector_from_update_v1_batch(ymerge_ctx *c, const uint8_t *bytes,
+                                                         const uint64_t *upd_off, uint64_t n_docs,
+                                                         ymerge_batch_result **res) {
+  if (!c || !res) return YMERGE_ERR_OTHER;
+  return host_plan_exec(c, false, bytes, upd_off, nullptr, nullptr, n_docs, res);
+}
+
+static char *single_result(ymerge_batch_result *r, uint32_t *out_len) {
+  if (r->status[0]) {
+    g_last_error = r->status[0];
+    ymerge_batch_result_destroy(r);
+    return nullptr;
+  }
+  const uint64_t n = r->out_off[1] - r->out_off[0];
+  char *res = (char *)malloc(n ? n : 1);
+  memcpy(res, r->out + r->out_off[0], n);
+  *out_len = (uint32_t)n;
+  ymerge_batch_result_destroy(r);
+  return res;
+}
+
+extern "C" char *ydiff_updates_v1(const char *update, uint32_t update_len, const char *state_vector,
+                                  uint32_t sv_len, uint32_t *out_len) {
+  g_last_error = 0;
+  ymerge_ctx *c = default_ctx();
+  if (!c) {
+    g_last_error = YMERGE_ERR_DEVICE;
+    return nullptr;
+  }
+  const uint64_t uo[2] = {0, update_len}, so[2] = {0, sv_len};
+  ymerge_batch_result *r = nullptr;
+  int st = ydiff_updates_v1_batch(c, (const uint8_t *)update, uo, (const uint8_t *)state_vector, so, 1, &r);
+  if (st) {
+    g_last_error = (uint8_t)st;
+    return nullptr;
+  }
+  return single_result(r, out_len);
+}
+extern "C" char *yencode_state_vector_from_update_v1(const char *update, uint32_t update_len, uint32_t *out_len) {
+  g_last_error = 0;
+  ymerge_ctx *c = default_ctx();
+  if (!c) {
+    g_last_error = YMERGE_ERR_DEVICE;
+    return nullptr;
+  }
+  const uint64_t uo[2] = {0, update_len};
+  ymerge_batch_result *r = nullptr;
+  int st = yencode_state_vector_from_update_v1_batch(c, (const uint8_t *)update, uo, 1, &r);
+  if (st) {
+    g_last_error = (uint8_t)st;
+    return nullptr;
+  }
+  return single_result(r, out_len);
 }
 
 extern "C" void ybinary_destroy(char *ptr, uint32_t) { free(ptr); }

@@ -167,3 +167,103 @@ def trace_updates(path=None, client=1):
     _L().yw_free(b)
     _L().yw_free(uo)
     return Batch(data, upd_off, np.array([0, len(pos)], np.uint64), name="C1"), d["endContent"]
+
+
+def _var(x):
+    out = bytearray()
+    while True:
+        b, x = x & 0x7F, x >> 7
+        if x:
+            out.append(b | 0x80)
+        else:
+            out.append(b)
+            return bytes(out)
+
+
+def _rv(b, i):
+    v = s = 0
+    while True:
+        x = b[i]
+        i += 1
+        v |= (x & 0x7F) << s
+        s += 7
+        if x < 0x80:
+            return v, i
+
+
+def parse_sv(b):
+    """Encoded state vector -> [(client, clock)] in stream order."""
+    n, i = _rv(b, 0)
+    out = []
+    for _ in range(n):
+        c, i = _rv(b, i)
+        k, i = _rv(b, i)
+        out.append((c, k))
+    return out
+
+
+def encode_sv(pairs):
+    return _var(len(pairs)) + b"".join(_var(c) + _var(k) for c, k in pairs)
+
+
+def remote_svs(sv_arena, sv_off, seed=0x5713):
+    """C5 remote state vectors: per document, each client's remote clock drawn from
+    {0, U[0, max), max - U[1, 8], max} (max = the document's own clock for that client).
+    Returns (bytes, offsets)."""
+    rng = np.random.default_rng(seed)
+    parts, offs, tot = [], [0], 0
+    for d in range(len(sv_off) - 1):
+        own = parse_sv(bytes(sv_arena[int(sv_off[d]):int(sv_off[d + 1])]))
+        pairs = []
+        for c, mx in own:
+            k = int(rng.integers(4))
+            if k == 0:
+                v = 0
+            elif k == 1:
+                v = int(rng.integers(0, max(1, mx)))
+            elif k == 2:
+                v = max(0, mx - int(rng.integers(1, 9)))
+            else:
+                v = mx
+            pairs.append((c, v))
+        rng.shuffle(pairs)
+        e = encode_sv(pairs)
+        parts.append(e)
+        tot += len(e)
+        offs.append(tot)
+    return np.frombuffer(b"".join(parts) or b"\0", dtype=np.uint8)[:tot].copy(), np.array(offs, np.uint64)
+
+
+class DiffBatch:
+    """One update per document (+ one remote state vector per document for diff)."""
+
+    def __init__(self, data, upd_off, sv=None, sv_off=None, name=""):
+        self.data, self.upd_off, self.sv, self.sv_off, self.name = data, upd_off, sv, sv_off, name
+
+    @property
+    def n_docs(self):
+        return len(self.upd_off) - 1
+
+    @property
+    def n_bytes(self):
+        return int(self.upd_off[-1])
+
+    def update(self, d):
+        return self.data[int(self.upd_off[d]):int(self.upd_off[d + 1])].tobytes()
+
+
+def compacted_docs(merged, offs, status=None, seed=0x5713, sv_fn=None):
+    """C5 input from merged (compacted) documents: the merge outputs become the updates,
+    remote state vectors are drawn against each document's own state vector (sv_fn:
+    (data, off) -> (sv arena, sv offsets, status); the oracle or the engine)."""
+    data = np.frombuffer(merged, dtype=np.uint8) if isinstance(merged, (bytes, bytearray)) else merged
+    offs = np.asarray(offs, np.uint64)
+    if status is not None and (np.asarray(status) != 0).any():
+        keep = [d for d in range(len(offs) - 1) if status[d] == 0]
+        parts = [data[int(offs[d]):int(offs[d + 1])] for d in keep]
+        lens = np.array([len(p) for p in parts], np.uint64)
+        offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+        data = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+    sv, sv_off, st = sv_fn(data, offs)
+    rsv, rsv_off = remote_svs(np.frombuffer(sv, np.uint8) if isinstance(sv, bytes) else sv, sv_off, seed)
+    return DiffBatch(np.ascontiguousarray(data), offs, rsv, rsv_off, name="C5")

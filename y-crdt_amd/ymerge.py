@@ -75,6 +75,9 @@ def lib():
     L.yencode_state_vector_from_update_v1.argtypes = [c.c_char_p, u32, c.POINTER(u32)]
     L.ybinary_destroy.argtypes = [vp, u32]
     L.ymerge_last_error.restype = c.c_uint8
+    L.ydiff_updates_v1_batch.argtypes = [vp, vp, vp, vp, vp, u64, c.POINTER(c.c_void_p)]
+    L.yencode_state_vector_from_update_v1_batch.argtypes = [vp, vp, vp, u64, c.POINTER(c.c_void_p)]
+    L.ymerge_batch_result_destroy.argtypes = [vp]
     _lib = L
     return L
 
@@ -182,6 +185,30 @@ class Engine:
         s = _Stats()
         lib().ymerge_last_stats(self._ctx, ctypes.byref(s))
         return {k: getattr(s, k) for k, _ in _Stats._fields_}
+
+    def _host_batch(self, args_dev, fn):
+        import torch
+        dev = torch.device("cuda", self.device)
+        ts = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in args_dev]
+        torch.cuda.synchronize(dev)
+        r = fn(*[t.data_ptr() for t in ts])
+        return r.to_host()
+
+    def diff_host(self, ubytes, u_off, svbytes, sv_off):
+        """Batched diff_updates_v1: document d = (update d, remote state vector d)."""
+        n = len(u_off) - 1
+        ub = np.ascontiguousarray(ubytes, dtype=np.uint8)
+        sb = np.ascontiguousarray(svbytes, dtype=np.uint8)
+        args = [ub if len(ub) else np.zeros(1, np.uint8), np.asarray(u_off, np.uint64).view(np.int64),
+                sb if len(sb) else np.zeros(1, np.uint8), np.asarray(sv_off, np.uint64).view(np.int64)]
+        return self._host_batch(args, lambda a, b, c, d: self.diff_device(a, b, c, d, n))
+
+    def state_vector_host(self, ubytes, u_off):
+        """Batched encode_state_vector_from_update_v1 (one update per document)."""
+        n = len(u_off) - 1
+        ub = np.ascontiguousarray(ubytes, dtype=np.uint8)
+        args = [ub if len(ub) else np.zeros(1, np.uint8), np.asarray(u_off, np.uint64).view(np.int64)]
+        return self._host_batch(args, lambda a, b: self.state_vector_device(a, b, n))
 
     # convenience: host arrays in, host arrays out (uses torch for HBM residency)
     def merge_host(self, data, upd_off, doc_upd):
