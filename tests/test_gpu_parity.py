@@ -134,7 +134,7 @@ def test_exact_engine_only(oracle):
         e.close()
 
 
-@pytest.mark.parametrize("threads", ["256", "1024"])
+@pytest.mark.parametrize("threads", ["512", "1024"])
 def test_fast_path_workgroup_sizes(oracle, threads):
     import ymerge
     os.environ["YMERGE_FAST_THREADS"] = threads

@@ -11,13 +11,13 @@ import numpy as np  # noqa: E402
 import workloads  # noqa: E402
 import ymerge  # noqa: E402
 
-NAMES = ["stage", "walk1", "scan", "walk2", "sort", "classify", "sizes", "write", "ds_sort", "ds_order",
-         "ds_rsort", "ds_union", "ds_write"]
+NAMES = ["decode", "-", "sort", "classify", "sizes", "write", "ds_clients", "ds_order", "ds_rsort", "ds_union",
+         "ds_write"]
 
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
-    threads = os.environ.get("YMERGE_FAST_THREADS", "512")
+    threads = os.environ.get("YMERGE_FAST_THREADS", "256")
     b = workloads.text_docs(n, 1000)
     e = ymerge.Engine(0)
     e.merge_host(b.data, b.upd_off, b.doc_upd)
@@ -25,10 +25,14 @@ def main():
     L.ymerge_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
     st = np.zeros((n, 16), np.uint64)
     assert L.ymerge_debug_stamps(e._ctx, n, st.ctypes.data) == 0
-    ok = st[:, 13] > 0
-    d = np.diff(st[ok][:, :14].astype(np.int64), axis=1)
+    ok = st[:, 11] > 0
+    d = np.diff(st[ok][:, :12].astype(np.int64), axis=1)
     tot = d.sum(axis=1).mean()
     print(f"threads/WG {threads}: {ok.sum()} fast docs, mean {tot:.0f} cycles per doc")
+    r = st[ok].astype(np.int64)
+    print("  round 0: exact-walk fallbacks %.1f lanes, staging %.0f, parse %.0f, scan %.0f (cycles)" % (
+        r[:, 12].mean(), (r[:, 13] - r[:, 0]).mean(), (r[:, 14] - r[:, 13]).mean(),
+        (r[:, 15] - r[:, 14]).mean()))
     for i, nm in enumerate(NAMES):
         print(f"  {nm:10s} {d[:, i].mean():10.0f} cycles  {100 * d[:, i].mean() / tot:5.1f}%")
 

@@ -1,0 +1,155 @@
+// ylds.h — fast-shape decode of one v1 update staged in LDS.
+//
+// A round of NT consecutive updates of a document is one contiguous byte range in
+// HBM; the workgroup copies it into LDS with coalesced dword loads, then every lane
+// decodes its own update from LDS.  Varints are read branch-free: two dword reads
+// (ds_read2_b32) cover the <= 5 bytes of a u32 LEB128, the terminator is found with
+// a ctz over the continuation bits, so lanes stay converged whatever the varint
+// lengths.  The shapes handled are the ones a text editor emits (one client section
+// with one GC / Skip / Deleted / String block, any DeleteSet); anything else, and any
+// malformed input, bails out (-1) and the caller runs the exact walk (ysm.h), which
+// also owns the error codes.  Semantics follow Update::decode_v1
+// (yrs/src/update.rs:714-749, 433-488), ItemContent::decode (yrs/src/block.rs:1786-1835)
+// and IdSet::decode (yrs/src/id_set.rs:412-426), exactly as ysm.h restates them.
+#pragma once
+#include "ycodec.h"
+
+namespace ym {
+
+struct LCur {
+  const uint32_t *w; // staged dwords
+  uint32_t p, end;   // byte position / end (exclusive) within the staged buffer
+};
+YM_INLINE uint32_t lds_byte(const uint32_t *w, uint32_t p) { return (w[p >> 2] >> ((p & 3) * 8)) & 0xFF; }
+
+// one LEB128 u32 (<= 5 bytes) with yrs' wrapping_shl semantics; false = bail
+YM_INLINE bool lvar(LCur &c, uint32_t &v, bool &canon) {
+  const uint32_t q = c.p >> 2, sh = (c.p & 3) * 8;
+  const uint64_t d = ((uint64_t)c.w[q + 1] << 32) | c.w[q];
+  const uint32_t x = (uint32_t)(d >> sh);
+  const uint32_t b4 = (uint32_t)(d >> (sh + 32)) & 0xFF;
+  const uint32_t stop = ~x & 0x80808080u;
+  uint32_t len;
+  if (stop) {
+    len = (__builtin_ctz(stop) >> 3) + 1;
+  } else {
+    if (b4 & 0x80) return false; // longer than 5 bytes: exact walk
+    len = 5;
+  }
+  if (c.p + len > c.end) return false;
+  uint32_t val = (x & 0x7Fu) | ((x >> 1) & 0x3F80u) | ((x >> 2) & 0x1FC000u) | ((x >> 3) & 0xFE00000u);
+  if (len < 4) val &= (1u << (7 * len)) - 1;
+  else if (len == 5) val |= (b4 & 0x7Fu) << 28;
+  const uint32_t last = len == 5 ? b4 : (x >> (8 * (len - 1))) & 0xFF;
+  canon = len == varlen(val) && (len != 5 || last < 16);
+  v = val;
+  c.p += len;
+  return true;
+}
+
+// Decodes one staged update into the sink.  Returns 0, a sink error, or -1 (bail).
+template <class S> YM_INLINE int fast_walk(const uint32_t *w, uint32_t start, uint32_t n, S &s) {
+  LCur c{w, start, start + n};
+  bool cn;
+  uint32_t ncl, nds;
+  if (!lvar(c, ncl, cn)) return -1;
+  if (ncl > 1) return -1;
+  if (ncl == 1) {
+    uint32_t nb, client, clock;
+    if (!lvar(c, nb, cn) || !lvar(c, client, cn) || !lvar(c, clock, cn)) return -1;
+    if (nb > 1) return -1;
+    s.on_section(client);
+    if (nb == 1) {
+      const uint32_t bpos = c.p;
+      if (c.p >= c.end) return -1;
+      const uint32_t info = lds_byte(w, c.p++);
+      BlockInfo bi;
+      bi.info = (uint8_t)info;
+      bi.reenc = bi.unsupported = bi.enc_panic = false;
+      bi.canon = 0;
+      uint32_t v;
+      if (info == 10 || info == 0) {
+        bi.kind = info == 10 ? BK_SKIP : BK_GC;
+        bi.ref = 0;
+        if (!lvar(c, bi.len, cn)) return -1;
+        bi.reenc = !cn;
+      } else {
+        bi.kind = BK_ITEM;
+        uint32_t want = info & 0xCF;
+        bool ok = true;
+        if (info & 0x80) {
+          ok = lvar(c, v, cn) && (bi.reenc |= !cn, lvar(c, v, cn)) && (bi.reenc |= !cn, true);
+        }
+        if (ok && (info & 0x40)) {
+          ok = lvar(c, v, cn) && (bi.reenc |= !cn, lvar(c, v, cn)) && (bi.reenc |= !cn, true);
+        }
+        if (!ok) return -1;
+        if ((info & 0xC0) == 0) {
+          uint32_t pi;
+          if (!lvar(c, pi, cn)) return -1;
+          bi.reenc |= !cn || (pi != 1 && pi != 0);
+          if (!lvar(c, v, cn)) return -1;
+          bi.reenc |= !cn;
+          if (pi == 1) {
+            if (v > c.end - c.p) return -1;
+            c.p += v;
+          } else {
+            if (!lvar(c, v, cn)) return -1;
+            bi.reenc |= !cn;
+          }
+          if (info & 0x20) {
+            want |= 0x20;
+            if (!lvar(c, v, cn)) return -1;
+            bi.reenc |= !cn;
+            if (v > c.end - c.p) return -1;
+            c.p += v;
+          }
+        }
+        if (want != info) bi.reenc = true;
+        const uint32_t ref = info & 15;
+        bi.ref = (uint8_t)ref;
+        if (ref == 1) {
+          if (!lvar(c, bi.len, cn)) return -1;
+          bi.reenc |= !cn;
+        } else if (ref == 4) {
+          if (!lvar(c, v, cn)) return -1;
+          bi.reenc |= !cn;
+          if (v > c.end - c.p) return -1;
+          const uint32_t s0 = c.p;
+          c.p += v;
+          if (v == 1) {
+            bi.len = 1;
+          } else {
+            uint32_t hi = 0;
+            for (uint32_t q = 0; q < v; q++) hi |= lds_byte(w, s0 + q);
+            if (hi >= 0x80) return -1; // UTF-16 length of non-ASCII text: exact walk
+            bi.len = v;
+          }
+        } else {
+          return -1;
+        }
+      }
+      if (!(bi.kind == BK_ITEM && bi.len == 0)) {
+        if ((uint64_t)clock + bi.len > 0xFFFFFFFFull) return -1;
+        YM_TRY(s.on_block(client, clock, bi, bpos - start, c.p - bpos));
+      }
+    }
+  }
+  if (!lvar(c, nds, cn)) return -1;
+  YM_TRY(s.on_ds_begin(nds));
+  for (uint32_t i = 0; i < nds; i++) {
+    uint32_t client, nr;
+    if (!lvar(c, client, cn) || !lvar(c, nr, cn)) return -1;
+    if (nr > n) return -1; // cannot fit: let the exact walk report it
+    YM_TRY(s.on_ds_entry(client, nr));
+    for (uint32_t k = 0; k < nr; k++) {
+      uint32_t st, ln;
+      if (!lvar(c, st, cn) || !lvar(c, ln, cn)) return -1;
+      if ((uint64_t)st + ln > 0xFFFFFFFFull) return -1;
+      s.on_ds_range(st, st + ln);
+    }
+  }
+  return s.on_ds_done();
+}
+
+} // namespace ym

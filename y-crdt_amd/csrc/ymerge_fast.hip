@@ -20,6 +20,8 @@
 #include "ycodec.h"
 #include "ykernels.h"
 #include "ywalk.h"
+#include "ysm.h"
+#include "ylds.h"
 
 namespace ym {
 
@@ -29,9 +31,8 @@ namespace ym {
 //   phase 3/4/6 (blocks): sort keys, classify flags, per-position output offsets
 //   phase 5 (DeleteSet): sort keys, union flags/offsets, per-client tables
 struct FastLayout {
-  uint32_t in, uoff, bc, bk, bl, bp, bm, ec, et, rs, re, ri;
-  uint32_t cB, cE, cR;
-  uint32_t skey, sval, sE, sf, sz, sseg;
+  uint32_t bc, bk, bl, bp, bm, ec, et, rs, re, ri;
+  uint32_t stage, skey, sval, sE, sf, sz, sseg;
   uint32_t dkey, dval, cend, coff, chead, dcl, dfirst, dord, dnc, dbeg, doff, dtab;
   uint32_t misc, total;
 };
@@ -40,6 +41,7 @@ __host__ __device__ inline uint32_t pow2ceil(uint32_t x) {
   while (p < x) p <<= 1;
   return p;
 }
+constexpr uint32_t STAGE_BYTES = 16384; // LDS staging of one decode round
 constexpr uint32_t BTAB = 64; // client table of the counting sort (<= 8 distinct clients used)
 __host__ __device__ inline FastLayout fast_layout(const FastCaps &c) {
   FastLayout L;
@@ -50,8 +52,6 @@ __host__ __device__ inline FastLayout fast_layout(const FastCaps &c) {
     return r;
   };
   const uint32_t BS = pow2ceil(c.b_cap), RS = pow2ceil(c.r_cap > c.e_cap ? c.r_cap : c.e_cap);
-  L.in = take(c.in_cap + 16);
-  L.uoff = take(4 * (c.u_cap + 1));
   L.bc = take(4 * c.b_cap);
   L.bk = take(4 * c.b_cap);
   L.bl = take(4 * c.b_cap);
@@ -64,10 +64,9 @@ __host__ __device__ inline FastLayout fast_layout(const FastCaps &c) {
   L.ri = take(4 * c.r_cap);
   L.misc = take(4 * 256 + 8 * BTAB);
   const uint32_t u0 = o;
-  L.cB = take(4 * (c.u_cap + 1));
-  L.cE = take(4 * (c.u_cap + 1));
-  L.cR = take(4 * (c.u_cap + 1));
   uint32_t end = o;
+  L.stage = take(STAGE_BYTES + 16);
+  if (o > end) end = o;
   o = u0;
   L.skey = take(8 * BS);
   L.sval = take(4 * BS);
@@ -83,11 +82,11 @@ __host__ __device__ inline FastLayout fast_layout(const FastCaps &c) {
   L.coff = take(4 * (RS + 1));
   L.chead = take(4 * (RS + 1));
   L.dcl = take(4 * (c.e_cap + 1)); // per distinct client (D <= NE)
-  L.dfirst = take(4 * (c.e_cap + 1)); // per distinct client (D <= NE)
-  L.dord = take(4 * (c.e_cap + 1)); // per distinct client (D <= NE)
-  L.dnc = take(4 * (c.e_cap + 1)); // per distinct client (D <= NE)
-  L.dbeg = take(4 * (c.e_cap + 1)); // per distinct client (D <= NE)
-  L.doff = take(4 * (c.e_cap + 1)); // per distinct client (D <= NE)
+  L.dfirst = take(4 * (c.e_cap + 1));
+  L.dord = take(4 * (c.e_cap + 1));
+  L.dnc = take(4 * (c.e_cap + 1));
+  L.dbeg = take(4 * (c.e_cap + 1));
+  L.doff = take(4 * (c.e_cap + 1));
   L.dtab = take(8 * (2 * pow2ceil(c.e_cap) > RS ? 2 * pow2ceil(c.e_cap) : RS));
   if (o > end) end = o;
   L.total = end;
@@ -236,47 +235,65 @@ template <int NT> YM_INLINE void bitonic(uint64_t *k, uint32_t *v, uint32_t n) {
 }
 
 // ------------------------------------------------------------------ walk sinks
-struct FastCount {
+// One walk per update.  The common shapes (<= 1 block, <= 1 DeleteSet entry with <= 2
+// ranges) are kept in registers until the round's scan places them; any other update
+// is re-walked once by FastFill at its scanned positions.
+struct RegSink {
   uint32_t nb, ne, nr;
   bool unsupported, big_ds;
+  uint32_t b_client, b_clock, b_len, b_pos, b_meta; // first block
+  uint32_t e_client;                                // first DeleteSet entry
+  uint32_t r0s, r0e, r1s, r1e;                      // its first two ranges
+  const uint8_t *doc;
+  uint32_t doc_len, ubase;
   YM_INLINE void on_section(uint32_t) {}
-  YM_INLINE int on_block(uint32_t, uint32_t, const BlockInfo &bi, uint32_t, uint32_t) {
-    if (bi.kind != BK_SKIP) nb++;
+  YM_INLINE int on_block(uint32_t client, uint32_t clock, const BlockInfo &bi, uint32_t bpos, uint32_t blen) {
     if (bi.unsupported) unsupported = true;
+    if (bi.kind == BK_SKIP) return 0;
+    if (nb == 0) {
+      b_client = client;
+      b_clock = clock;
+      b_len = bi.len;
+      b_pos = ubase + bpos;
+      b_meta = (uint32_t)bi.kind | (bi.reenc ? 4u : 0u) | (bi.enc_panic ? 8u : 0u) | (blen << 8);
+    }
+    nb++;
     return 0;
   }
   YM_INLINE int on_ds_begin(uint32_t nds) {
     if (nds > DS_SMALL) big_ds = true; // table emulation beyond 16 buckets: exact engine
     return 0;
   }
-  YM_INLINE int on_ds_entry(uint32_t, uint32_t) {
+  YM_INLINE int on_ds_entry(uint32_t client, uint32_t) {
+    if (ne == 0) e_client = client;
     ne++;
     return 0;
   }
-  YM_INLINE void on_ds_range(uint32_t, uint32_t) { nr++; }
+  YM_INLINE void on_ds_range(uint32_t s0, uint32_t e0) {
+    if (nr == 0) {
+      r0s = s0;
+      r0e = e0;
+    } else if (nr == 1) {
+      r1s = s0;
+      r1e = e0;
+    }
+    nr++;
+  }
   YM_INLINE int on_ds_done() { return 0; }
 };
 
 struct FastFill {
   uint32_t *bc, *bk, *bl, *bp, *bm, *ec, *et, *rs, *re, *ri;
-  const uint8_t *doc;
-  uint32_t doc_len, upd, ubase; // update index, byte offset of update within doc
+  uint32_t upd, ubase; // update index, byte offset of update within doc
   uint32_t nb, ne, nr, ebase;
   YM_INLINE void on_section(uint32_t) {}
   YM_INLINE int on_block(uint32_t client, uint32_t clock, const BlockInfo &bi, uint32_t bpos, uint32_t blen) {
     if (bi.kind == BK_SKIP) return 0;
-    uint32_t pos = ubase + bpos;
-    uint32_t canon = blen;
-    if (bi.reenc && !bi.enc_panic) {
-      Counter cn;
-      emit_block(doc, doc_len, pos, client, clock, bi.len, 0, cn);
-      canon = (uint32_t)cn.n;
-    }
     bc[nb] = client;
     bk[nb] = clock;
     bl[nb] = bi.len;
-    bp[nb] = pos | (blen << 16);
-    bm[nb] = (uint32_t)bi.kind | (bi.reenc ? 4u : 0u) | (bi.enc_panic ? 8u : 0u) | (canon << 8);
+    bp[nb] = ubase + bpos;
+    bm[nb] = (uint32_t)bi.kind | (bi.reenc ? 4u : 0u) | (bi.enc_panic ? 8u : 0u) | (blen << 8);
     nb++;
     return 0;
   }
@@ -298,7 +315,7 @@ struct FastFill {
   }
   YM_INLINE int on_ds_done() {
     uint32_t n = ne - ebase;
-    if (n >= 2) { // (n <= DS_SMALL here: walk 1 handed larger tables to the exact engine)
+    if (n >= 2) { // (n <= DS_SMALL here: larger tables go to the exact engine)
       ds_small_order(ec + ebase, n, et + ebase);
       for (uint32_t i = 0; i < n; i++) {
         uint32_t p = et[ebase + i];
@@ -308,6 +325,15 @@ struct FastFill {
     return 0;
   }
 };
+
+// canonical encoded size of a kept block (bm: kind | reenc 4 | panic 8 | input bytes << 8)
+__device__ __forceinline__ uint32_t canon_size(const uint8_t *doc, uint32_t doc_len, uint32_t pos, uint32_t client,
+                                               uint32_t clock, uint32_t len, uint32_t meta) {
+  if (!(meta & 4) || (meta & 8)) return meta >> 8;
+  Counter cn;
+  emit_block(doc, doc_len, pos, client, clock, len, 0, cn);
+  return (uint32_t)cn.n;
+}
 
 // ------------------------------------------------------------------ the kernel
 // Diagnostic build only (STAMPS=true, env YMERGE_STAMPS): lane 0 records s_memtime at
@@ -338,63 +364,139 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
   const uint32_t nbytes = (uint32_t)(B1 - B0);
   const uint64_t slot = 2 * B0 + 64ull * d;
   const uint64_t cap = 2ull * nbytes + 64;
-  if (U > caps.u_cap || nbytes > caps.in_cap) {
+  const uint8_t *in = b.bytes + B0; // document bytes stay in HBM; lanes read them through WCur
+  auto handover = [&]() {
     if (t == 0) {
       o.path[d] = 1;
       o.status[d] = 0;
       o.out_len[d] = 0;
       o.out_start[d] = slot;
     }
+  };
+  if (B1 - B0 >= (1ull << 31)) {
+    handover();
     return;
   }
-  YM_STAMP(0);
-  // ---- 1 stage bytes (word copy + byte tail) and update offsets
-  uint8_t *in = smem + L.in;
-  {
-    const uint64_t a0 = B0 & ~3ull;
-    const uint32_t shift = (uint32_t)(B0 - a0);
-    const uint32_t nfull = (uint32_t)((B1 - a0) / 4);
-    const uint32_t *src = (const uint32_t *)(b.bytes + a0);
-    uint32_t *dst = (uint32_t *)in;
-    for (uint32_t k = t; k < nfull; k += NT) dst[k] = src[k];
-    for (uint64_t q = a0 + 4ull * nfull + t; q < B1; q += NT) in[q - a0] = b.bytes[q];
-    in += shift; // doc byte j at in[j]
-  }
-  uint32_t *uoff = (uint32_t *)(smem + L.uoff);
-  for (uint32_t i = t; i <= U; i += NT) uoff[i] = (uint32_t)(b.upd_off[u0 + i] - B0);
   if (t == 0) {
     misc[0] = 0xFFFFFFFFu;
     misc[1] = 0;
   }
+  YM_STAMP(0);
+  uint32_t *bc = (uint32_t *)(smem + L.bc), *bk = (uint32_t *)(smem + L.bk), *bl = (uint32_t *)(smem + L.bl),
+           *bp = (uint32_t *)(smem + L.bp), *bm = (uint32_t *)(smem + L.bm);
+  uint32_t *ec = (uint32_t *)(smem + L.ec), *et = (uint32_t *)(smem + L.et);
+  uint32_t *rs = (uint32_t *)(smem + L.rs), *re = (uint32_t *)(smem + L.re), *ri = (uint32_t *)(smem + L.ri);
+  // ---- 1 decode: rounds of NT updates, one walk per update (register window over HBM);
+  //      the round's counts are scanned and every lane writes its records in update order
+  uint32_t NB = 0, NE = 0, NR = 0;
+  uint32_t flags = 0; // 1 unsupported, 2 big DS table, 4 capacity, 8 huge block
   __syncthreads();
-
-  YM_STAMP(1);
-  // ---- 2a walk: counts, first error, unsupported
-  uint32_t *cB = (uint32_t *)(smem + L.cB), *cE = (uint32_t *)(smem + L.cE), *cR = (uint32_t *)(smem + L.cR);
-  {
-    FastCount s;
-    s.unsupported = s.big_ds = false;
-    for (uint32_t i = t; i < U; i += NT) {
-      s.nb = s.ne = s.nr = 0;
-      int e = walk_update(in + uoff[i], uoff[i + 1] - uoff[i], s);
-      if (e) atomicMin(&misc[0], (i << 8) | (uint32_t)e);
-      cB[i] = s.nb;
-      cE[i] = s.ne;
-      cR[i] = s.nr;
+  uint32_t *stage = (uint32_t *)(smem + L.stage);
+  for (uint32_t r0 = 0; r0 < U; r0 += NT) {
+    const uint32_t i = r0 + t;
+    // stage the round's bytes [A, E) into LDS (coalesced dwords, at most STAGE_BYTES)
+    if (t == 0) {
+      const uint32_t rl = U - r0 < NT ? U - r0 : NT;
+      sc[4] = (uint32_t)(b.upd_off[u0 + r0] - B0);
+      sc[5] = (uint32_t)(b.upd_off[u0 + r0 + rl] - B0);
     }
-    if (s.unsupported || s.big_ds) atomicOr(&misc[1], (s.unsupported ? 1u : 0u) | (s.big_ds ? 2u : 0u));
-  }
-  __syncthreads();
-  {
-    uint32_t ek = misc[0];
-    const uint32_t fl = misc[1];
-    if (ek == 0xFFFFFFFFu && (fl & 2)) { // an update with > DS_SMALL DeleteSet entries
-      if (t == 0) {
-        o.path[d] = 1;
-        o.status[d] = 0;
-        o.out_len[d] = 0;
-        o.out_start[d] = slot;
+    __syncthreads();
+    const uint64_t sbase = (B0 + sc[4]) & ~3ull; // absolute, dword aligned
+    uint64_t nd = (B0 + sc[5] - sbase + 3) >> 2;
+    if (nd > STAGE_BYTES / 4) nd = STAGE_BYTES / 4;
+    for (uint32_t k = t; k < nd; k += NT) stage[k] = ((const uint32_t *)(b.bytes + sbase))[k];
+    __syncthreads();
+    if (STAMPS && r0 == 0 && t == 0) o.stamps[(size_t)blockIdx.x * 16 + 13] = __builtin_amdgcn_s_memtime();
+    RegSink s;
+    s.nb = s.ne = s.nr = 0;
+    s.unsupported = s.big_ds = false;
+    uint32_t ubase = 0, ulen = 0, lpos = 0;
+    bool staged = false;
+    int e = 0;
+    if (i < U) {
+      const uint64_t a0 = b.upd_off[u0 + i], a1 = b.upd_off[u0 + i + 1];
+      ubase = (uint32_t)(a0 - B0);
+      ulen = (uint32_t)(a1 - a0);
+      s.ubase = ubase;
+      lpos = (uint32_t)(a0 - sbase); // upd_off and sbase are offsets into b.bytes
+      staged = a1 - sbase <= 4 * nd;
+      e = staged ? fast_walk(stage, lpos, ulen, s) : -1;
+      if (STAMPS && e < 0 && r0 == 0) atomicAdd((unsigned long long *)&o.stamps[(size_t)blockIdx.x * 16 + 12], 1ull);
+      if (e < 0) { // not a fast shape (or malformed): exact walk over HBM
+        s.nb = s.ne = s.nr = 0;
+        s.unsupported = s.big_ds = false;
+        staged = false;
+        WCur c;
+        wc_init(c, in + ubase, ulen);
+        e = smwalk_update(c, s);
       }
+      if (e) atomicMin(&misc[0], (i << 8) | (uint32_t)e);
+      if (s.unsupported) flags |= 1;
+      if (s.big_ds) flags |= 2;
+      if (ulen >= (1u << 24)) flags |= 8;
+    }
+    if (STAMPS && r0 == 0) {
+      __syncthreads();
+      if (t == 0) o.stamps[(size_t)blockIdx.x * 16 + 14] = __builtin_amdgcn_s_memtime();
+    }
+    if (e) s.nb = s.ne = s.nr = 0;
+    // packed scan: blocks | entries << 21 | ranges << 42 (each < 2^21 per round)
+    uint64_t T;
+    const uint64_t pk = (uint64_t)s.nb | ((uint64_t)s.ne << 21) | ((uint64_t)s.nr << 42);
+    const uint64_t pre = bscan_sum64<NT>(pk, (uint64_t *)(misc + 2), T);
+    const uint32_t pb = NB + (uint32_t)(pre & 0x1FFFFF), pe = NE + (uint32_t)((pre >> 21) & 0x1FFFFF),
+                   pr = NR + (uint32_t)(pre >> 42);
+    NB += (uint32_t)(T & 0x1FFFFF);
+    NE += (uint32_t)((T >> 21) & 0x1FFFFF);
+    NR += (uint32_t)(T >> 42);
+    if (STAMPS && r0 == 0 && t == 0) o.stamps[(size_t)blockIdx.x * 16 + 15] = __builtin_amdgcn_s_memtime();
+    if (NB > caps.b_cap || NE > caps.e_cap || NR > caps.r_cap) {
+      flags |= 4;
+      break; // uniform: every lane sees the same totals
+    }
+    if (i < U && !e) {
+      if (s.nb <= 1 && s.ne <= 1 && s.nr <= 2) {
+        if (s.nb) {
+          bc[pb] = s.b_client;
+          bk[pb] = s.b_clock;
+          bl[pb] = s.b_len;
+          bp[pb] = s.b_pos;
+          bm[pb] = s.b_meta;
+        }
+        if (s.ne) {
+          ec[pe] = s.e_client;
+          et[pe] = 0x80000000u | (i << 8);
+          if (s.nr > 0) {
+            rs[pr] = s.r0s;
+            re[pr] = s.r0e;
+            ri[pr] = pe;
+          }
+          if (s.nr > 1) {
+            rs[pr + 1] = s.r1s;
+            re[pr + 1] = s.r1e;
+            ri[pr + 1] = pe;
+          }
+        }
+      } else if (!s.big_ds) {
+        FastFill f{bc, bk, bl, bp, bm, ec, et, rs, re, ri, i, ubase, pb, pe, pr, 0};
+        if (staged) {
+          fast_walk(stage, lpos, ulen, f);
+        } else {
+          WCur c;
+          wc_init(c, in + ubase, ulen);
+          smwalk_update(c, f);
+        }
+      }
+    }
+    __syncthreads(); // the next round re-stages
+  }
+  if (flags) atomicOr(&misc[1], flags);
+  __syncthreads();
+  YM_STAMP(1);
+  {
+    const uint32_t ek = misc[0], fl = misc[1];
+    if (ek == 0xFFFFFFFFu && (fl & 14)) { // big DS table, capacity, huge block: exact engine
+      handover();
       return;
     }
     if (ek != 0xFFFFFFFFu || fl) {
@@ -408,71 +510,6 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
     }
   }
   YM_STAMP(2);
-  // ---- 2b exclusive scans of the per-update counts (contiguous chunk per lane)
-  uint32_t NB, NE, NR;
-  {
-    const uint32_t per = (U + NT - 1) / NT, j0 = t * per, j1 = j0 + per < U ? j0 + per : U;
-    uint32_t sb = 0, se = 0, sr = 0;
-    for (uint32_t j = j0; j < j1; j++) {
-      sb += cB[j];
-      se += cE[j];
-      sr += cR[j];
-    }
-    uint32_t pb = bscan_sum<NT>(sb, ws, NB);
-    uint32_t pe = bscan_sum<NT>(se, ws, NE);
-    uint32_t pr = bscan_sum<NT>(sr, ws, NR);
-    for (uint32_t j = j0; j < j1; j++) {
-      uint32_t x = cB[j], y = cE[j], z = cR[j];
-      cB[j] = pb;
-      cE[j] = pe;
-      cR[j] = pr;
-      pb += x;
-      pe += y;
-      pr += z;
-    }
-  }
-  __syncthreads();
-  if (NB > caps.b_cap || NE > caps.e_cap || NR > caps.r_cap) {
-    if (t == 0) {
-      o.path[d] = 1;
-      o.status[d] = 0;
-      o.out_len[d] = 0;
-      o.out_start[d] = slot;
-    }
-    return;
-  }
-  uint32_t *bc = (uint32_t *)(smem + L.bc), *bk = (uint32_t *)(smem + L.bk), *bl = (uint32_t *)(smem + L.bl),
-           *bp = (uint32_t *)(smem + L.bp), *bm = (uint32_t *)(smem + L.bm);
-  uint32_t *ec = (uint32_t *)(smem + L.ec), *et = (uint32_t *)(smem + L.et);
-  uint32_t *rs = (uint32_t *)(smem + L.rs), *re = (uint32_t *)(smem + L.re), *ri = (uint32_t *)(smem + L.ri);
-  YM_STAMP(3);
-  // ---- 2c second walk: records at scanned positions
-  {
-    FastFill f;
-    f.bc = bc;
-    f.bk = bk;
-    f.bl = bl;
-    f.bp = bp;
-    f.bm = bm;
-    f.ec = ec;
-    f.et = et;
-    f.rs = rs;
-    f.re = re;
-    f.ri = ri;
-    f.doc = in;
-    f.doc_len = nbytes;
-    for (uint32_t i = t; i < U; i += NT) {
-      f.upd = i;
-      f.ubase = uoff[i];
-      f.nb = cB[i];
-      f.ne = cE[i];
-      f.nr = cR[i];
-      walk_update(in + uoff[i], uoff[i + 1] - uoff[i], f);
-    }
-  }
-  __syncthreads();
-
-  YM_STAMP(4);
   // ---- 3 sort blocks by (client desc, clock asc, input order).
   // Stable counting sort by client rank (<= 32 distinct clients: LDS table), then a
   // per-client clock-order check; LDS bitonic only when that check fails.
@@ -585,6 +622,7 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
       bitonic<NT>(skey, sval, n2);
     }
   }
+  YM_STAMP(3);
   // ---- 4 classify: per lane a contiguous chunk of sorted positions
   uint32_t *sE = (uint32_t *)(smem + L.sE), *sf = (uint32_t *)(smem + L.sf), *sz = (uint32_t *)(smem + L.sz);
   const uint32_t per = (NB + NT - 1) / NT, j0 = t * per, j1 = j0 + per < NB ? j0 + per : NB;
@@ -658,9 +696,9 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
         uint32_t kr = sval[last - 1];
         if (bk[kr] == bk[r]) {
           // same start: must be an exact duplicate (kind, length, bytes)
-          uint32_t pa = bp[kr] & 0xFFFF, la = bp[kr] >> 16, pb = bp[r] & 0xFFFF, lb = bp[r] >> 16;
+          uint32_t pa = bp[kr], la = bm[kr] >> 8, pb = bp[r], lb = bm[r] >> 8;
           bool same = la == lb && (bm[kr] & 3) == (bm[r] & 3) && bl[kr] == bl[r];
-          for (uint32_t q = 0; same && q < la; q++) same = in[pa + q] == in[pb + q];
+          if (same) same = equal_window(in + pa, in + pb, la);
           if (!same) viol = 1;
         }
       } else
@@ -693,7 +731,7 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
       return;
     }
   }
-  YM_STAMP(6);
+  YM_STAMP(4);
   // ---- 6a block section sizes: per client header + (Skip) + canonical block bytes
   uint32_t blocks_size, NC;
   uint32_t *sseg = (uint32_t *)(smem + L.sseg);
@@ -740,7 +778,7 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
         s += varlen(cnt) + varlen(bc[r]) + varlen(bk[r]);
       }
       if (sf[j] & 2) s += 1 + varlen(bk[r] - sE[j]);
-      if (sf[j] & 1) s += bm[r] >> 8;
+      if (sf[j] & 1) s += canon_size(in, nbytes, bp[r], bc[r], bk[r], bl[r], bm[r]);
       ls += s;
     }
     uint32_t tot;
@@ -753,14 +791,14 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
       uint32_t s = 0;
       if (head) s += varlen(sf[j] >> 8) + varlen(bc[r]) + varlen(bk[r]);
       if (sf[j] & 2) s += 1 + varlen(bk[r] - sE[j]);
-      if (sf[j] & 1) s += bm[r] >> 8;
+      if (sf[j] & 1) s += canon_size(in, nbytes, bp[r], bc[r], bk[r], bl[r], bm[r]);
       sz[j] = pos;
       pos += s;
     }
     blocks_size = base + tot;
     __syncthreads();
   }
-  YM_STAMP(7);
+  YM_STAMP(5);
   // ---- 6b write the block section into the document's slot
   uint8_t *out = o.out + slot;
   if (blocks_size <= cap) {
@@ -782,20 +820,20 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
         w_var(w, bk[r] - sE[j]);
       }
       if (sf[j] & 1) {
-        uint32_t p = bp[r] & 0xFFFF, len = bp[r] >> 16;
+        uint32_t p = bp[r], len = bm[r] >> 8;
         if (bm[r] & 4) {
           Writer w2 = w; // only the out-of-line re-encode takes a Writer by reference
           emit_block(in, nbytes, p, bc[r], bk[r], bl[r], 0, w2);
           w.n = w2.n;
         } else {
-          for (uint32_t q = 0; q < len; q++) w.p[w.n + q] = in[p + q];
+          copy_window(w.p + w.n, in + p, len);
         }
       }
     }
   }
   __syncthreads();
 
-  YM_STAMP(8);
+  YM_STAMP(6);
   // ---- 5 DeleteSet: distinct clients in yrs' table order, union of ranges
   uint64_t *dkey = (uint64_t *)(smem + L.dkey);
   uint32_t *dval = (uint32_t *)(smem + L.dval);
@@ -846,7 +884,7 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
     d_first[r] = (uint32_t)kj;
   }
   __syncthreads();
-  YM_STAMP(9);
+  YM_STAMP(7);
   // 5b yrs' table order (IdSet::merge inserts in first-occurrence order, hashbrown layout)
   if (t == 0) {
     // insertion order: sort ranks by first occurrence (insertion sort; D is small in practice)
@@ -924,7 +962,7 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
     }
     return;
   }
-  YM_STAMP(10);
+  YM_STAMP(8);
   // 5c ranges of live entries sorted by (client, start, index): rank sort, every lane
   //    counts the smaller keys with LDS broadcast reads (no barrier stages)
   {
@@ -964,7 +1002,7 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
     for (uint32_t j = t; j < NR; j += NT) c += dkey[j] != ~0ull;
     bscan_sum<NT>(c, ws, NL);
   }
-  YM_STAMP(11);
+  YM_STAMP(9);
   // 5d segmented union over sorted live ranges: comp heads, comp end, comp size at comp tails
   uint32_t *cmp_end = (uint32_t *)(smem + L.cend);
   uint32_t *cmp_off = (uint32_t *)(smem + L.coff);
@@ -1030,7 +1068,7 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
     if (t == 0) cmp_off[NL] = ds_comp_total;
   }
   __syncthreads();
-  YM_STAMP(12);
+  YM_STAMP(10);
   // 5e per distinct client (rank r, ascending client): range segment, #components, bytes
   // d_aux[0..D) holds iteration order; compute per-rank [rb, re) by binary search
   uint32_t *r_beg = (uint32_t *)(smem + L.dbeg);
@@ -1117,7 +1155,7 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
     o.out_len[d] = total;
     o.out_start[d] = slot;
   }
-  YM_STAMP(13);
+  YM_STAMP(11);
 }
 
 size_t fast_lds_bytes(const FastCaps &c) { return fast_layout(c).total; }

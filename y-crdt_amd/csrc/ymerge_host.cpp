@@ -57,8 +57,8 @@ struct ymerge_ctx {
   uint64_t *h_pinned = nullptr;
   hipEvent_t ev[6];
   ymerge_stats stats{};
-  ym::FastCaps caps{32768, 2048, 2048, 512, 1024}; // bytes, updates, blocks, DS entries, DS ranges
-  int fast_threads = 512;
+  ym::FastCaps caps{0, 0, 1024, 512, 512}; // (unused), (unused), blocks, DS entries, DS ranges
+  int fast_threads = 256;
   std::mutex mu;
 };
 
