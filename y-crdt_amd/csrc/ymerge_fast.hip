@@ -32,7 +32,7 @@ namespace ym {
 //   phase 5 (DeleteSet): sort keys, union flags/offsets, per-client tables
 struct FastLayout {
   uint32_t bc, bk, bl, bp, bm, ec, et, rs, re, ri;
-  uint32_t stage, skey, sval, sE, sf, sz, sseg;
+  uint32_t stage, skey, sval;
   uint32_t dkey, dval, cend, coff, chead, dcl, dfirst, dord, dnc, dbeg, doff, dtab;
   uint32_t misc, total;
 };
@@ -42,6 +42,9 @@ __host__ __device__ inline uint32_t pow2ceil(uint32_t x) {
   return p;
 }
 constexpr uint32_t STAGE_BYTES = 16384; // LDS staging of one decode round
+constexpr uint32_t FAST_BCAP = 1024;   // blocks per document on the fast path (caps.b_cap)
+constexpr uint32_t DCAP = 64;          // distinct DeleteSet clients per document on the fast path
+constexpr uint32_t DTAB_SLOTS = 256;   // LDS hash table for them
 constexpr uint32_t BTAB = 64; // client table of the counting sort (<= 8 distinct clients used)
 __host__ __device__ inline FastLayout fast_layout(const FastCaps &c) {
   FastLayout L;
@@ -70,10 +73,6 @@ __host__ __device__ inline FastLayout fast_layout(const FastCaps &c) {
   o = u0;
   L.skey = take(8 * BS);
   L.sval = take(4 * BS);
-  L.sE = take(4 * c.b_cap);
-  L.sf = take(4 * c.b_cap);
-  L.sz = take(4 * (c.b_cap + 1));
-  L.sseg = take(4 * (c.b_cap + 1));
   if (o > end) end = o;
   o = u0;
   L.dkey = take(8 * RS);
@@ -81,13 +80,13 @@ __host__ __device__ inline FastLayout fast_layout(const FastCaps &c) {
   L.cend = take(4 * (RS + 1));
   L.coff = take(4 * (RS + 1));
   L.chead = take(4 * (RS + 1));
-  L.dcl = take(4 * (c.e_cap + 1)); // per distinct client (D <= NE)
-  L.dfirst = take(4 * (c.e_cap + 1));
-  L.dord = take(4 * (c.e_cap + 1));
-  L.dnc = take(4 * (c.e_cap + 1));
-  L.dbeg = take(4 * (c.e_cap + 1));
-  L.doff = take(4 * (c.e_cap + 1));
-  L.dtab = take(8 * (2 * pow2ceil(c.e_cap) > RS ? 2 * pow2ceil(c.e_cap) : RS));
+  L.dcl = take(4 * (DCAP + 1)); // per distinct DeleteSet client (D <= DCAP)
+  L.dfirst = take(4 * (DCAP + 1));
+  L.dord = take(4 * (DCAP + 1));
+  L.dnc = take(4 * (DCAP + 1));
+  L.dbeg = take(4 * (DCAP + 1));
+  L.doff = take(4 * (DCAP + 1));
+  L.dtab = take(8 * (DTAB_SLOTS > RS ? DTAB_SLOTS : RS)); // client table, then range sort keys (NR)
   if (o > end) end = o;
   L.total = end;
   return L;
@@ -347,7 +346,8 @@ __device__ __forceinline__ uint32_t canon_size(const uint8_t *doc, uint32_t doc_
   } while (0)
 
 template <int NT, bool STAMPS>
-__global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, FastOut o) {
+__global__ void __launch_bounds__(NT, 4) k_fast_merge(BatchIn b, FastCaps caps, FastOut o) {
+  constexpr int PER = (int)(FAST_BCAP / NT); // sorted positions per lane (b_cap == FAST_BCAP)
   extern __shared__ __align__(16) uint8_t smem[];
   const FastLayout L = fast_layout(caps);
   const uint32_t d = blockIdx.x;
@@ -623,105 +623,116 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
     }
   }
   YM_STAMP(3);
-  // ---- 4 classify: per lane a contiguous chunk of sorted positions
-  uint32_t *sE = (uint32_t *)(smem + L.sE), *sf = (uint32_t *)(smem + L.sf), *sz = (uint32_t *)(smem + L.sz);
-  const uint32_t per = (NB + NT - 1) / NT, j0 = t * per, j1 = j0 + per < NB ? j0 + per : NB;
+  // ---- 4 register chunk: lane t owns sorted positions j = t*PER + k (k < PER); the
+  //      records are read once through sval into registers for classify, sizes, write
+  const uint32_t j0 = t * PER;
+  uint32_t rc[PER], rk[PER], rl[PER], rp[PER], rm[PER], rE[PER], rF[PER], rS[PER];
+  bool hd[PER];
   {
-    // segmented exclusive max of block ends (segments = clients)
+    bool havepc = false;
+    uint32_t pc = 0;
+    if (j0 > 0 && j0 < NB) {
+      pc = bc[sval[j0 - 1]];
+      havepc = true;
+    }
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      const uint32_t j = j0 + k;
+      rc[k] = rk[k] = rl[k] = rp[k] = rm[k] = rE[k] = rF[k] = rS[k] = 0;
+      hd[k] = false;
+      if (j < NB) {
+        const uint32_t r = sval[j];
+        rc[k] = bc[r];
+        rk[k] = bk[r];
+        rl[k] = bl[r];
+        rp[k] = bp[r];
+        rm[k] = bm[r];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      const uint32_t j = j0 + k;
+      if (k == 0) hd[0] = j < NB && (j == 0 || !havepc || pc != rc[0]);
+      else hd[k] = j < NB && rc[k] != rc[k - 1];
+    }
+  }
+  // classify: segmented exclusive max of block ends (segments = clients)
+  {
     uint32_t lf = 0, lv = 0;
-    for (uint32_t j = j0; j < j1; j++) {
-      uint32_t r = sval[j];
-      bool head = j == 0 || bc[sval[j - 1]] != bc[r];
-      uint32_t e = bk[r] + bl[r];
-      if (head) {
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      if (j0 + k >= NB) continue;
+      const uint32_t e = rk[k] + rl[k];
+      if (hd[k]) {
         lf = 1;
         lv = e;
-      } else
+      } else {
         lv = OpMax::f(lv, e);
+      }
     }
     uint32_t pf, pv;
     bscan_seg<NT, OpMax>(lf, lv, ws, pf, pv);
-    uint32_t run = pv; // running max of ends before j within the current segment
-    uint32_t viol = 0;
-    for (uint32_t j = j0; j < j1; j++) {
-      uint32_t r = sval[j];
-      bool head = j == 0 || bc[sval[j - 1]] != bc[r];
-      uint32_t k = bk[r], e = k + bl[r];
-      uint32_t E = head ? 0 : run;
+    uint32_t run = pv, viol = 0;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      if (j0 + k >= NB) continue;
+      const uint32_t e = rk[k] + rl[k];
+      const uint32_t E = hd[k] ? 0 : run;
       uint32_t flag = 0;
-      if (bl[r] == 0) viol = 1; // zero-length GC: leave to the exact engine
-      if (head || k >= E) {
-        flag = 1; // keep
-        if (!head && k > E) flag |= 2; // Skip of (k - E) before it
+      if (rl[k] == 0) viol = 1; // zero-length GC: leave to the exact engine
+      if (hd[k] || rk[k] >= E) {
+        flag = 1;                               // keep
+        if (!hd[k] && rk[k] > E) flag |= 2;     // Skip of (k - E) before it
       } else if (e > E) {
         viol = 1; // partial overlap
       }
-      sE[j] = E;
-      sf[j] = flag;
-      run = head ? e : OpMax::f(run, e);
+      rE[k] = E;
+      rF[k] = flag;
+      run = hd[k] ? e : OpMax::f(run, e);
     }
-    viol = __syncthreads_or(viol);
-    if (viol) {
-      if (t == 0) {
-        o.path[d] = 1;
-        o.status[d] = 0;
-        o.out_len[d] = 0;
-        o.out_start[d] = slot;
-      }
+    if (__syncthreads_or(viol)) {
+      handover();
       return;
     }
   }
   // dropped blocks must be covered with a later start, or byte-identical to the last kept block
   {
-    // last kept sorted index before j (segmented "max" of kept positions)
     uint32_t lf = 0, lv = 0;
-    for (uint32_t j = j0; j < j1; j++) {
-      uint32_t r = sval[j];
-      bool head = j == 0 || bc[sval[j - 1]] != bc[r];
-      if (head) {
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      if (j0 + k >= NB) continue;
+      if (hd[k]) {
         lf = 1;
         lv = 0;
       }
-      if (sf[j] & 1) lv = j + 1;
+      if (rF[k] & 1) lv = j0 + k + 1;
     }
     uint32_t pf, pv;
     bscan_seg<NT, OpMax>(lf, lv, ws, pf, pv);
-    uint32_t last = pv;
-    uint32_t viol = 0;
-    for (uint32_t j = j0; j < j1; j++) {
-      uint32_t r = sval[j];
-      bool head = j == 0 || bc[sval[j - 1]] != bc[r];
-      if (head) last = 0;
-      if (!(sf[j] & 1)) {
-        uint32_t kr = sval[last - 1];
-        if (bk[kr] == bk[r]) {
-          // same start: must be an exact duplicate (kind, length, bytes)
-          uint32_t pa = bp[kr], la = bm[kr] >> 8, pb = bp[r], lb = bm[r] >> 8;
-          bool same = la == lb && (bm[kr] & 3) == (bm[r] & 3) && bl[kr] == bl[r];
-          if (same) same = equal_window(in + pa, in + pb, la);
+    uint32_t last = pv, viol = 0, pan = 0;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      if (j0 + k >= NB) continue;
+      if (hd[k]) last = 0;
+      if (!(rF[k] & 1)) {
+        const uint32_t kr = sval[last - 1];
+        if (bk[kr] == rk[k]) { // same start: must be an exact duplicate (kind, length, bytes)
+          const uint32_t la = bm[kr] >> 8, lb = rm[k] >> 8;
+          bool same = la == lb && (bm[kr] & 3) == (rm[k] & 3) && bl[kr] == rl[k];
+          if (same) same = equal_window(in + bp[kr], in + rp[k], la);
           if (!same) viol = 1;
         }
-      } else
-        last = j + 1;
-    }
-    viol = __syncthreads_or(viol);
-    if (viol) {
-      if (t == 0) {
-        o.path[d] = 1;
-        o.status[d] = 0;
-        o.out_len[d] = 0;
-        o.out_start[d] = slot;
+      } else {
+        last = j0 + k + 1;
+        if (rm[k] & 8) pan = 1; // yrs panics encoding a kept String that is not valid UTF-8
       }
+    }
+    const uint32_t vp = __syncthreads_or(viol | (pan << 1));
+    if (vp & 1) {
+      handover();
       return;
     }
-  }
-  // yrs panics while encoding a kept String block that is not valid UTF-8
-  {
-    uint32_t pan = 0;
-    for (uint32_t j = j0; j < j1; j++)
-      if ((sf[j] & 1) && (bm[sval[j]] & 8)) pan = 1;
-    pan = __syncthreads_or(pan);
-    if (pan) {
+    if (vp & 2) {
       if (t == 0) {
         o.path[d] = 0;
         o.status[d] = E_PANIC;
@@ -734,69 +745,70 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
   YM_STAMP(4);
   // ---- 6a block section sizes: per client header + (Skip) + canonical block bytes
   uint32_t blocks_size, NC;
-  uint32_t *sseg = (uint32_t *)(smem + L.sseg);
+  uint32_t *sseg = (uint32_t *)(smem + L.skey); // blocks emitted per client (skey is free now)
   {
     uint32_t nh = 0, lf = 0, lv = 0;
-    for (uint32_t j = j0; j < j1; j++) {
-      uint32_t r = sval[j];
-      bool head = j == 0 || bc[sval[j - 1]] != bc[r];
-      uint32_t c = (sf[j] & 1) + ((sf[j] >> 1) & 1);
-      if (head) {
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      if (j0 + k >= NB) continue;
+      const uint32_t c = (rF[k] & 1) + ((rF[k] >> 1) & 1);
+      if (hd[k]) {
         nh++;
         lf = 1;
         lv = c;
-      } else
+      } else {
         lv += c;
+      }
     }
     const uint32_t hpre = bscan_sum<NT>(nh, ws, NC);
     uint32_t pf, pv;
     bscan_seg<NT, OpSum>(lf, lv, ws, pf, pv);
+    // tail of the chunk's last element: head of the next sorted position
+    const uint32_t jl = j0 + PER;
+    const bool next_head = jl >= NB || (jl < NB && bc[sval[jl]] != rc[PER - 1]);
     uint32_t rank = hpre, run = pv;
-    for (uint32_t j = j0; j < j1; j++) {
-      uint32_t r = sval[j];
-      bool head = j == 0 || bc[sval[j - 1]] != bc[r];
-      uint32_t c = (sf[j] & 1) + ((sf[j] >> 1) & 1);
-      if (head) {
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      if (j0 + k >= NB) continue;
+      const uint32_t c = (rF[k] & 1) + ((rF[k] >> 1) & 1);
+      if (hd[k]) {
         rank++;
         run = c;
-      } else
+      } else {
         run += c;
-      bool tail = j + 1 == NB || bc[sval[j + 1]] != bc[r];
-      if (tail) sseg[rank - 1] = run; // blocks emitted for this client
+      }
+      const bool tail = k + 1 < PER ? (j0 + k + 1 >= NB || hd[k + 1]) : next_head;
+      if (tail) sseg[rank - 1] = run;
     }
     __syncthreads();
     uint32_t ls = 0;
     rank = hpre;
-    for (uint32_t j = j0; j < j1; j++) {
-      uint32_t r = sval[j];
-      bool head = j == 0 || bc[sval[j - 1]] != bc[r];
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      if (j0 + k >= NB) continue;
       uint32_t s = 0;
-      if (head) {
+      if (hd[k]) {
         rank++;
-        uint32_t cnt = sseg[rank - 1];
-        sf[j] |= cnt << 8;
-        s += varlen(cnt) + varlen(bc[r]) + varlen(bk[r]);
+        const uint32_t cnt = sseg[rank - 1];
+        rF[k] |= cnt << 8;
+        s += varlen(cnt) + varlen(rc[k]) + varlen(rk[k]);
       }
-      if (sf[j] & 2) s += 1 + varlen(bk[r] - sE[j]);
-      if (sf[j] & 1) s += canon_size(in, nbytes, bp[r], bc[r], bk[r], bl[r], bm[r]);
+      if (rF[k] & 2) s += 1 + varlen(rk[k] - rE[k]);
+      if (rF[k] & 1) s += canon_size(in, nbytes, rp[k], rc[k], rk[k], rl[k], rm[k]);
+      rS[k] = s;
       ls += s;
     }
     uint32_t tot;
     const uint32_t pre = bscan_sum<NT>(ls, ws, tot);
     const uint32_t base = varlen(NC);
     uint32_t pos = base + pre;
-    for (uint32_t j = j0; j < j1; j++) {
-      uint32_t r = sval[j];
-      bool head = j == 0 || bc[sval[j - 1]] != bc[r];
-      uint32_t s = 0;
-      if (head) s += varlen(sf[j] >> 8) + varlen(bc[r]) + varlen(bk[r]);
-      if (sf[j] & 2) s += 1 + varlen(bk[r] - sE[j]);
-      if (sf[j] & 1) s += canon_size(in, nbytes, bp[r], bc[r], bk[r], bl[r], bm[r]);
-      sz[j] = pos;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      const uint32_t s = rS[k];
+      rS[k] = pos;
       pos += s;
     }
     blocks_size = base + tot;
-    __syncthreads();
   }
   YM_STAMP(5);
   // ---- 6b write the block section into the document's slot
@@ -806,27 +818,25 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
       Writer w{out, 0};
       w_var(w, NC);
     }
-    for (uint32_t j = j0; j < j1; j++) {
-      uint32_t r = sval[j];
-      bool head = j == 0 || bc[sval[j - 1]] != bc[r];
-      Writer w{out, sz[j]};
-      if (head) {
-        w_var(w, sf[j] >> 8);
-        w_var(w, bc[r]);
-        w_var(w, bk[r]);
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      if (j0 + k >= NB) continue;
+      Writer w{out, rS[k]};
+      if (hd[k]) {
+        w_var(w, rF[k] >> 8);
+        w_var(w, rc[k]);
+        w_var(w, rk[k]);
       }
-      if (sf[j] & 2) {
+      if (rF[k] & 2) {
         w.u8(10);
-        w_var(w, bk[r] - sE[j]);
+        w_var(w, rk[k] - rE[k]);
       }
-      if (sf[j] & 1) {
-        uint32_t p = bp[r], len = bm[r] >> 8;
-        if (bm[r] & 4) {
+      if (rF[k] & 1) {
+        if ((rm[k] & 4) && !(rm[k] & 8)) {
           Writer w2 = w; // only the out-of-line re-encode takes a Writer by reference
-          emit_block(in, nbytes, p, bc[r], bk[r], bl[r], 0, w2);
-          w.n = w2.n;
+          emit_block(in, nbytes, rp[k], rc[k], rk[k], rl[k], 0, w2);
         } else {
-          copy_window(w.p + w.n, in + p, len);
+          copy_window(w.p + w.n, in + rp[k], rm[k] >> 8);
         }
       }
     }
@@ -843,10 +853,11 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
   // 5a distinct clients of live entries and their first occurrence (upd << 8 | tpos):
   //    LDS open-addressing table, 64-bit CAS insert, atomicMin on a hit
   uint64_t *dtab = (uint64_t *)(smem + L.dtab);
-  const uint32_t TS = 2 * pow2ceil(caps.e_cap); // table slots (>= 2 * NE)
+  const uint32_t TS = DTAB_SLOTS;
   for (uint32_t j = t; j < TS; j += NT) dtab[j] = ~0ull;
   __syncthreads();
-  for (uint32_t j = t; j < NE; j += NT) {
+  uint32_t tovf = 0;
+  for (uint32_t j = t; j < NE && !tovf; j += NT) {
     if (!(et[j] & 0x80000000u)) continue;
     const uint32_t c = ec[j];
     const uint64_t v = ((uint64_t)c << 32) | (et[j] & 0x7FFFFFFFu);
@@ -862,9 +873,16 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
         break;
       }
       h = (h + 1) & (TS - 1);
+      if (h == (mix32(c) & (TS - 1))) { // table full: more distinct clients than the fast path keeps
+        tovf = 1;
+        break;
+      }
     }
   }
-  __syncthreads();
+  if (__syncthreads_or(tovf)) {
+    handover();
+    return;
+  }
   // compact the occupied slots, then order them by client (rank sort: D is small)
   uint32_t D;
   {
@@ -873,7 +891,11 @@ __global__ void __launch_bounds__(NT) k_fast_merge(BatchIn b, FastCaps caps, Fas
     for (uint32_t j = s0; j < s1; j++) nh += dtab[j] != ~0ull;
     uint32_t pre = bscan_sum<NT>(nh, ws, D);
     for (uint32_t j = s0; j < s1; j++)
-      if (dtab[j] != ~0ull) dkey[pre++] = dtab[j];
+      if (dtab[j] != ~0ull && pre < DCAP) dkey[pre++] = dtab[j];
+  }
+  if (D > DCAP) {
+    handover();
+    return;
   }
   __syncthreads();
   for (uint32_t j = t; j < D; j += NT) {

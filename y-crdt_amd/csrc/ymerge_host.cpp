@@ -57,7 +57,7 @@ struct ymerge_ctx {
   uint64_t *h_pinned = nullptr;
   hipEvent_t ev[6];
   ymerge_stats stats{};
-  ym::FastCaps caps{0, 0, 1024, 512, 512}; // (unused), (unused), blocks, DS entries, DS ranges
+  ym::FastCaps caps{0, 0, 1024, 512, 512}; // b_cap must equal FAST_BCAP (ymerge_fast.hip) // (unused), (unused), blocks, DS entries, DS ranges
   int fast_threads = 256;
   std::mutex mu;
 };
