@@ -58,14 +58,8 @@ def pmc_traffic():
 
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
-    if dist:
-        import torch.distributed as tdist
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import dist
+    rank, world, local = dist.init_from_env("nccl")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -73,10 +67,7 @@ def main():
     import ymerge
 
     # ---- shard: doc-hash partition of world * docs global documents
-    if dist:
-        ids = workloads.shard_ids(world * a.docs, rank, world)
-    else:
-        ids = np.arange(a.docs, dtype=np.uint64)
+    ids = dist.shard(world * a.docs, rank, world) if world > 1 else np.arange(a.docs, dtype=np.uint64)
     batch = workloads.text_docs(len(ids), a.ops, ids=ids)
     t_b = torch.from_numpy(batch.data).to(dev)
     t_u = torch.from_numpy(batch.upd_off.view(np.int64)).to(dev)
@@ -90,8 +81,7 @@ def main():
 
     for _ in range(a.warmup):
         step()
-    if dist:
-        tdist.barrier()
+    dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     kstats = []
@@ -99,8 +89,7 @@ def main():
         res = step()
         kstats.append(eng.stats())
     torch.cuda.synchronize(dev)
-    if dist:
-        tdist.barrier()
+    dist.barrier()
     elapsed = time.perf_counter() - t0
 
     out_bytes = res.out_bytes
@@ -109,17 +98,9 @@ def main():
     ms_kernel = float(np.mean([s["ms_fast"] for s in kstats]))
     ms_exact = float(np.mean([s["ms_exact"] for s in kstats]))
     docs_exact = int(kstats[-1]["docs_exact"])
-    local_stats = torch.tensor([batch.n_docs, batch.n_bytes, out_bytes, n_err, elapsed, ms_kernel],
-                               dtype=torch.float64, device=dev)
-    if dist:
-        gathered = [torch.zeros_like(local_stats) for _ in range(world)]
-        tdist.all_gather(gathered, local_stats)
-        allst = torch.stack(gathered).cpu().numpy()
-    else:
-        allst = local_stats.cpu().numpy()[None, :]
+    allst = dist.gather_stats([batch.n_docs, batch.n_bytes, out_bytes, n_err, elapsed, ms_kernel], device=dev)
     if rank != 0:
-        if dist:
-            tdist.destroy_process_group()
+        dist.finalize()
         return
 
     t_max = float(allst[:, 4].max())
@@ -163,8 +144,7 @@ def main():
         "cpu_baseline": cpu,
     }
     print(json.dumps(line))
-    if dist:
-        tdist.destroy_process_group()
+    dist.finalize()
 
 
 if __name__ == "__main__":

@@ -1,0 +1,78 @@
+"""Multi-process path on CPU (gloo, world_size 2): the doc-hash partition used by
+bench.py / dist.py is disjoint and complete, every rank merges only its shard, and
+the per-rank stats all-gather + max-over-ranks reduction reproduce the single-process
+totals.  The merge itself is the CPU oracle here (test infrastructure; the GPU engine
+runs the same shards on the box)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+N_DOCS, OPS = 48, 60
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "y-crdt_amd"), os.path.join(root, "oracle")):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import dist
+    import oracle
+    import workloads
+    r, w, _ = dist.init_from_env("gloo")
+    ids = dist.shard(N_DOCS, r, w)
+    b = workloads.text_docs(len(ids), OPS, ids=ids)
+    out, off, st = oracle.merge_batch(b.data, b.upd_off, b.doc_upd, mode=1, threads=2)
+    per_doc = {int(ids[k]): out[int(off[k]):int(off[k + 1])] for k in range(len(ids))}
+    dist.barrier()
+    stats = dist.gather_stats([len(ids), b.n_bytes, len(out), int((st != 0).sum()), 0.1 * (r + 1)])
+    gathered = [None] * w
+    torch.distributed.all_gather_object(gathered, per_doc)
+    if r == 0:
+        q.put((stats, gathered))
+    dist.finalize()
+
+
+def test_two_rank_sharded_merge(oracle):
+    import workloads
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    stats, gathered = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # partition: disjoint and complete
+    keys = [set(g) for g in gathered]
+    assert not (keys[0] & keys[1])
+    assert keys[0] | keys[1] == set(range(N_DOCS))
+    # shard sizes as the hash partition says
+    for r in range(world):
+        assert len(workloads.shard_ids(N_DOCS, r, world)) == int(stats[r, 0])
+    # each document's output equals the single-process merge of that document
+    full = workloads.text_docs(N_DOCS, OPS, ids=np.arange(N_DOCS, dtype=np.uint64))
+    out, off, st = oracle.merge_batch(full.data, full.upd_off, full.doc_upd, mode=1, threads=2)
+    merged = {**gathered[0], **gathered[1]}
+    for d in range(N_DOCS):
+        assert merged[d] == out[int(off[d]):int(off[d + 1])]
+    # stats reduction: totals over ranks, time = max over ranks
+    assert int(stats[:, 0].sum()) == N_DOCS
+    assert int(stats[:, 1].sum()) == full.n_bytes
+    assert int(stats[:, 2].sum()) == len(out)
+    assert stats[:, 4].max() == pytest.approx(0.2)
