@@ -63,6 +63,7 @@ typedef struct {
   uint64_t n_docs, bytes_in, bytes_out;
   uint64_t docs_fast, docs_exact, docs_error;
   float ms_total, ms_fast, ms_exact, ms_tail;
+  float ms_decode; /* merge: k_decode (ms_fast = k_fast_merge only) */
 } ymerge_stats;
 
 /* Device-resident result, owned by the context, valid until the next batch.

@@ -29,10 +29,7 @@ def main():
     d = np.diff(st[ok][:, :12].astype(np.int64), axis=1)
     tot = d.sum(axis=1).mean()
     print(f"threads/WG {threads}: {ok.sum()} fast docs, mean {tot:.0f} cycles per doc")
-    r = st[ok].astype(np.int64)
-    print("  round 0: exact-walk fallbacks %.1f lanes, staging %.0f, parse %.0f, scan %.0f (cycles)" % (
-        r[:, 12].mean(), (r[:, 13] - r[:, 0]).mean(), (r[:, 14] - r[:, 13]).mean(),
-        (r[:, 15] - r[:, 14]).mean()))
+    print("  per doc: %.1f REC_SLOW records, %.1f REC_COMPLEX records" % (st[ok][:, 12].mean(), st[ok][:, 13].mean()))
     for i, nm in enumerate(NAMES):
         print(f"  {nm:10s} {d[:, i].mean():10.0f} cycles  {100 * d[:, i].mean() / tot:5.1f}%")
 

@@ -12,7 +12,24 @@ struct BatchIn {
   const uint64_t *upd_off;
   const uint64_t *doc_upd;
   uint32_t n_docs;
+  const uint32_t *rec; // per-update decode records (k_decode), REC_WORDS u32 each; fast path only
+  const uint32_t *ovf; // their overflow words (DEC_OVF per decode workgroup)
 };
+
+// Per-update decode record written by k_decode (one lane per update over the whole
+// batch) and consumed by k_fast_merge.  w0 = error code (bits 0-7) | REC_UNSUP |
+// REC_BIGDS | shape << 10 | DeleteSet ranges << 12 | REC_SLOW (needs the exact walk,
+// done by k_fast_merge); then by shape
+//   REC_BLOCK   : client, clock, length, byte position within the update, meta
+//   REC_DS      : client, start0, end0, start1, end1 (one DeleteSet entry, <= 2 ranges)
+//   REC_COMPLEX : blocks, entries, ranges, [REC_OVF: word offset of its records in the
+//                 overflow buffer (OvfFill layout), else the fast kernel walks it again]
+constexpr uint32_t DEC_NT = 256, DEC_STAGE = 16384, DEC_OVF = 1024; // overflow words per decode workgroup
+constexpr uint32_t REC_WORDS = 6;
+constexpr uint32_t REC_UNSUP = 1u << 8, REC_BIGDS = 1u << 9, REC_SLOW = 1u << 14, REC_OVF = 1u << 15;
+constexpr uint32_t REC_EMPTY = 0, REC_BLOCK = 1, REC_DS = 2, REC_COMPLEX = 3;
+void launch_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_updates, uint32_t *rec, uint32_t *ovf,
+                   hipStream_t s);
 
 // LDS capacities of the one-workgroup-per-document fast path (per document)
 struct FastCaps {

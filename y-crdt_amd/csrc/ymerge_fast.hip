@@ -1,9 +1,11 @@
 // ymerge_fast.hip — parallel merge_updates_v1: one workgroup per document, LDS-resident.
 //
 // Stages (all inside one launch, one document per workgroup):
-//   1 stage   : coalesced copy of the document's bytes + update offsets into LDS
-//   2 decode  : lane-per-update walk (ywalk.h), counts -> block scan -> second walk
-//               writes SoA block / DeleteSet records at their scanned positions
+//   0 k_decode: (separate launch, one lane per update over the batch) LDS-staged
+//               walk of every update -> one fixed-size record per update
+//   1 gather  : lane-per-update record loads, counts -> block scan -> SoA block /
+//               DeleteSet records at their scanned positions (rare multi-block
+//               updates are walked again over HBM)
 //   3 sort    : blocks by (client desc, clock asc, input order) — LDS bitonic,
 //               skipped when already ordered
 //   4 squash  : segmented max-scan of block ends -> keep / gap(Skip) / violation.
@@ -26,13 +28,12 @@
 namespace ym {
 
 // ------------------------------------------------------------------ LDS layout
-// [in][uoff][block records][DS records] then a union of three phase-local regions:
-//   phase 2 (decode): per-update counts -> offsets
+// [block records][DS records][misc] then a union of two phase-local regions:
 //   phase 3/4/6 (blocks): sort keys, classify flags, per-position output offsets
 //   phase 5 (DeleteSet): sort keys, union flags/offsets, per-client tables
 struct FastLayout {
   uint32_t bc, bk, bl, bp, bm, ec, et, rs, re, ri;
-  uint32_t stage, skey, sval;
+  uint32_t skey, sval;
   uint32_t dkey, dval, cend, coff, chead, dcl, dfirst, dord, dnc, dbeg, doff, dtab;
   uint32_t misc, total;
 };
@@ -41,7 +42,6 @@ __host__ __device__ inline uint32_t pow2ceil(uint32_t x) {
   while (p < x) p <<= 1;
   return p;
 }
-constexpr uint32_t STAGE_BYTES = 16384; // LDS staging of one decode round
 constexpr uint32_t FAST_BCAP = 1024;   // blocks per document on the fast path (caps.b_cap)
 constexpr uint32_t DCAP = 64;          // distinct DeleteSet clients per document on the fast path
 constexpr uint32_t DTAB_SLOTS = 256;   // LDS hash table for them
@@ -68,9 +68,6 @@ __host__ __device__ inline FastLayout fast_layout(const FastCaps &c) {
   L.misc = take(4 * 256 + 8 * BTAB);
   const uint32_t u0 = o;
   uint32_t end = o;
-  L.stage = take(STAGE_BYTES + 16);
-  if (o > end) end = o;
-  o = u0;
   L.skey = take(8 * BS);
   L.sval = take(4 * BS);
   if (o > end) end = o;
@@ -313,17 +310,138 @@ struct FastFill {
     nr++;
   }
   YM_INLINE int on_ds_done() {
-    uint32_t n = ne - ebase;
-    if (n >= 2) { // (n <= DS_SMALL here: larger tables go to the exact engine)
-      ds_small_order(ec + ebase, n, et + ebase);
-      for (uint32_t i = 0; i < n; i++) {
-        uint32_t p = et[ebase + i];
-        et[ebase + i] = (p == DS_DEAD ? 0u : 0x80000000u | p) | (upd << 8);
-      }
-    }
+    const uint32_t n = ne - ebase;
+    if (n >= 2) ds_order_packed(ec + ebase, n, et + ebase, upd << 8); // (n <= DS_SMALL: else exact engine)
     return 0;
   }
 };
+
+// Writes one multi-record update (REC_COMPLEX) into its workgroup's overflow words:
+// [blocks: 5 words each (client, clock, length, position in update, meta)]
+// [entry clients] [ranges: 3 words each (start, end, entry index within the update)]
+// (the per-update table order of the entries is computed by k_fast_merge in LDS)
+struct OvfFill {
+  uint32_t *ov;
+  uint32_t NBt, NEt; // totals of this update (RegSink pass)
+  uint32_t nb, ne, nr;
+  YM_INLINE void on_section(uint32_t) {}
+  YM_INLINE int on_block(uint32_t client, uint32_t clock, const BlockInfo &bi, uint32_t bpos, uint32_t blen) {
+    if (bi.kind == BK_SKIP) return 0;
+    uint32_t *w = ov + 5 * nb;
+    w[0] = client;
+    w[1] = clock;
+    w[2] = bi.len;
+    w[3] = bpos;
+    w[4] = (uint32_t)bi.kind | (bi.reenc ? 4u : 0u) | (bi.enc_panic ? 8u : 0u) | (blen << 8);
+    nb++;
+    return 0;
+  }
+  YM_INLINE int on_ds_begin(uint32_t) { return 0; }
+  YM_INLINE int on_ds_entry(uint32_t client, uint32_t) {
+    ov[5 * NBt + ne] = client;
+    ne++;
+    return 0;
+  }
+  YM_INLINE void on_ds_range(uint32_t s0, uint32_t e0) {
+    uint32_t *w = ov + 5 * NBt + NEt + 3 * nr;
+    w[0] = s0;
+    w[1] = e0;
+    w[2] = ne - 1;
+    nr++;
+  }
+  YM_INLINE int on_ds_done() { return 0; }
+};
+
+// sink -> record (ykernels.h REC_*); positions stay relative to the update
+YM_INLINE void rec_pack(const RegSink &s, int e, uint32_t &w0, uint32_t &w1, uint32_t &w2, uint32_t &w3, uint32_t &w4,
+                        uint32_t &w5) {
+  w0 = (uint32_t)e & 0xFF;
+  w1 = w2 = w3 = w4 = w5 = 0;
+  if (s.unsupported) w0 |= REC_UNSUP;
+  if (s.big_ds) w0 |= REC_BIGDS;
+  if (e) return;
+  if (s.nb == 1 && s.ne == 0) {
+    w0 |= REC_BLOCK << 10;
+    w1 = s.b_client;
+    w2 = s.b_clock;
+    w3 = s.b_len;
+    w4 = s.b_pos;
+    w5 = s.b_meta;
+  } else if (s.nb == 0 && s.ne == 1 && s.nr <= 2) {
+    w0 |= (REC_DS << 10) | (s.nr << 12);
+    w1 = s.e_client;
+    w2 = s.r0s;
+    w3 = s.r0e;
+    w4 = s.r1s;
+    w5 = s.r1e;
+  } else if (s.nb || s.ne) {
+    w0 |= REC_COMPLEX << 10;
+    w1 = s.nb;
+    w2 = s.ne;
+    w3 = s.nr;
+  }
+}
+
+// ------------------------------------------------------------------ k_decode
+// One lane per update over the whole batch (updates of all documents are one
+// contiguous byte range): the workgroup stages its NT updates' bytes into LDS with
+// coalesced dword loads, every lane decodes its own update (fast_walk, branch-free
+// varints) and writes one REC_WORDS record.  Other shapes and malformed updates are
+// marked REC_SLOW and walked exactly (ysm.h) by k_fast_merge, so this kernel keeps
+// the fast walk's small register footprint.
+// Decoding here, rather than inside the per-document workgroup, runs the latency-bound
+// byte walk at full occupancy (16 KB LDS, no per-document phases holding registers).
+__global__ void __launch_bounds__(DEC_NT) k_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_upd,
+                                                   uint32_t *rec, uint32_t *ovf) {
+  __shared__ __align__(16) uint32_t stage[DEC_STAGE / 4 + 4];
+  __shared__ uint32_t ovf_top;
+  const uint64_t g0 = (uint64_t)blockIdx.x * DEC_NT;
+  const uint32_t t = threadIdx.x;
+  const uint64_t i = g0 + t;
+  const uint64_t rl = n_upd - g0 < DEC_NT ? n_upd - g0 : DEC_NT;
+  const uint64_t A = upd_off[g0], E = upd_off[g0 + rl];
+  const uint64_t sbase = A & ~3ull;
+  uint64_t nd = (E - sbase + 3) >> 2;
+  if (nd > DEC_STAGE / 4) nd = DEC_STAGE / 4;
+  const uint32_t *src = (const uint32_t *)(bytes + sbase);
+  for (uint32_t k = t; k < nd; k += DEC_NT) stage[k] = src[k];
+  if (t == 0) ovf_top = 0;
+  __syncthreads();
+  if (i >= n_upd) return;
+  const uint64_t a0 = upd_off[i], a1 = upd_off[i + 1];
+  const uint32_t ulen = (uint32_t)(a1 - a0);
+  RegSink s;
+  s.nb = s.ne = s.nr = 0;
+  s.unsupported = s.big_ds = false;
+  s.ubase = 0;
+  const int e = a1 - sbase <= 4 * nd ? fast_walk(stage, (uint32_t)(a0 - sbase), ulen, s) : -1;
+  uint32_t w0 = REC_SLOW, w1 = 0, w2 = 0, w3 = 0, w4 = 0, w5 = 0;
+  if (e >= 0) rec_pack(s, e, w0, w1, w2, w3, w4, w5);
+  if (e == 0 && ((w0 >> 10) & 3) == REC_COMPLEX && !s.big_ds) {
+    // multi-record update: its records go to this workgroup's overflow words (LDS bump
+    // allocation); if they do not fit, k_fast_merge walks the update again
+    const uint32_t need = 5 * s.nb + s.ne + 3 * s.nr;
+    const uint32_t off = need <= DEC_OVF ? atomicAdd(&ovf_top, need) : DEC_OVF;
+    if (off + need <= DEC_OVF) {
+      const uint32_t at = blockIdx.x * DEC_OVF + off;
+      OvfFill f{ovf + at, s.nb, s.ne, 0, 0, 0};
+      fast_walk(stage, (uint32_t)(a0 - sbase), ulen, f);
+      w0 |= REC_OVF;
+      w4 = at;
+    }
+  }
+  uint2 *o = (uint2 *)(rec + i * REC_WORDS);
+  o[0] = make_uint2(w0, w1);
+  o[1] = make_uint2(w2, w3);
+  o[2] = make_uint2(w4, w5);
+}
+
+void launch_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_updates, uint32_t *rec, uint32_t *ovf,
+                   hipStream_t s) {
+  if (!n_updates) return;
+  hipLaunchKernelGGL(k_decode, dim3((unsigned)((n_updates + DEC_NT - 1) / DEC_NT)), dim3(DEC_NT), 0, s, bytes, upd_off,
+                     n_updates, rec, ovf);
+}
 
 // canonical encoded size of a kept block (bm: kind | reenc 4 | panic 8 | input bytes << 8)
 __device__ __forceinline__ uint32_t canon_size(const uint8_t *doc, uint32_t doc_len, uint32_t pos, uint32_t client,
@@ -391,104 +509,116 @@ __global__ void __launch_bounds__(NT, 4) k_fast_merge(BatchIn b, FastCaps caps, 
   uint32_t NB = 0, NE = 0, NR = 0;
   uint32_t flags = 0; // 1 unsupported, 2 big DS table, 4 capacity, 8 huge block
   __syncthreads();
-  uint32_t *stage = (uint32_t *)(smem + L.stage);
   for (uint32_t r0 = 0; r0 < U; r0 += NT) {
     const uint32_t i = r0 + t;
-    // stage the round's bytes [A, E) into LDS (coalesced dwords, at most STAGE_BYTES)
-    if (t == 0) {
-      const uint32_t rl = U - r0 < NT ? U - r0 : NT;
-      sc[4] = (uint32_t)(b.upd_off[u0 + r0] - B0);
-      sc[5] = (uint32_t)(b.upd_off[u0 + r0 + rl] - B0);
-    }
-    __syncthreads();
-    const uint64_t sbase = (B0 + sc[4]) & ~3ull; // absolute, dword aligned
-    uint64_t nd = (B0 + sc[5] - sbase + 3) >> 2;
-    if (nd > STAGE_BYTES / 4) nd = STAGE_BYTES / 4;
-    for (uint32_t k = t; k < nd; k += NT) stage[k] = ((const uint32_t *)(b.bytes + sbase))[k];
-    __syncthreads();
-    if (STAMPS && r0 == 0 && t == 0) o.stamps[(size_t)blockIdx.x * 16 + 13] = __builtin_amdgcn_s_memtime();
-    RegSink s;
-    s.nb = s.ne = s.nr = 0;
-    s.unsupported = s.big_ds = false;
-    uint32_t ubase = 0, ulen = 0, lpos = 0;
-    bool staged = false;
-    int e = 0;
+    uint32_t ubase = 0, ulen = 0, e = 0, shape = 0, w0f = 0, w1 = 0, w2 = 0, w3 = 0, w4 = 0, w5 = 0;
+    uint32_t snb = 0, sne = 0, snr = 0;
     if (i < U) {
       const uint64_t a0 = b.upd_off[u0 + i], a1 = b.upd_off[u0 + i + 1];
       ubase = (uint32_t)(a0 - B0);
       ulen = (uint32_t)(a1 - a0);
-      s.ubase = ubase;
-      lpos = (uint32_t)(a0 - sbase); // upd_off and sbase are offsets into b.bytes
-      staged = a1 - sbase <= 4 * nd;
-      e = staged ? fast_walk(stage, lpos, ulen, s) : -1;
-      if (STAMPS && e < 0 && r0 == 0) atomicAdd((unsigned long long *)&o.stamps[(size_t)blockIdx.x * 16 + 12], 1ull);
-      if (e < 0) { // not a fast shape (or malformed): exact walk over HBM
+      const uint2 *rp = (const uint2 *)(b.rec + (size_t)(u0 + i) * REC_WORDS);
+      const uint2 x0 = rp[0], x1 = rp[1], x2 = rp[2];
+      uint32_t w0 = x0.x;
+      w1 = x0.y;
+      w2 = x1.x;
+      w3 = x1.y;
+      w4 = x2.x;
+      w5 = x2.y;
+      if (STAMPS && (w0 & REC_SLOW)) atomicAdd((unsigned long long *)&o.stamps[(size_t)blockIdx.x * 16 + 12], 1ull);
+      if (STAMPS && ((w0 >> 10) & 3) == REC_COMPLEX)
+        atomicAdd((unsigned long long *)&o.stamps[(size_t)blockIdx.x * 16 + 13], 1ull);
+      if (w0 & REC_SLOW) { // not a fast shape (or malformed): exact walk over HBM
+        RegSink s;
         s.nb = s.ne = s.nr = 0;
         s.unsupported = s.big_ds = false;
-        staged = false;
+        s.ubase = 0;
         WCur c;
         wc_init(c, in + ubase, ulen);
-        e = smwalk_update(c, s);
+        const int es = smwalk_update(c, s);
+        rec_pack(s, es, w0, w1, w2, w3, w4, w5);
       }
-      if (e) atomicMin(&misc[0], (i << 8) | (uint32_t)e);
-      if (s.unsupported) flags |= 1;
-      if (s.big_ds) flags |= 2;
+      w0f = w0;
+      e = w0 & 0xFF;
+      shape = (w0 >> 10) & 3;
+      if (e) atomicMin(&misc[0], (i << 8) | e);
+      if (w0 & REC_UNSUP) flags |= 1;
+      if (w0 & REC_BIGDS) flags |= 2;
       if (ulen >= (1u << 24)) flags |= 8;
+      if (!e) {
+        if (shape == REC_BLOCK) snb = 1;
+        else if (shape == REC_DS) {
+          sne = 1;
+          snr = (w0 >> 12) & 3;
+        } else if (shape == REC_COMPLEX) {
+          snb = w1;
+          sne = w2;
+          snr = w3;
+        }
+      }
     }
-    if (STAMPS && r0 == 0) {
-      __syncthreads();
-      if (t == 0) o.stamps[(size_t)blockIdx.x * 16 + 14] = __builtin_amdgcn_s_memtime();
-    }
-    if (e) s.nb = s.ne = s.nr = 0;
     // packed scan: blocks | entries << 21 | ranges << 42 (each < 2^21 per round)
     uint64_t T;
-    const uint64_t pk = (uint64_t)s.nb | ((uint64_t)s.ne << 21) | ((uint64_t)s.nr << 42);
+    const uint64_t pk = (uint64_t)snb | ((uint64_t)sne << 21) | ((uint64_t)snr << 42);
     const uint64_t pre = bscan_sum64<NT>(pk, (uint64_t *)(misc + 2), T);
     const uint32_t pb = NB + (uint32_t)(pre & 0x1FFFFF), pe = NE + (uint32_t)((pre >> 21) & 0x1FFFFF),
                    pr = NR + (uint32_t)(pre >> 42);
     NB += (uint32_t)(T & 0x1FFFFF);
     NE += (uint32_t)((T >> 21) & 0x1FFFFF);
     NR += (uint32_t)(T >> 42);
-    if (STAMPS && r0 == 0 && t == 0) o.stamps[(size_t)blockIdx.x * 16 + 15] = __builtin_amdgcn_s_memtime();
     if (NB > caps.b_cap || NE > caps.e_cap || NR > caps.r_cap) {
       flags |= 4;
       break; // uniform: every lane sees the same totals
     }
     if (i < U && !e) {
-      if (s.nb <= 1 && s.ne <= 1 && s.nr <= 2) {
-        if (s.nb) {
-          bc[pb] = s.b_client;
-          bk[pb] = s.b_clock;
-          bl[pb] = s.b_len;
-          bp[pb] = s.b_pos;
-          bm[pb] = s.b_meta;
+      if (shape == REC_BLOCK) {
+        bc[pb] = w1;
+        bk[pb] = w2;
+        bl[pb] = w3;
+        bp[pb] = ubase + w4;
+        bm[pb] = w5;
+      } else if (shape == REC_DS) {
+        ec[pe] = w1;
+        et[pe] = 0x80000000u | (i << 8);
+        if (snr > 0) {
+          rs[pr] = w2;
+          re[pr] = w3;
+          ri[pr] = pe;
         }
-        if (s.ne) {
-          ec[pe] = s.e_client;
-          et[pe] = 0x80000000u | (i << 8);
-          if (s.nr > 0) {
-            rs[pr] = s.r0s;
-            re[pr] = s.r0e;
-            ri[pr] = pe;
-          }
-          if (s.nr > 1) {
-            rs[pr + 1] = s.r1s;
-            re[pr + 1] = s.r1e;
-            ri[pr + 1] = pe;
-          }
+        if (snr > 1) {
+          rs[pr + 1] = w4;
+          re[pr + 1] = w5;
+          ri[pr + 1] = pe;
         }
-      } else if (!s.big_ds) {
+      } else if (w0f & REC_OVF) { // multi-record update decoded by k_decode
+        const uint32_t *ov = b.ovf + w4;
+        for (uint32_t k = 0; k < snb; k++) {
+          bc[pb + k] = ov[5 * k];
+          bk[pb + k] = ov[5 * k + 1];
+          bl[pb + k] = ov[5 * k + 2];
+          bp[pb + k] = ubase + ov[5 * k + 3];
+          bm[pb + k] = ov[5 * k + 4];
+        }
+        ov += 5 * snb;
+        for (uint32_t k = 0; k < sne; k++) {
+          ec[pe + k] = ov[k];
+          et[pe + k] = 0x80000000u | (i << 8);
+        }
+        if (sne >= 2) ds_order_packed(ec + pe, sne, et + pe, i << 8);
+        ov += sne;
+        for (uint32_t k = 0; k < snr; k++) {
+          rs[pr + k] = ov[3 * k];
+          re[pr + k] = ov[3 * k + 1];
+          ri[pr + k] = pe + ov[3 * k + 2];
+        }
+      } else if (shape == REC_COMPLEX && !(flags & 2)) {
+        // not a one-record shape: walk the update again over HBM at its scanned positions
         FastFill f{bc, bk, bl, bp, bm, ec, et, rs, re, ri, i, ubase, pb, pe, pr, 0};
-        if (staged) {
-          fast_walk(stage, lpos, ulen, f);
-        } else {
-          WCur c;
-          wc_init(c, in + ubase, ulen);
-          smwalk_update(c, f);
-        }
+        WCur c;
+        wc_init(c, in + ubase, ulen);
+        smwalk_update(c, f);
       }
     }
-    __syncthreads(); // the next round re-stages
   }
   if (flags) atomicOr(&misc[1], flags);
   __syncthreads();

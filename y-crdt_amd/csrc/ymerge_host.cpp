@@ -52,7 +52,7 @@ struct ymerge_ctx {
   hipStream_t s = nullptr;
   DevBuf in_bytes, in_upd_off, in_doc_upd, in_sv, in_sv_off;
   DevBuf status, path, out_start, out_len, pack_off, counts, need, scr_off, scratch, sizes, spill_off, scan_tmp;
-  DevBuf arena, packed, counter, stamps, plan_small, plan_big;
+  DevBuf arena, packed, counter, stamps, plan_small, plan_big, rec, ovf;
   bool want_stamps = false;
   uint64_t *h_pinned = nullptr;
   hipEvent_t ev[6];
@@ -98,7 +98,7 @@ extern "C" void ymerge_ctx_destroy(ymerge_ctx *c) {
   if (!c) return;
   hipSetDevice(c->device);
   if (c->s) hipStreamSynchronize(c->s);
-  for (DevBuf *b : {&c->in_bytes, &c->in_upd_off, &c->in_doc_upd, &c->in_sv, &c->in_sv_off, &c->status, &c->path,
+  for (DevBuf *b : {&c->in_bytes, &c->in_upd_off, &c->in_doc_upd, &c->in_sv, &c->in_sv_off, &c->rec, &c->ovf, &c->status, &c->path,
                     &c->out_start, &c->out_len, &c->pack_off, &c->counts, &c->need, &c->scr_off, &c->scratch,
                     &c->sizes, &c->spill_off, &c->scan_tmp, &c->arena, &c->packed, &c->counter, &c->stamps,
                     &c->plan_small, &c->plan_big})
@@ -131,19 +131,23 @@ static bool ensure_keep(ymerge_ctx *c, DevBuf &b, size_t bytes, size_t keep) {
 
 // One batch: fast path for every document, exact engine for the documents it hands over.
 static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes, const uint64_t *d_upd_off,
-                        const uint64_t *d_doc_upd, uint64_t n_docs, ymerge_device_result *res) {
+                        uint64_t n_updates, const uint64_t *d_doc_upd, uint64_t n_docs, ymerge_device_result *res) {
   if (hipSetDevice(c->device) != hipSuccess) return YMERGE_ERR_DEVICE;
   if (n_docs > 0xFFFFFFFFull) return YMERGE_ERR_OTHER;
   const uint32_t n = (uint32_t)n_docs;
-  ym::BatchIn b{d_bytes, d_upd_off, d_doc_upd, n};
+  ym::BatchIn b{d_bytes, d_upd_off, d_doc_upd, n, nullptr, nullptr};
   const size_t nn = (size_t)n + 1;
   const uint64_t slots = 2 * n_bytes + 64 * (uint64_t)n_docs;
   if (!c->status.ensure(nn) || !c->path.ensure(nn) || !c->out_start.ensure(nn * 8) || !c->out_len.ensure(nn * 8) ||
       !c->pack_off.ensure(nn * 8) || !c->counts.ensure(4 * nn * 4) || !c->need.ensure(nn * 8) ||
       !c->scr_off.ensure(nn * 8) || !c->sizes.ensure(nn * 8) || !c->spill_off.ensure(nn * 8) ||
       !c->scan_tmp.ensure(ym::scan_tmp_elems(n) * 8 + 64) || !c->counter.ensure(64) ||
-      !ensure_keep(c, c->arena, slots + slots / 8 + 4096, 0))
+      !ensure_keep(c, c->arena, slots + slots / 8 + 4096, 0) ||
+      (c->fast_threads && (!c->rec.ensure((n_updates + 1) * ym::REC_WORDS * 4) ||
+                           !c->ovf.ensure(((n_updates + ym::DEC_NT - 1) / ym::DEC_NT + 1) * ym::DEC_OVF * 4))))
     return YMERGE_ERR_DEVICE;
+  b.rec = c->rec.as<uint32_t>();
+  b.ovf = c->ovf.as<uint32_t>();
   uint8_t *arena = c->arena.as<uint8_t>();
   uint64_t *ostart = c->out_start.as<uint64_t>(), *olen = c->out_len.as<uint64_t>();
   uint8_t *status = c->status.as<uint8_t>(), *path = c->path.as<uint8_t>();
@@ -156,10 +160,15 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     stamps = c->stamps.as<uint64_t>();
   }
   ym::FastOut fo{arena, ostart, olen, status, path, stamps};
-  if (c->fast_threads)
+  if (c->fast_threads) {
+    ym::launch_decode(d_bytes, d_upd_off, n_updates, c->rec.as<uint32_t>(), c->ovf.as<uint32_t>(), c->s);
+    hipEventRecord(c->ev[5], c->s);
     ym::launch_fast_merge(b, c->caps, fo, c->fast_threads, c->s);
-  else
+  }
+  else {
+    hipEventRecord(c->ev[5], c->s);
     hipMemsetAsync(path, 1, n, c->s);
+  }
   hipEventRecord(c->ev[1], c->s);
   // exact engine for documents the fast path handed over (path == 1)
   ym::launch_seq_count(b, path, status, c->counts.as<uint32_t>(), c->need.as<uint64_t>(), c->counter.as<uint32_t>(),
@@ -191,8 +200,9 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   uint64_t total = 0;
   if (!read_words(c, c->pack_off.as<uint64_t>() + n, 8, &total)) return YMERGE_ERR_DEVICE;
   if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
-  float t01 = 0, t12 = 0, t23 = 0, t03 = 0;
-  hipEventElapsedTime(&t01, c->ev[0], c->ev[1]);
+  float t01 = 0, t12 = 0, t23 = 0, t03 = 0, t05 = 0;
+  hipEventElapsedTime(&t05, c->ev[0], c->ev[5]);
+  hipEventElapsedTime(&t01, c->ev[5], c->ev[1]);
   hipEventElapsedTime(&t12, c->ev[1], c->ev[2]);
   hipEventElapsedTime(&t23, c->ev[2], c->ev[3]);
   hipEventElapsedTime(&t03, c->ev[0], c->ev[3]);
@@ -205,6 +215,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   c->stats.ms_fast = t01;
   c->stats.ms_exact = t12;
   c->stats.ms_tail = t23;
+  c->stats.ms_decode = t05;
   c->stats.ms_total = t03;
   res->d_out = arena;
   res->d_out_start = ostart;
@@ -219,9 +230,8 @@ extern "C" int ymerge_updates_v1_batch_device(ymerge_ctx *c, const uint8_t *d_by
                                               const uint64_t *d_upd_off, uint64_t n_updates, const uint64_t *d_doc_upd,
                                               uint64_t n_docs, ymerge_device_result *res) {
   if (!c || !res) return YMERGE_ERR_OTHER;
-  (void)n_updates;
   std::lock_guard<std::mutex> g(c->mu);
-  return merge_device(c, d_bytes, n_bytes, d_upd_off, d_doc_upd, n_docs, res);
+  return merge_device(c, d_bytes, n_bytes, d_upd_off, n_updates, d_doc_upd, n_docs, res);
 }
 
 // diff_updates_v1 / encode_state_vector_from_update_v1 over a batch (one update per document):
@@ -358,7 +368,7 @@ extern "C" int ymerge_updates_v1_batch(ymerge_ctx *c, const uint8_t *bytes, cons
       hipMemcpyAsync(c->in_doc_upd.p, doc_upd, (n_docs + 1) * 8, hipMemcpyHostToDevice, c->s) != hipSuccess)
     return YMERGE_ERR_DEVICE;
   ymerge_device_result dr{};
-  int st = merge_device(c, c->in_bytes.as<uint8_t>(), nbytes, c->in_upd_off.as<uint64_t>(),
+  int st = merge_device(c, c->in_bytes.as<uint8_t>(), nbytes, c->in_upd_off.as<uint64_t>(), n_updates,
                         c->in_doc_upd.as<uint64_t>(), n_docs, &dr);
   if (st) return st;
   auto *r = (ymerge_batch_result *)calloc(1, sizeof(ymerge_batch_result));

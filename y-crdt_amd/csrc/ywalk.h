@@ -101,4 +101,55 @@ __device__ __noinline__ void ds_small_order(const uint32_t *clients, uint32_t n,
     if (hb.slot[s]) pos_out[hb.slot[s] - 1] = k++;
 }
 
+// ds_small_order without a stack: for n <= DS_SMALL entries the table has at most 16
+// buckets (4 -> 8 -> 16), where hashbrown's group probe (16 control bytes, trailing
+// mirror / EMPTY bytes) reduces to linear probing with wrap-around from client & mask.
+// Slot -> entry+1 lives in one u64 (4 bits per slot).  Writes every entry's code
+// (0x80000000 | iteration position, or 0 if a later entry replaced it) | tag into et.
+YM_INLINE uint32_t hb_probe(uint64_t m, uint32_t nb, uint32_t key) {
+  uint32_t s = key & (nb - 1);
+  while ((m >> (4 * s)) & 15) s = (s + 1) & (nb - 1);
+  return s;
+}
+YM_INLINE void ds_order_packed(const uint32_t *cl, uint32_t n, uint32_t *et, uint32_t tag) {
+  uint64_t map = 0;
+  uint32_t buckets = 0, items = 0, growth = 0, dead = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t c = cl[i];
+    if (growth == 0) { // HashMap::insert -> reserve(1) -> resize (old slots re-placed in slot order)
+      const uint32_t full = buckets ? (uint32_t)mask_to_cap(buckets - 1) : 0;
+      const uint32_t need = items + 1;
+      const uint32_t nb = (uint32_t)cap_to_buckets(need > full + 1 ? need : full + 1);
+      uint64_t nm = 0;
+      for (uint32_t s = 0; s < buckets; s++) {
+        const uint32_t en = (uint32_t)(map >> (4 * s)) & 15;
+        if (en) nm |= (uint64_t)en << (4 * hb_probe(nm, nb, cl[en - 1]));
+      }
+      map = nm;
+      buckets = nb;
+      growth = (uint32_t)mask_to_cap(nb - 1) - items;
+    }
+    int fs = -1;
+    for (uint32_t s = 0; s < buckets; s++) {
+      const uint32_t en = (uint32_t)(map >> (4 * s)) & 15;
+      if (en && cl[en - 1] == c) fs = (int)s;
+    }
+    if (fs >= 0) { // replace in place: the earlier entry is dead
+      dead |= 1u << (((uint32_t)(map >> (4 * fs)) & 15) - 1);
+      map = (map & ~(15ull << (4 * fs))) | ((uint64_t)(i + 1) << (4 * fs));
+    } else {
+      map |= (uint64_t)(i + 1) << (4 * hb_probe(map, buckets, c));
+      items++;
+      growth--;
+    }
+  }
+  uint32_t k = 0;
+  for (uint32_t s = 0; s < buckets; s++) {
+    const uint32_t en = (uint32_t)(map >> (4 * s)) & 15;
+    if (en) et[en - 1] = 0x80000000u | k++ | tag;
+  }
+  for (uint32_t i = 0; i < n; i++)
+    if ((dead >> i) & 1) et[i] = tag;
+}
+
 } // namespace ym

@@ -35,7 +35,7 @@ class _Stats(ctypes.Structure):
     _fields_ = [("n_docs", ctypes.c_uint64), ("bytes_in", ctypes.c_uint64), ("bytes_out", ctypes.c_uint64),
                 ("docs_fast", ctypes.c_uint64), ("docs_exact", ctypes.c_uint64), ("docs_error", ctypes.c_uint64),
                 ("ms_total", ctypes.c_float), ("ms_fast", ctypes.c_float), ("ms_exact", ctypes.c_float),
-                ("ms_tail", ctypes.c_float)]
+                ("ms_tail", ctypes.c_float), ("ms_decode", ctypes.c_float)]
 
 
 class _DevRes(ctypes.Structure):
