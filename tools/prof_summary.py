@@ -54,12 +54,17 @@ def main():
     res = {"tag": tag, "unit": "KiB per launch (mean over launches)", "fetch_size": fetch, "write_size": write}
     with open(os.path.join(prof, f"{tag}_pmc.json"), "w") as f:
         json.dump(res, f, indent=1)
-    fk = [k for k in fetch if kern in k]
-    wk = [k for k in write if kern in k]
-    if fk and wk:
-        t = (2 * fetch[fk[0]] + write[wk[0]]) * 1024
+    # KERNEL_SUBSTRING may list several kernels ("k_decode,k_fast_merge"): the dominant
+    # stage is then their sum per step, matching bench.py's combined kernel_ms.
+    names = kern.split(",")
+    fk = [next((k for k in fetch if n in k), None) for n in names]
+    wk = [next((k for k in write if n in k), None) for n in names]
+    if all(fk) and all(wk):
+        fs = sum(fetch[k] for k in fk)
+        ws = sum(write[k] for k in wk)
+        t = (2 * fs + ws) * 1024
         with open(os.path.join(prof, "pmc_traffic.json"), "w") as f:
-            json.dump({"tag": tag, "kernel": fk[0], "fetch_kib": fetch[fk[0]], "write_kib": write[wk[0]],
+            json.dump({"tag": tag, "kernel": " + ".join(fk), "fetch_kib": fs, "write_kib": ws,
                        "traffic_bytes_per_launch": t,
                        "formula": "(2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE half-count correction)"},
                       f, indent=1)
