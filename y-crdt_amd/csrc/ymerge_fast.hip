@@ -1129,16 +1129,43 @@ __global__ void __launch_bounds__(NT, 4) k_fast_merge(BatchIn b, FastCaps caps, 
       if (tkey[j] > tkey[j + 1]) unsorted = 1;
     unsorted = __syncthreads_or(unsorted);
     if (unsorted) {
-      for (uint32_t j = t; j < NR; j += NT) {
-        const uint64_t kj = tkey[j];
-        uint32_t r = 0;
-        for (uint32_t q = 0; q < NR; q++) { // uniform trip count: one broadcast read per step
-          const uint64_t kq = tkey[q];
-          r += (kq < kj) | ((kq == kj) & (q < j));
+      // bottom-up stable merge sort, one barrier per level: an element of a left run lands
+      // at base + i + #(right-run keys < k), of a right run at base + i + #(left-run keys
+      // <= k) (binary searches).  Equal keys keep index order, exactly like a rank sort by
+      // (key, index).  cmp_end is free until 5d and carries the indices of the tkey side.
+      uint64_t *ka = tkey, *kb = dkey;
+      uint32_t *ia = (uint32_t *)(smem + L.cend), *ib = dval;
+      for (uint32_t j = t; j < NR; j += NT) ia[j] = j;
+      __syncthreads();
+      for (uint32_t w = 1; w < NR; w <<= 1) {
+        for (uint32_t j = t; j < NR; j += NT) {
+          const uint64_t kj = ka[j];
+          const uint32_t run = j / w, i = j - run * w;
+          const bool left = !(run & 1);
+          const uint32_t base = (left ? run : run - 1) * w;
+          uint32_t lo = left ? base + w : base, hi = left ? base + 2 * w : base + w;
+          if (lo > NR) lo = NR;
+          if (hi > NR) hi = NR;
+          const uint32_t b0 = lo;
+          while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            const uint64_t km = ka[mid];
+            if (left ? (km < kj) : (km <= kj)) lo = mid + 1;
+            else hi = mid;
+          }
+          const uint32_t dst = base + i + (lo - b0);
+          kb[dst] = kj;
+          ib[dst] = ia[j];
         }
-        dkey[r] = kj;
-        dval[r] = j;
+        __syncthreads();
+        uint64_t *tk = ka; ka = kb; kb = tk;
+        uint32_t *ti = ia; ia = ib; ib = ti;
       }
+      if (ka != dkey)
+        for (uint32_t j = t; j < NR; j += NT) {
+          dkey[j] = ka[j];
+          dval[j] = ia[j];
+        }
     } else {
       for (uint32_t j = t; j < NR; j += NT) {
         dkey[j] = tkey[j];
