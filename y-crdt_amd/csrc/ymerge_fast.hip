@@ -35,7 +35,7 @@ struct FastLayout {
   uint32_t bc, bk, bl, bp, bm, ec, et, rs, re, ri;
   uint32_t skey, sval;
   uint32_t dkey, dval, cend, coff, chead, dcl, dfirst, dord, dnc, dbeg, doff, dtab;
-  uint32_t misc, total;
+  uint32_t misc, stage, total;
 };
 __host__ __device__ inline uint32_t pow2ceil(uint32_t x) {
   uint32_t p = 1;
@@ -46,6 +46,9 @@ constexpr uint32_t FAST_BCAP = 1024;   // blocks per document on the fast path (
 constexpr uint32_t DCAP = 64;          // distinct DeleteSet clients per document on the fast path
 constexpr uint32_t DTAB_SLOTS = 256;   // LDS hash table for them
 constexpr uint32_t BTAB = 64; // client table of the counting sort (<= 8 distinct clients used)
+// LDS staging of the block section (6b): the phase-local union is free while it is written;
+// it is grown to at least this size (total stays under 160 KB / 3 workgroups per CU)
+constexpr uint32_t STAGE_MIN = 20 * 1024;
 __host__ __device__ inline FastLayout fast_layout(const FastCaps &c) {
   FastLayout L;
   uint32_t o = 0;
@@ -85,6 +88,8 @@ __host__ __device__ inline FastLayout fast_layout(const FastCaps &c) {
   L.doff = take(4 * (DCAP + 1));
   L.dtab = take(8 * (DTAB_SLOTS > RS ? DTAB_SLOTS : RS)); // client table, then range sort keys (NR)
   if (o > end) end = o;
+  L.stage = u0;
+  if (u0 + STAGE_MIN > end) end = u0 + STAGE_MIN;
   L.total = end;
   return L;
 }
@@ -943,15 +948,22 @@ __global__ void __launch_bounds__(NT, 4) k_fast_merge(BatchIn b, FastCaps caps, 
   YM_STAMP(5);
   // ---- 6b write the block section into the document's slot
   uint8_t *out = o.out + slot;
+  // Lanes write their pieces into LDS at the destination's 16-byte phase, then the
+  // workgroup stores whole aligned 16-byte chunks (partial end chunks byte by byte: the
+  // neighbouring bytes belong to other slots).  Sections larger than the stage are written
+  // straight to HBM.
+  const uint32_t phase = (uint32_t)((uintptr_t)out & 15);
+  const bool staged = phase + blocks_size <= L.total - L.stage;
+  uint8_t *wdst = staged ? smem + L.stage + phase : out;
   if (blocks_size <= cap) {
     if (t == 0) {
-      Writer w{out, 0};
+      Writer w{wdst, 0};
       w_var(w, NC);
     }
 #pragma unroll
     for (int k = 0; k < PER; k++) {
       if (j0 + k >= NB) continue;
-      Writer w{out, rS[k]};
+      Writer w{wdst, rS[k]};
       if (hd[k]) {
         w_var(w, rF[k] >> 8);
         w_var(w, rc[k]);
@@ -967,6 +979,20 @@ __global__ void __launch_bounds__(NT, 4) k_fast_merge(BatchIn b, FastCaps caps, 
           emit_block(in, nbytes, rp[k], rc[k], rk[k], rl[k], 0, w2);
         } else {
           copy_window(w.p + w.n, in + rp[k], rm[k] >> 8);
+        }
+      }
+    }
+    if (staged) {
+      __syncthreads();
+      const uint8_t *st = smem + L.stage;
+      uint8_t *gbase = out - phase;
+      const uint32_t span = phase + blocks_size, nch = (span + 15) >> 4;
+      for (uint32_t c = t; c < nch; c += NT) {
+        const uint32_t b0 = c << 4, lo = b0 < phase ? phase : b0, hi = b0 + 16 < span ? b0 + 16 : span;
+        if (lo == b0 && hi == b0 + 16) {
+          *(uint4 *)(gbase + b0) = *(const uint4 *)(st + b0);
+        } else {
+          for (uint32_t q = lo; q < hi; q++) gbase[q] = st[q];
         }
       }
     }
