@@ -596,6 +596,8 @@ __global__ void __launch_bounds__(NT, 4) k_fast_merge(BatchIn b, FastCaps caps, 
           ri[pr + 1] = pe;
         }
       } else if (w0f & REC_OVF) { // multi-record update decoded by k_decode
+        if (STAMPS) atomicAdd((unsigned long long *)&o.stamps[(size_t)blockIdx.x * 16 + 15],
+                              (unsigned long long)(5 * snb + sne + 3 * snr));
         const uint32_t *ov = b.ovf + w4;
         for (uint32_t k = 0; k < snb; k++) {
           bc[pb + k] = ov[5 * k];
@@ -618,6 +620,7 @@ __global__ void __launch_bounds__(NT, 4) k_fast_merge(BatchIn b, FastCaps caps, 
         }
       } else if (shape == REC_COMPLEX && !(flags & 2)) {
         // not a one-record shape: walk the update again over HBM at its scanned positions
+        if (STAMPS) atomicAdd((unsigned long long *)&o.stamps[(size_t)blockIdx.x * 16 + 14], 1ull);
         FastFill f{bc, bk, bl, bp, bm, ec, et, rs, re, ri, i, ubase, pb, pe, pr, 0};
         WCur c;
         wc_init(c, in + ubase, ulen);
