@@ -1164,9 +1164,43 @@ __global__ void __launch_bounds__(NT, 4) k_fast_merge(BatchIn b, FastCaps caps, 
       // (key, index).  cmp_end is free until 5d and carries the indices of the tkey side.
       uint64_t *ka = tkey, *kb = dkey;
       uint32_t *ia = (uint32_t *)(smem + L.cend), *ib = dval;
-      for (uint32_t j = t; j < NR; j += NT) ia[j] = j;
+      // levels w < 64 in registers: each wave bitonic-sorts 64-element segments by
+      // (key, index) with lane shuffles (index makes keys distinct, so this equals the
+      // stable order); padding lanes carry (~0, index >= NR) and sort last
+      {
+        const uint32_t lane = t & 63;
+        for (uint32_t jb = t - lane; jb < NR; jb += NT) { // uniform per wave
+          const uint32_t j = jb + lane;
+          uint64_t key = j < NR ? tkey[j] : ~0ull;
+          uint32_t idx = j;
+#pragma unroll
+          for (uint32_t k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+            for (uint32_t sft = k >> 1; sft > 0; sft >>= 1) {
+              const uint32_t okl = __shfl_xor((uint32_t)key, (int)sft, 64);
+              const uint32_t okh = __shfl_xor((uint32_t)(key >> 32), (int)sft, 64);
+              const uint32_t oi = __shfl_xor(idx, (int)sft, 64);
+              const uint64_t ok = ((uint64_t)okh << 32) | okl;
+              const bool other_less = ok < key || (ok == key && oi < idx);
+              const bool up = (lane & k) == 0, lower = (lane & sft) == 0;
+              if (lower == up ? other_less : !other_less) {
+                key = ok;
+                idx = oi;
+              }
+            }
+          }
+          if (j < NR) {
+            kb[j] = key;
+            ib[j] = idx;
+          }
+        }
+      }
       __syncthreads();
-      for (uint32_t w = 1; w < NR; w <<= 1) {
+      {
+        uint64_t *tk = ka; ka = kb; kb = tk;
+        uint32_t *ti = ia; ia = ib; ib = ti;
+      }
+      for (uint32_t w = 64; w < NR; w <<= 1) {
         for (uint32_t j = t; j < NR; j += NT) {
           const uint64_t kj = ka[j];
           const uint32_t run = j / w, i = j - run * w;
