@@ -469,7 +469,7 @@ __device__ __forceinline__ uint32_t canon_size(const uint8_t *doc, uint32_t doc_
   } while (0)
 
 template <int NT, bool STAMPS>
-__global__ void __launch_bounds__(NT, 4) k_fast_merge(BatchIn b, FastCaps caps, FastOut o) {
+__global__ void __launch_bounds__(NT, 3) k_fast_merge(BatchIn b, FastCaps caps, FastOut o) {
   constexpr int PER = (int)(FAST_BCAP / NT); // sorted positions per lane (b_cap == FAST_BCAP)
   extern __shared__ __align__(16) uint8_t smem[];
   const FastLayout L = fast_layout(caps);
