@@ -221,3 +221,30 @@ def test_ds_heavy_updates_exact_engine(oracle):
         check_batch(e, oracle, batch_of(ds_heavy_docs(32)))
     finally:
         e.close()
+
+
+def _root_text_update(client, clock, s):
+    """One v1 update: a single String item with no origins under root type "t"
+    (yrs/src/update.rs:433-488 decode_block; parent info 1 = root name)."""
+    body = bytes([0x04]) + _var(1) + _var(1) + b"t" + _var(len(s)) + s.encode()
+    return _var(1) + _var(1) + _var(client) + _var(clock) + body + _var(0)
+
+
+def test_large_block_sections(engine, oracle):
+    """Block sections around and above the fast path's 20 KB LDS stage (staged and
+    direct-to-HBM writers), updates in shuffled order from two clients."""
+    rng = np.random.default_rng(0x57A6E)
+    docs = []
+    for n in (150, 300, 330, 360, 480):
+        ups = []
+        for c in (3, 9):
+            clock = 0
+            for i in range(n // 2):
+                s = "".join(chr(97 + int(x)) for x in rng.integers(0, 26, 60))
+                ups.append(_root_text_update(c, clock, s))
+                clock += len(s)
+        order = rng.permutation(len(ups))
+        docs.append([ups[i] for i in order])
+    check_batch(engine, oracle, batch_of(docs))
+    st = engine.stats()
+    assert st["docs_exact"] == 0
