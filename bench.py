@@ -1,23 +1,30 @@
-"""Benchmark: batched merge_updates_v1 on MI355X (BASELINE.json metric).
+"""Benchmark: batched merge_updates_v1 / diff_updates_v1 on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--docs D] [--ops O]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c1|c2|c3|c4|c5] [--docs D] [--ops O]
 
-Workload (BASELINE.json configs[1]): per GPU 10,000 synthetic YText documents x
-1,000 single-op v1 updates (1-4 synced clients, 80/20 insert/delete), inputs
-resident in HBM before the timed region.  One step = one full batched
-merge_updates_v1 over the GPU's shard (validate/count, scratch plan, size plan,
-scan, write).  For N > 1 (torch.distributed.run, one rank per GPU) documents are
-sharded by splitmix64(doc_id) % N with no data-path collective; RCCL is used for
-the barrier, the max-over-ranks time and a per-shard stats gather.
+Workloads (BASELINE.json configs; inputs resident in HBM before the timed region):
+  c2 (default, configs[1])  per GPU D=10,000 synthetic YText docs x O=1,000 single-op v1 updates
+                            (1-4 synced clients, 80/20 insert/delete); weak scaling
+  c1 (configs[0])           the automerge-paper trace as 259,778 per-op updates, one document
+  c3 (configs[2])           1,000,000 docs with Zipf(1.5) update counts on [1, 1e4], doc-hash
+                            sharded over the ranks (total work fixed: strong scaling)
+  c4 (configs[3])           2,000 delete-heavy docs x 5,000 updates (GC'd snapshot + per-op log)
+  c5 (configs[4])           diff_updates_v1 of 100,000 compacted docs (C2 merge outputs) against
+                            per-document remote state vectors (sync-step-2 serving); weak scaling
+One step = one full batched call over the GPU's shard.  For N > 1 (torch.distributed.run,
+one rank per GPU) documents are sharded by splitmix64(doc_id) % N with no data-path
+collective; RCCL carries the barrier, the max-over-ranks time and a per-shard stats gather.
 
-Prints ONE JSON line (rank 0).  `value` = input GB/s over all ranks; docs/s,
-roofline of the dominant kernel (HIP-event timed on the engine's stream) and the
-CPU baseline (the oracle, literal yrs algorithm, on a bounded sample, rank 0,
-N=1) ride along.
+Prints ONE JSON line (rank 0).  `value` = input GB/s over all ranks; docs/s, the roofline
+of the device pipeline (HIP events on the engine's stream), an end-to-end number (H2D +
+pipeline + pack + D2H) and the CPU baseline (the oracle, literal yrs algorithm, bounded
+sample, rank 0, N=1) ride along.
 """
 import argparse
 import json
 import os
+import platform
+import statistics
 import sys
 import time
 
@@ -30,6 +37,7 @@ import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "input GB/s + docs compacted/sec, batched merge_updates_v1 @ 1/2/4/8 GPUs"
+METRIC_DIFF = "input GB/s + docs served/sec, batched diff_updates_v1 (sync-step-2) @ 1/2/4/8 GPUs"
 
 
 def parse():
@@ -37,43 +45,129 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--docs", type=int, default=10_000, help="documents per GPU")
-    ap.add_argument("--ops", type=int, default=1_000, help="updates per document")
-    ap.add_argument("--cpu-sample", type=int, default=10_000, help="docs in the CPU-baseline sample")
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
+    ap.add_argument("--docs", type=int, default=None, help="documents (per GPU for c2/c4/c5, total for c3)")
+    ap.add_argument("--ops", type=int, default=None, help="updates per document (c2/c4/c5)")
+    ap.add_argument("--cpu-seconds", type=float, default=1.5, help="target wall time of one CPU-baseline run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
     return ap.parse_args()
 
 
-def pmc_traffic():
-    """HBM bytes per launch of the dominant kernel from a committed rocprofv3 PMC pass, if any."""
+def pmc_traffic(workload):
+    """HBM bytes per launch of the pipeline from a committed rocprofv3 PMC pass, if any."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(p):
         try:
             with open(p) as f:
-                return json.load(f).get("traffic_bytes_per_launch")
+                d = json.load(f)
+            if d.get("workload", "c2") == workload:
+                return d.get("traffic_bytes_per_launch")
         except Exception:
             return None
     return None
 
 
-def main():
-    a = parse()
+def host_cpu():
+    model = platform.processor() or ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        share = len(os.sched_getaffinity(0))
+    except AttributeError:
+        share = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        share = min(share, int(env))  # the GPU box's CPU share for this job
+    return model, os.cpu_count() or 1, max(1, share)
+
+
+def timed_runs(fn, runs):
+    fn()  # warm-up
+    ts = []
+    for _ in range(runs):
+        t = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t)
+    return statistics.median(ts)
+
+
+# ------------------------------------------------------------------ workloads
+def build_merge(a, rank, world):
     import dist
-    rank, world, local = dist.init_from_env("nccl")
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-
     import workloads
-    import ymerge
+    w = a.workload
+    if w == "c1":
+        batch, _ = workloads.trace_updates()
+        return batch, "C1: automerge-paper trace as 259,778 per-op v1 updates, one document, merge_updates_v1", \
+            "replicas", {"docs": 1, "updates": batch.n_updates}
+    if w == "c2":
+        docs, ops = a.docs or 10_000, a.ops or 1_000
+        ids = dist.shard(world * docs, rank, world) if world > 1 else np.arange(docs, dtype=np.uint64)
+        batch = workloads.text_docs(len(ids), ops, ids=ids)
+        return batch, f"C2: {docs} synthetic YText docs x {ops} single-op v1 updates per GPU, batched " \
+                      "merge_updates_v1", "weak", {"docs_per_gpu": docs, "updates_per_doc": ops}
+    if w == "c3":
+        docs = a.docs or 1_000_000
+        ids = dist.shard(docs, rank, world) if world > 1 else np.arange(docs, dtype=np.uint64)
+        batch = workloads.zipf_docs(docs, ids=ids) if world > 1 else workloads.zipf_docs(docs)
+        return batch, f"C3: {docs} docs total, Zipf(1.5) update counts on [1, 1e4], doc-hash sharded, " \
+                      "batched merge_updates_v1", "strong", {"docs_total": docs}
+    if w == "c4":
+        docs, ops = a.docs or 2_000, a.ops or 5_000
+        batch = workloads.delete_heavy_docs(docs, ops)
+        return batch, f"C4: {docs} delete-heavy docs x {ops} updates per GPU (70% deletes, GC'd snapshot + " \
+                      "per-op log, withheld/duplicated updates)", "weak", {"docs_per_gpu": docs,
+                                                                         "updates_per_doc": ops}
+    raise ValueError(w)
 
-    # ---- shard: doc-hash partition of world * docs global documents
-    ids = dist.shard(world * a.docs, rank, world) if world > 1 else np.arange(a.docs, dtype=np.uint64)
-    batch = workloads.text_docs(len(ids), a.ops, ids=ids)
-    t_b = torch.from_numpy(batch.data).to(dev)
+
+def cpu_merge_baseline(batch, a):
+    import oracle
+    model, nproc, share = host_cpu()
+    if batch.n_docs == 1:  # C1: one document, quadratic reference loop -> bounded prefix, 1 core
+        n_pre = min(batch.n_updates, 60_000)
+        data = batch.data[:int(batch.upd_off[n_pre])]
+        uo, du = batch.upd_off[:n_pre + 1], np.array([0, n_pre], np.uint64)
+        dt = timed_runs(lambda: oracle.merge_batch(data, uo, du, mode=0, threads=1), 3)
+        return {"value": len(data) / dt / 1e9, "unit": "GB/s", "cores": 1, "kind": "port",
+                "docs_per_s": 1 / dt, "cpu_model": model, "nproc": nproc,
+                "sample": f"first {n_pre} updates of the trace ({len(data)} B) as one merge_updates_v1 call, "
+                          f"oracle literal yrs loop (quadratic per-iteration decoder re-sort), 1 core, "
+                          f"median of 3 after 1 warm-up: {dt:.3f} s"}
+    # sample sized so one all-cores run takes ~cpu_seconds (assumes ~25 MB/s per core)
+    per_doc = max(1, batch.n_bytes // max(1, batch.n_docs))
+    n_all = int(min(batch.n_docs, max(16, a.cpu_seconds * 25e6 * share / per_doc)))
+    n_one = int(min(batch.n_docs, max(4, a.cpu_seconds * 25e6 / per_doc)))
+    s_all = batch.prefix(n_all)
+    s_one = batch.prefix(n_one)
+    t_all = timed_runs(lambda: oracle.merge_batch(s_all.data, s_all.upd_off, s_all.doc_upd, mode=0,
+                                                  threads=share), 5)
+    t_one = timed_runs(lambda: oracle.merge_batch(s_one.data, s_one.upd_off, s_one.doc_upd, mode=0, threads=1), 5)
+    return {"value": s_all.n_bytes / t_all / 1e9, "unit": "GB/s", "cores": share, "kind": "port",
+            "docs_per_s": n_all / t_all, "cpu_model": model, "nproc": nproc,
+            "one_core": {"value": s_one.n_bytes / t_one / 1e9, "unit": "GB/s", "docs_per_s": n_one / t_one,
+                         "sample_docs": n_one, "sample_bytes": s_one.n_bytes},
+            "sample": f"first {n_all} docs of the same workload ({s_all.n_bytes} B), oracle literal yrs loop "
+                      f"(per-iteration decoder re-sort, DS re-squash), {share} threads (the job's CPU share of "
+                      f"{nproc} host CPUs), median of 5 after 1 warm-up: {t_all:.3f} s"}
+
+
+def run_merge(a, rank, world, dev):
+    import dist
+    import ymerge
+    batch, desc, scaling, cfg = build_merge(a, rank, world)
+    t_b = torch.from_numpy(batch.data if batch.n_bytes else np.zeros(1, np.uint8)).to(dev)
     t_u = torch.from_numpy(batch.upd_off.view(np.int64)).to(dev)
     t_d = torch.from_numpy(batch.doc_upd.view(np.int64)).to(dev)
     torch.cuda.synchronize(dev)
-    eng = ymerge.Engine(local)
+    eng = ymerge.Engine(dev.index)
 
     def step():
         return eng.merge_device(t_b.data_ptr(), batch.n_bytes, t_u.data_ptr(), batch.n_updates, t_d.data_ptr(),
@@ -95,59 +189,158 @@ def main():
     out_bytes = res.out_bytes
     _, _, st = res.to_host()
     n_err = int((st != 0).sum())
-    ms_merge = float(np.mean([s["ms_fast"] for s in kstats]))
-    ms_decode = float(np.mean([s["ms_decode"] for s in kstats]))
-    ms_kernel = ms_merge + ms_decode
-    ms_exact = float(np.mean([s["ms_exact"] for s in kstats]))
+    mean = lambda k: float(np.mean([s[k] for s in kstats]))  # noqa: E731
+    ms_decode, ms_fast, ms_exact = mean("ms_decode"), mean("ms_fast"), mean("ms_exact")
+    ms_pipe = ms_decode + ms_fast + ms_exact
     docs_exact = int(kstats[-1]["docs_exact"])
-    allst = dist.gather_stats([batch.n_docs, batch.n_bytes, out_bytes, n_err, elapsed, ms_kernel], device=dev)
-    if rank != 0:
-        dist.finalize()
-        return
 
+    e2e = None
+    if not a.no_e2e:  # end-to-end: pinned host arena -> H2D -> pipeline -> pack -> D2H
+        h_b = torch.from_numpy(batch.data if batch.n_bytes else np.zeros(1, np.uint8)).pin_memory()
+        h_u = torch.from_numpy(batch.upd_off.view(np.int64)).pin_memory()
+        h_d = torch.from_numpy(batch.doc_upd.view(np.int64)).pin_memory()
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        g_b, g_u, g_d = (x.to(dev, non_blocking=True) for x in (h_b, h_u, h_d))
+        torch.cuda.synchronize(dev)
+        r = eng.merge_device(g_b.data_ptr(), batch.n_bytes, g_u.data_ptr(), batch.n_updates, g_d.data_ptr(),
+                             batch.n_docs)
+        r.to_host()
+        e2e = time.perf_counter() - t
+        del g_b, g_u, g_d
+
+    allst = dist.gather_stats([batch.n_docs, batch.n_bytes, out_bytes, n_err, elapsed, ms_pipe,
+                               e2e or 0.0], device=dev)
+    if rank != 0:
+        return None
     t_max = float(allst[:, 4].max())
     docs_total = float(allst[:, 0].sum()) * a.steps
     bytes_in_total = float(allst[:, 1].sum()) * a.steps
-    ms_step = t_max / a.steps * 1e3
-    value = bytes_in_total / t_max / 1e9
-    # roofline of the merge kernel pair (k_decode -> k_fast_merge; together they are the path,
-    # neither does the merge alone), algorithmic bytes = input + output
+    # roofline of the merge pipeline (k_decode -> k_fast_merge -> exact engine for handed-over
+    # documents; together they are the path), algorithmic bytes = input + output
     alg_bytes = batch.n_bytes + out_bytes
-    achieved = alg_bytes / (ms_kernel * 1e-3) / 1e9
-    traffic = pmc_traffic()
+    achieved = alg_bytes / (ms_pipe * 1e-3) / 1e9
+    cpu = None
+    if not a.no_cpu_baseline and world == 1:
+        cpu = cpu_merge_baseline(batch, a)
+    line = {
+        "metric": METRIC, "value": bytes_in_total / t_max / 1e9, "unit": "GB/s", "n_gpus": world,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": t_max / a.steps * 1e3, "higher_is_better": True,
+        "scaling": scaling, "vs_baseline": None, "dtype": "u8", "data": "synthetic" if a.workload != "c1" else
+        "automerge-paper editing trace (CC BY 4.0) replayed into per-op updates",
+        "docs_per_s": docs_total / t_max,
+        "config": dict({"workload": desc + ", inputs HBM-resident", "bytes_in_per_gpu": int(allst[0, 1]),
+                        "bytes_out_per_gpu": int(allst[0, 2]), "updates_per_gpu": batch.n_updates,
+                        "parallelism": f"doc-hash sharding x{world}", "error_docs": int(allst[:, 3].sum())},
+                       **cfg),
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(a.workload),
+                     "kernel": "k_decode+k_fast_merge(+exact engine)", "kernel_ms": ms_pipe,
+                     "k_decode_ms": ms_decode, "k_fast_merge_ms": ms_fast, "exact_path_ms": ms_exact,
+                     "docs_exact_path": docs_exact, "alg_bytes_per_launch": alg_bytes},
+        "end_to_end": None if e2e is None else {
+            "value": float(allst[:, 1].sum()) / float(allst[:, 6].max()) / 1e9, "unit": "GB/s",
+            "note": "pinned host arena -> H2D -> merge -> pack -> D2H, one batch"},
+        "cpu_baseline": cpu,
+    }
+    return line
 
+
+def run_diff(a, rank, world, dev):
+    """C5: diff_updates_v1 of compacted documents (the C2 merge outputs) against remote SVs."""
+    import dist
+    import workloads
+    import ymerge
+    docs, ops = a.docs or 100_000, a.ops or 1_000
+    ids = dist.shard(world * docs, rank, world) if world > 1 else np.arange(docs, dtype=np.uint64)
+    eng = ymerge.Engine(dev.index)
+    # compact in chunks on the GPU (the merge outputs are the C5 documents)
+    parts, chunk = [], 20_000
+    for c0 in range(0, len(ids), chunk):
+        b = workloads.text_docs(0, ops, ids=ids[c0:c0 + chunk])
+        out, off, st = eng.merge_host(b.data, b.upd_off, b.doc_upd)
+        assert not st.any(), "compaction failed"
+        parts.append((out, off))
+    data = np.concatenate([p[0] for p in parts])
+    lens = np.concatenate([np.diff(p[1]) for p in parts]).astype(np.uint64)
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+
+    def sv_fn(dd, oo):
+        return eng.state_vector_host(dd, oo)
+    db = workloads.compacted_docs(data, offs, sv_fn=sv_fn)
+    t_b = torch.from_numpy(db.data).to(dev)
+    t_u = torch.from_numpy(db.upd_off.view(np.int64)).to(dev)
+    t_s = torch.from_numpy(db.sv if len(db.sv) else np.zeros(1, np.uint8)).to(dev)
+    t_so = torch.from_numpy(db.sv_off.view(np.int64)).to(dev)
+    torch.cuda.synchronize(dev)
+
+    def step():
+        return eng.diff_device(t_b.data_ptr(), t_u.data_ptr(), t_s.data_ptr(), t_so.data_ptr(), db.n_docs)
+
+    for _ in range(a.warmup):
+        step()
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    kstats = []
+    for _ in range(a.steps):
+        res = step()
+        kstats.append(eng.stats())
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    out_bytes = res.out_bytes
+    _, _, st = res.to_host()
+    n_err = int((st != 0).sum())
+    mean = lambda k: float(np.mean([s[k] for s in kstats]))  # noqa: E731
+    ms_pipe = mean("ms_fast") + mean("ms_exact") + mean("ms_tail")
+    bytes_in = db.n_bytes + int(db.sv_off[-1])
+    allst = dist.gather_stats([db.n_docs, bytes_in, out_bytes, n_err, elapsed, ms_pipe], device=dev)
+    if rank != 0:
+        return None
+    t_max = float(allst[:, 4].max())
+    alg = bytes_in + out_bytes  # |update| + |remote SV| + |diff| (SURVEY §8d)
+    achieved = alg / (ms_pipe * 1e-3) / 1e9
     cpu = None
     if not a.no_cpu_baseline and world == 1:
         import oracle
-        n_s = min(a.cpu_sample, batch.n_docs)
-        sample = batch.subset(range(n_s))
-        threads = min(16, os.cpu_count() or 1)
-        t = time.perf_counter()
-        oracle.merge_batch(sample.data, sample.upd_off, sample.doc_upd, mode=0, threads=threads)
-        dt = time.perf_counter() - t
-        cpu = {"value": sample.n_bytes / dt / 1e9, "unit": "GB/s", "cores": threads, "kind": "port",
-               "docs_per_s": n_s / dt,
-               "sample": f"first {n_s} docs of the same workload ({sample.n_bytes} B), oracle literal yrs loop "
-                         f"(per-iteration decoder re-sort, DS re-squash), {threads} threads, {dt:.2f} s wall"}
-
-    line = {
-        "metric": METRIC, "value": value, "unit": "GB/s", "n_gpus": world, "steps": a.steps,
-        "warmup": a.warmup, "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-        "docs_per_s": docs_total / t_max,
-        "config": {"workload": f"C2: {a.docs} synthetic YText docs x {a.ops} single-op v1 updates per GPU, "
-                               "batched merge_updates_v1, inputs HBM-resident",
-                   "docs_per_gpu": a.docs, "updates_per_doc": a.ops,
-                   "bytes_in_per_gpu": int(allst[0, 1]), "bytes_out_per_gpu": int(allst[0, 2]),
-                   "parallelism": f"doc-hash sharding x{world}", "error_docs": int(allst[:, 3].sum())},
+        model, nproc, share = host_cpu()
+        per = max(1, bytes_in // max(1, db.n_docs))
+        n_s = int(min(db.n_docs, max(16, a.cpu_seconds * 60e6 * share / per)))
+        ub, uo = db.data[:int(db.upd_off[n_s])], db.upd_off[:n_s + 1]
+        sb, so = db.sv[:int(db.sv_off[n_s])], db.sv_off[:n_s + 1]
+        dt = timed_runs(lambda: oracle.diff_batch(ub, uo, sb, so, threads=share), 5)
+        cpu = {"value": (len(ub) + len(sb)) / dt / 1e9, "unit": "GB/s", "cores": share, "kind": "port",
+               "docs_per_s": n_s / dt, "cpu_model": model, "nproc": nproc,
+               "sample": f"first {n_s} documents, oracle diff_updates_v1 restatement, {share} threads, "
+                         f"median of 5 after 1 warm-up: {dt:.3f} s"}
+    return {
+        "metric": METRIC_DIFF, "value": float(allst[:, 1].sum()) * a.steps / t_max / 1e9, "unit": "GB/s",
+        "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": t_max / a.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "docs_per_s": float(allst[:, 0].sum()) * a.steps / t_max,
+        "config": {"workload": f"C5: diff_updates_v1 of {docs} compacted docs per GPU (C2 merge outputs of {ops} "
+                               "updates) against per-doc remote state vectors, inputs HBM-resident",
+                   "docs_per_gpu": docs, "bytes_in_per_gpu": int(allst[0, 1]),
+                   "bytes_out_per_gpu": int(allst[0, 2]), "error_docs": int(allst[:, 3].sum()),
+                   "parallelism": f"doc-hash sharding x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_decode+k_fast_merge", "kernel_ms": ms_kernel, "k_decode_ms": ms_decode,
-                     "k_fast_merge_ms": ms_merge, "exact_path_ms": ms_exact,
-                     "docs_exact_path": docs_exact, "alg_bytes_per_launch": alg_bytes},
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic("c5"), "kernel": "k_plan+k_exec",
+                     "kernel_ms": ms_pipe, "k_plan_ms": mean("ms_fast"), "replan_ms": mean("ms_exact"),
+                     "k_exec_ms": mean("ms_tail"), "alg_bytes_per_launch": alg},
         "cpu_baseline": cpu,
     }
-    print(json.dumps(line))
+
+
+def main():
+    a = parse()
+    import dist
+    rank, world, local = dist.init_from_env("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    line = run_diff(a, rank, world, dev) if a.workload == "c5" else run_merge(a, rank, world, dev)
+    if rank == 0:
+        print(json.dumps(line))
     dist.finalize()
 
 

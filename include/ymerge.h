@@ -5,7 +5,8 @@
  *   ymerge_updates_v1                  replaces yrs::merge_updates_v1                 yrs/src/alt.rs:15-28
  *   ydiff_updates_v1                   replaces yrs::diff_updates_v1                  yrs/src/alt.rs:73-81
  *   yencode_state_vector_from_update_v1 replaces yrs::encode_state_vector_from_update_v1 yrs/src/alt.rs:54-57
- *   ybinary_destroy                    same contract as yffi's ybinary_destroy       yffi/src/lib.rs:384-388
+ *   ymerge_binary_destroy              same contract as yffi's ybinary_destroy       yffi/src/lib.rs:384-388
+ *   ybinary_destroy                    weak alias of ymerge_binary_destroy (see below)
  * yffi in this snapshot exports no merge/diff-of-updates function;
  * the signatures follow yffi conventions: `const char *` + `uint32_t` length
  * inputs, a library-owned `char *` result with its length in `*out_len`, NULL on
@@ -49,9 +50,17 @@ char *ymerge_updates_v1(const char *const *updates, const uint32_t *updates_len,
 char *ydiff_updates_v1(const char *update, uint32_t update_len, const char *state_vector, uint32_t sv_len,
                        uint32_t *out_len);
 char *yencode_state_vector_from_update_v1(const char *update, uint32_t update_len, uint32_t *out_len);
+/* frees a buffer returned by the three calls above */
+void ymerge_binary_destroy(char *ptr, uint32_t len);
+/* yffi's name, exported as a WEAK symbol: alone it frees this library's buffers; in a
+ * process that also links yffi, yffi's (strong) ybinary_destroy wins and this library's
+ * buffers must be freed with ymerge_binary_destroy. */
 void ybinary_destroy(char *ptr, uint32_t len);
 /* error code of the last failed call on this thread (0 after a success) */
 uint8_t ymerge_last_error(void);
+/* device of the single-document calls (default: env YMERGE_DEVICE, else 0);
+ * returns 0 or YMERGE_ERR_DEVICE for a device that does not exist */
+int ymerge_set_default_device(int device);
 
 /* ---------------------------------------------------------------- batched, device-resident */
 typedef struct ymerge_ctx ymerge_ctx;
@@ -79,7 +88,9 @@ typedef struct {
 } ymerge_device_result;
 
 /* merge_updates_v1 over a batch whose arena (n_bytes) and offsets (n_updates + 1,
- * n_docs + 1) already live in HBM of the context's device.
+ * n_docs + 1) already live in HBM of the context's device.  The kernels load the arena
+ * in aligned 4/16-byte words: d_bytes must stay readable for 16 bytes past n_bytes (pad
+ * the allocation; the host entry points do).  Same for the update/SV arenas below.
  * Returns 0 or YMERGE_ERR_DEVICE. */
 int ymerge_updates_v1_batch_device(ymerge_ctx *ctx, const uint8_t *d_bytes, uint64_t n_bytes,
                                    const uint64_t *d_upd_off, uint64_t n_updates, const uint64_t *d_doc_upd,

@@ -13,19 +13,23 @@
  * the order DeleteSet and StateVector clients are written in.
  *
  * Policies where yrs is not deterministic or not total (documented in DESIGN.md):
- *  - Any::Map is a RandomState HashMap in yrs (any.rs:23): we keep first-seen key
- *    order, last value wins on duplicate keys.  Same for Doc options (doc.rs:814).
+ *  - Any::Map is a RandomState HashMap in yrs (any.rs:23): a repeated key keeps its last
+ *    value and each distinct key is written at its last occurrence.  Doc options
+ *    (doc.rs:814) are rebuilt in as_any order.
  *  - allocation failures: a fallible try_reserve fails (NotEnoughMemory) and an
  *    infallible with_capacity aborts (REFERENCE_PANIC) when it would need more
  *    than 2^36 bytes.
  *  - Item-vs-GC ties at one (client, clock) make yrs' comparator inconsistent
  *    (update.rs:580-582); we follow Rust's insertion sort (exact for <= 20 live
  *    decoders, unpinned above).
- *  - Embed/Format JSON (serde_json round trip) is not restated: YO_ERR_UNSUPPORTED.
+ *  - Embed/Format JSON goes through the serde_json + ryu restatement below (JSON section);
+ *    objects with >= 2 distinct keys are RandomState-ordered in yrs: written at each key's
+ *    last occurrence (the same policy as Any maps above).
  */
 #include "yrs_oracle.h"
 
 #include <math.h>
+#include <stdio.h>
 #include <pthread.h>
 #include <stdbool.h>
 #include <stdlib.h>
@@ -423,8 +427,7 @@ static void upd_free(upd_t *u) {
 
 /* ------------------------------------------------------------------ Any (any.rs:37-83) */
 /* Validates one Any value.  Policy shared with the device: a container nested
- * 64 deep -> UNSUPPORTED; duplicate keys in an ItemContent::Any map -> UNSUPPORTED
- * (yrs collapses them into a RandomState HashMap whose order is random anyway). */
+ * 64 deep -> UNSUPPORTED.  (Duplicate map keys are legal: any_encode collapses them.) */
 static int any_skip2(rd_t *r, int depth, bool check_dups) {
   uint8_t tag;
   TRY(rd_u8(r, &tag));
@@ -442,19 +445,8 @@ static int any_skip2(rd_t *r, int depth, bool check_dups) {
     TRY(rd_var_u64(r, &n));
     if (n && (n > (1ull << 40) || cap_to_buckets((size_t)n) * 49ull > ALLOC_LIMIT)) return YO_ERR_REFERENCE_PANIC;
     if (depth >= 64) return YO_ERR_UNSUPPORTED;
-    size_t map_start = r->i;
     for (uint64_t i = 0; i < n; i++) {
       TRY(rd_buf(r, &s, &n32));
-      if (check_dups) {
-        rd_t q = {r->p, r->n, map_start};
-        for (uint64_t j = 0; j < i; j++) {
-          const uint8_t *ks;
-          uint32_t kn;
-          rd_buf(&q, &ks, &kn);
-          if (kn == n32 && !memcmp(ks, s, kn)) return YO_ERR_UNSUPPORTED;
-          any_skip2(&q, depth + 1, false);
-        }
-      }
       TRY(any_skip2(r, depth + 1, check_dups));
     }
     return 0;
@@ -525,7 +517,8 @@ static void any_encode(rd_t *r, wb_t *w) {
     return;
   case 118: {
     rd_var_u64(r, &n);
-    /* keys in first-seen order, last value wins (policy for RandomState map order) */
+    /* HashMap::insert (any.rs:61-68): a repeated key keeps its last value; RandomState
+     * order policy: each distinct key is written where it occurs last */
     VEC(span_t) keys = {0};
     VEC(size_t) vals = {0};
     for (uint64_t i = 0; i < n; i++) {
@@ -533,14 +526,16 @@ static void any_encode(rd_t *r, wb_t *w) {
       rd_buf(r, &k.p, &k.n);
       size_t vpos = r->i;
       any_skip(NULL, r, 0);
-      size_t j = 0;
-      for (; j < keys.n; j++)
-        if (keys.d[j].n == k.n && !memcmp(keys.d[j].p, k.p, k.n)) break;
-      if (j == keys.n) {
-        VPUSH(keys, k);
-        VPUSH(vals, vpos);
-      } else
-        vals.d[j] = vpos;
+      for (size_t j = 0; j < keys.n; j++)
+        if (keys.d[j].n == k.n && !memcmp(keys.d[j].p, k.p, k.n)) {
+          memmove(keys.d + j, keys.d + j + 1, (keys.n - j - 1) * sizeof(span_t));
+          memmove(vals.d + j, vals.d + j + 1, (vals.n - j - 1) * sizeof(size_t));
+          keys.n--;
+          vals.n--;
+          break;
+        }
+      VPUSH(keys, k);
+      VPUSH(vals, vpos);
     }
     size_t end = r->i;
     wb_u8(w, 118);
@@ -556,6 +551,619 @@ static void any_encode(rd_t *r, wb_t *w) {
     return;
   }
   }
+}
+
+/* ------------------------------------------------------------------ JSON (content refs 5/6)
+ * ItemContent::Embed / Format carry JSON text (read_json -> Any::from_json, write_json ->
+ * Any::to_json: yrs/src/updates/decoder.rs:175-178, encoder.rs:170-174, any.rs:185-198).
+ * Restated here: serde_json 1.0.116's deserializer (Cargo.lock:725-726; default features,
+ * i.e. no float_roundtrip / arbitrary_precision: parse_integer, parse_long_integer,
+ * parse_decimal(+_overflow), parse_exponent(+_overflow), f64_from_parts with the POW10
+ * table, parse_str escapes with paired-surrogate validation, recursion limit 128), yrs'
+ * `Deserialize for Any` (yrs/src/encoding/serde/de.rs:17-211) with From<i64>/TryFrom<u64>
+ * (yrs/src/any.rs:243-318), `Serialize for Any` (yrs/src/encoding/serde/ser.rs:16-54),
+ * serde_json's CompactFormatter (string escapes, itoa) and ryu 1.0.17's shortest f64
+ * (Cargo.lock:684-685) in its `format64` layout.  Every parse error is InvalidJSON.
+ * Objects are a RandomState HashMap (de.rs:196-206): duplicate keys collapse (last value
+ * wins) and the order of >= 2 distinct keys is random in yrs; policy: an entry is written
+ * at the position of its key's LAST occurrence.  Parity: integers/strings/literals follow
+ * the restated serde_json; floats are "parity unpinned" (no reference vector holds one),
+ * the shortest-digit generator is pinned against CPython's repr (tests/test_json.py). */
+typedef struct {
+  const uint8_t *p;
+  size_t n, i;
+  int remaining_depth;
+} jp_t;
+static void jp_ws(jp_t *j) {
+  while (j->i < j->n && (j->p[j->i] == ' ' || j->p[j->i] == '\n' || j->p[j->i] == '\t' || j->p[j->i] == '\r')) j->i++;
+}
+static int jp_peek(const jp_t *j) { return j->i < j->n ? j->p[j->i] : -1; }
+
+/* --- unbounded-precision helpers for the shortest f64 digits (Burger & Dybvig free format,
+ *     ties to even like ryu's d2d) */
+#define BN_LIMBS 48
+typedef struct {
+  uint32_t w[BN_LIMBS];
+} bn_t;
+static void bn_set(bn_t *a, uint64_t v) {
+  memset(a, 0, sizeof(*a));
+  a->w[0] = (uint32_t)v;
+  a->w[1] = (uint32_t)(v >> 32);
+}
+static void bn_mul_small(bn_t *a, uint32_t m) {
+  uint64_t c = 0;
+  for (int i = 0; i < BN_LIMBS; i++) {
+    uint64_t t = (uint64_t)a->w[i] * m + c;
+    a->w[i] = (uint32_t)t;
+    c = t >> 32;
+  }
+}
+static void bn_shl(bn_t *a, int k) {
+  while (k >= 32) {
+    memmove(a->w + 1, a->w, (BN_LIMBS - 1) * 4);
+    a->w[0] = 0;
+    k -= 32;
+  }
+  if (!k) return;
+  for (int i = BN_LIMBS - 1; i > 0; i--) a->w[i] = a->w[i] << k | a->w[i - 1] >> (32 - k);
+  a->w[0] <<= k;
+}
+static int bn_cmp(const bn_t *a, const bn_t *b) {
+  for (int i = BN_LIMBS - 1; i >= 0; i--)
+    if (a->w[i] != b->w[i]) return a->w[i] < b->w[i] ? -1 : 1;
+  return 0;
+}
+static void bn_add(bn_t *r, const bn_t *a, const bn_t *b) {
+  uint64_t c = 0;
+  for (int i = 0; i < BN_LIMBS; i++) {
+    uint64_t t = (uint64_t)a->w[i] + b->w[i] + c;
+    r->w[i] = (uint32_t)t;
+    c = t >> 32;
+  }
+}
+static void bn_sub(bn_t *a, const bn_t *b) { /* a -= b, a >= b */
+  int64_t br = 0;
+  for (int i = 0; i < BN_LIMBS; i++) {
+    int64_t t = (int64_t)a->w[i] - b->w[i] - br;
+    br = t < 0;
+    a->w[i] = (uint32_t)(t + (br ? (1ll << 32) : 0));
+  }
+}
+/* shortest digits of a finite x > 0: digits[0..n), value = 0.d1..dn * 10^k */
+static int f64_shortest(double x, char *digits, int *k_out) {
+  uint64_t bits;
+  memcpy(&bits, &x, 8);
+  int be = (int)((bits >> 52) & 0x7FF);
+  uint64_t f = bits & ((1ull << 52) - 1);
+  int e;
+  if (be == 0) e = -1074;
+  else {
+    f |= 1ull << 52;
+    e = be - 1075;
+  }
+  const bool even = (f & 1) == 0;
+  const bool unequal = be > 1 && f == (1ull << 52); /* lower gap is half the upper */
+  bn_t r, s, mp, mm;
+  if (e >= 0) {
+    bn_set(&r, f);
+    bn_shl(&r, e + (unequal ? 2 : 1));
+    bn_set(&s, unequal ? 4 : 2);
+    bn_set(&mp, 1);
+    bn_shl(&mp, e + (unequal ? 1 : 0));
+    bn_set(&mm, 1);
+    bn_shl(&mm, e);
+  } else {
+    bn_set(&r, f);
+    bn_shl(&r, unequal ? 2 : 1);
+    bn_set(&s, 1);
+    bn_shl(&s, -e + (unequal ? 2 : 1));
+    bn_set(&mp, unequal ? 2 : 1);
+    bn_set(&mm, 1);
+  }
+  int k = (int)ceil(log10(x) - 1e-10);
+  if (k >= 0)
+    for (int q = 0; q < k; q++) bn_mul_small(&s, 10);
+  else
+    for (int q = 0; q < -k; q++) {
+      bn_mul_small(&r, 10);
+      bn_mul_small(&mp, 10);
+      bn_mul_small(&mm, 10);
+    }
+  bn_t hi;
+  for (;;) { /* fixup: (r + m+) / s must be below 1 (<= 1 when the bound is inclusive) */
+    bn_add(&hi, &r, &mp);
+    int c = bn_cmp(&hi, &s);
+    if (even ? c >= 0 : c > 0) {
+      bn_mul_small(&s, 10);
+      k++;
+      continue;
+    }
+    bn_t hi10 = hi;
+    bn_mul_small(&hi10, 10);
+    c = bn_cmp(&hi10, &s);
+    if (even ? c < 0 : c <= 0) {
+      bn_mul_small(&r, 10);
+      bn_mul_small(&mp, 10);
+      bn_mul_small(&mm, 10);
+      k--;
+      continue;
+    }
+    break;
+  }
+  int n = 0;
+  for (;;) {
+    bn_mul_small(&r, 10);
+    bn_mul_small(&mp, 10);
+    bn_mul_small(&mm, 10);
+    int d = 0;
+    while (bn_cmp(&r, &s) >= 0) {
+      bn_sub(&r, &s);
+      d++;
+    }
+    int cl = bn_cmp(&r, &mm);
+    bool tc1 = even ? cl <= 0 : cl < 0;
+    bn_add(&hi, &r, &mp);
+    int ch = bn_cmp(&hi, &s);
+    bool tc2 = even ? ch >= 0 : ch > 0;
+    if (!tc1 && !tc2) {
+      digits[n++] = (char)('0' + d);
+      continue;
+    }
+    if (tc1 && tc2) {
+      bn_t r2 = r;
+      bn_shl(&r2, 1);
+      int c2 = bn_cmp(&r2, &s);
+      if (c2 > 0 || (c2 == 0 && (d & 1))) d++;
+    } else if (tc2)
+      d++;
+    digits[n++] = (char)('0' + d);
+    break;
+  }
+  /* a rounded-up 9 carries (never produced for doubles; kept for safety) */
+  for (int q = n - 1; q > 0 && digits[q] > '9'; q--) {
+    digits[q] = '0';
+    digits[q - 1]++;
+  }
+  if (digits[0] > '9') {
+    digits[0] = '1';
+    k++;
+  }
+  while (n > 1 && digits[n - 1] == '0') n--;
+  *k_out = k;
+  return n;
+}
+/* ryu::Buffer::format_finite (ryu/src/pretty/mod.rs format64) */
+static void f64_ryu(wb_t *w, double x) {
+  uint64_t bits;
+  memcpy(&bits, &x, 8);
+  if (bits >> 63) wb_u8(w, '-');
+  if ((bits << 1) == 0) {
+    wb_bytes(w, (const uint8_t *)"0.0", 3);
+    return;
+  }
+  char dg[40];
+  int kk;
+  const int len = f64_shortest(fabs(x), dg, &kk);
+  const int k = kk - len; /* value = digits * 10^k */
+  if (0 <= k && kk <= 16) {
+    wb_bytes(w, (const uint8_t *)dg, len);
+    for (int i = len; i < kk; i++) wb_u8(w, '0');
+    wb_bytes(w, (const uint8_t *)".0", 2);
+  } else if (0 < kk && kk <= 16) {
+    wb_bytes(w, (const uint8_t *)dg, kk);
+    wb_u8(w, '.');
+    wb_bytes(w, (const uint8_t *)dg + kk, len - kk);
+  } else if (-5 < kk && kk <= 0) {
+    wb_bytes(w, (const uint8_t *)"0.", 2);
+    for (int i = 0; i < -kk; i++) wb_u8(w, '0');
+    wb_bytes(w, (const uint8_t *)dg, len);
+  } else {
+    wb_u8(w, (uint8_t)dg[0]);
+    if (len > 1) {
+      wb_u8(w, '.');
+      wb_bytes(w, (const uint8_t *)dg + 1, len - 1);
+    }
+    wb_u8(w, 'e');
+    char eb[8];
+    int en = snprintf(eb, sizeof eb, "%d", kk - 1);
+    wb_bytes(w, (const uint8_t *)eb, en);
+  }
+}
+static void wb_i64(wb_t *w, int64_t v) { /* itoa */
+  char b[24];
+  int n = snprintf(b, sizeof b, "%lld", (long long)v);
+  wb_bytes(w, (const uint8_t *)b, n);
+}
+/* Serialize for Any, Number (ser.rs:25-34): `value as i64 as f64 == value` -> i64, else f64 */
+static void json_number(wb_t *w, double x) {
+  int64_t i;
+  if (x != x) i = 0;
+  else if (x >= 9223372036854775808.0) i = INT64_MAX; /* Rust `as` saturates */
+  else if (x < -9223372036854775808.0) i = INT64_MIN;
+  else i = (int64_t)x;
+  if ((double)i == x) wb_i64(w, i);
+  else if (isfinite(x)) f64_ryu(w, x);
+  else wb_bytes(w, (const uint8_t *)"null", 4);
+}
+/* serde_json format_escaped_str: ", \ and control bytes; \u00XX in lowercase hex */
+static void json_str_out(wb_t *w, const uint8_t *s, size_t n) {
+  static const char hex[] = "0123456789abcdef";
+  wb_u8(w, '"');
+  for (size_t i = 0; i < n; i++) {
+    uint8_t c = s[i];
+    switch (c) {
+    case '"': wb_bytes(w, (const uint8_t *)"\\\"", 2); break;
+    case '\\': wb_bytes(w, (const uint8_t *)"\\\\", 2); break;
+    case '\b': wb_bytes(w, (const uint8_t *)"\\b", 2); break;
+    case '\f': wb_bytes(w, (const uint8_t *)"\\f", 2); break;
+    case '\n': wb_bytes(w, (const uint8_t *)"\\n", 2); break;
+    case '\r': wb_bytes(w, (const uint8_t *)"\\r", 2); break;
+    case '\t': wb_bytes(w, (const uint8_t *)"\\t", 2); break;
+    default:
+      if (c < 0x20) {
+        uint8_t e[6] = {'\\', 'u', '0', '0', (uint8_t)hex[c >> 4], (uint8_t)hex[c & 15]};
+        wb_bytes(w, e, 6);
+      } else
+        wb_u8(w, c);
+    }
+  }
+  wb_u8(w, '"');
+}
+static int hexval(int c) {
+  if (c >= '0' && c <= '9') return c - '0';
+  if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+  if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+  return -1;
+}
+static int jp_hex4(jp_t *j, uint32_t *v) {
+  if (j->n - j->i < 4) return YO_ERR_INVALID_JSON;
+  uint32_t x = 0;
+  for (int q = 0; q < 4; q++) {
+    int h = hexval(j->p[j->i + q]);
+    if (h < 0) return YO_ERR_INVALID_JSON;
+    x = x << 4 | (uint32_t)h;
+  }
+  j->i += 4;
+  *v = x;
+  return 0;
+}
+static void wb_utf8(wb_t *w, uint32_t c) {
+  if (c < 0x80) wb_u8(w, (uint8_t)c);
+  else if (c < 0x800) {
+    wb_u8(w, (uint8_t)(0xC0 | c >> 6));
+    wb_u8(w, (uint8_t)(0x80 | (c & 63)));
+  } else if (c < 0x10000) {
+    wb_u8(w, (uint8_t)(0xE0 | c >> 12));
+    wb_u8(w, (uint8_t)(0x80 | ((c >> 6) & 63)));
+    wb_u8(w, (uint8_t)(0x80 | (c & 63)));
+  } else {
+    wb_u8(w, (uint8_t)(0xF0 | c >> 18));
+    wb_u8(w, (uint8_t)(0x80 | ((c >> 12) & 63)));
+    wb_u8(w, (uint8_t)(0x80 | ((c >> 6) & 63)));
+    wb_u8(w, (uint8_t)(0x80 | (c & 63)));
+  }
+}
+/* serde_json parse_str (validate = true): the opening quote is consumed; unescaped bytes -> w */
+static int jp_string(jp_t *j, wb_t *w) {
+  for (;;) {
+    if (j->i >= j->n) return YO_ERR_INVALID_JSON;
+    uint8_t c = j->p[j->i++];
+    if (c == '"') return 0;
+    if (c < 0x20) return YO_ERR_INVALID_JSON;
+    if (c != '\\') {
+      wb_u8(w, c);
+      continue;
+    }
+    if (j->i >= j->n) return YO_ERR_INVALID_JSON;
+    c = j->p[j->i++];
+    switch (c) {
+    case '"': case '\\': case '/': wb_u8(w, c); break;
+    case 'b': wb_u8(w, '\b'); break;
+    case 'f': wb_u8(w, '\f'); break;
+    case 'n': wb_u8(w, '\n'); break;
+    case 'r': wb_u8(w, '\r'); break;
+    case 't': wb_u8(w, '\t'); break;
+    case 'u': {
+      uint32_t n1;
+      TRY(jp_hex4(j, &n1));
+      if (n1 >= 0xDC00 && n1 <= 0xDFFF) return YO_ERR_INVALID_JSON;
+      if (n1 >= 0xD800 && n1 <= 0xDBFF) {
+        if (j->n - j->i < 2 || j->p[j->i] != '\\' || j->p[j->i + 1] != 'u') return YO_ERR_INVALID_JSON;
+        j->i += 2;
+        uint32_t n2;
+        TRY(jp_hex4(j, &n2));
+        if (n2 < 0xDC00 || n2 > 0xDFFF) return YO_ERR_INVALID_JSON;
+        n1 = (((n1 - 0xD800) << 10) | (n2 - 0xDC00)) + 0x10000;
+      }
+      wb_utf8(w, n1);
+      break;
+    }
+    default: return YO_ERR_INVALID_JSON;
+    }
+  }
+}
+static double pow10_tab(int e) { /* serde_json POW10[e], 0 <= e <= 308: correctly rounded 1e{e} */
+  char b[16];
+  snprintf(b, sizeof b, "1e%d", e);
+  return strtod(b, NULL);
+}
+/* f64_from_parts (not float_roundtrip) */
+static int f64_from_parts(bool positive, uint64_t significand, int64_t exponent, double *out) {
+  double f = (double)significand;
+  for (;;) {
+    uint64_t ae = exponent < 0 ? (uint64_t)(-exponent) : (uint64_t)exponent;
+    if (ae <= 308) {
+      if (exponent >= 0) {
+        f *= pow10_tab((int)ae);
+        if (isinf(f)) return YO_ERR_INVALID_JSON;
+      } else
+        f /= pow10_tab((int)ae);
+      break;
+    }
+    if (f == 0.0) break;
+    if (exponent >= 0) return YO_ERR_INVALID_JSON;
+    f /= 1e308;
+    exponent += 308;
+  }
+  *out = positive ? f : -f;
+  return 0;
+}
+#define OVERFLOW10(a, b, c) ((a) >= (c) / 10 && ((a) > (c) / 10 || (b) > (c) % 10))
+static int jp_exponent(jp_t *j, bool positive, uint64_t sig, int64_t starting_exp, double *out) {
+  j->i++; /* e / E */
+  bool positive_exp = true;
+  if (jp_peek(j) == '+') j->i++;
+  else if (jp_peek(j) == '-') {
+    j->i++;
+    positive_exp = false;
+  }
+  int c = jp_peek(j);
+  if (c < '0' || c > '9') return YO_ERR_INVALID_JSON;
+  j->i++;
+  int32_t exp = c - '0';
+  while ((c = jp_peek(j)) >= '0' && c <= '9') {
+    j->i++;
+    int32_t d = c - '0';
+    if (OVERFLOW10(exp, d, INT32_MAX)) { /* parse_exponent_overflow */
+      if (sig != 0 && positive_exp) return YO_ERR_INVALID_JSON;
+      while ((c = jp_peek(j)) >= '0' && c <= '9') j->i++;
+      *out = positive ? 0.0 : -0.0;
+      return 0;
+    }
+    exp = exp * 10 + d;
+  }
+  int64_t fe = positive_exp ? starting_exp + exp : starting_exp - exp; /* saturating_* on i32 */
+  if (fe > INT32_MAX) fe = INT32_MAX;
+  if (fe < INT32_MIN) fe = INT32_MIN;
+  return f64_from_parts(positive, sig, fe, out);
+}
+static int jp_decimal(jp_t *j, bool positive, uint64_t sig, int64_t exp_before, double *out) {
+  j->i++; /* '.' */
+  int64_t after = 0;
+  int c;
+  while ((c = jp_peek(j)) >= '0' && c <= '9') {
+    uint64_t d = (uint64_t)(c - '0');
+    if (OVERFLOW10(sig, d, UINT64_MAX)) { /* parse_decimal_overflow: ignore further digits */
+      while ((c = jp_peek(j)) >= '0' && c <= '9') j->i++;
+      if (c == 'e' || c == 'E') return jp_exponent(j, positive, sig, exp_before + after, out);
+      return f64_from_parts(positive, sig, exp_before + after, out);
+    }
+    j->i++;
+    sig = sig * 10 + d;
+    after--;
+  }
+  if (after == 0) return YO_ERR_INVALID_JSON;
+  c = jp_peek(j);
+  if (c == 'e' || c == 'E') return jp_exponent(j, positive, sig, exp_before + after, out);
+  return f64_from_parts(positive, sig, exp_before + after, out);
+}
+/* deserialize_any on a number, then Deserialize for Any, then Serialize for Any */
+static int jp_number(jp_t *j, bool positive, wb_t *w) {
+  int c = jp_peek(j);
+  if (c < '0' || c > '9') return YO_ERR_INVALID_JSON;
+  j->i++;
+  uint64_t sig = (uint64_t)(c - '0');
+  double f;
+  if (c == '0') {
+    c = jp_peek(j);
+    if (c >= '0' && c <= '9') return YO_ERR_INVALID_JSON; /* only one leading '0' */
+  } else {
+    while ((c = jp_peek(j)) >= '0' && c <= '9') {
+      uint64_t d = (uint64_t)(c - '0');
+      if (OVERFLOW10(sig, d, UINT64_MAX)) { /* parse_long_integer: further digits scale */
+        int64_t exponent = 0;
+        while ((c = jp_peek(j)) >= '0' && c <= '9') {
+          j->i++;
+          exponent++;
+        }
+        if (c == '.') TRY(jp_decimal(j, positive, sig, exponent, &f));
+        else if (c == 'e' || c == 'E') TRY(jp_exponent(j, positive, sig, exponent, &f));
+        else TRY(f64_from_parts(positive, sig, exponent, &f));
+        json_number(w, f); /* visit_f64 -> Any::Number */
+        return 0;
+      }
+      j->i++;
+      sig = sig * 10 + d;
+    }
+  }
+  c = jp_peek(j);
+  if (c == '.') {
+    TRY(jp_decimal(j, positive, sig, 0, &f));
+    json_number(w, f);
+    return 0;
+  }
+  if (c == 'e' || c == 'E') {
+    TRY(jp_exponent(j, positive, sig, 0, &f));
+    json_number(w, f);
+    return 0;
+  }
+  if (positive) { /* visit_u64 -> TryFrom<u64> for Any (any.rs:302-318) */
+    if (sig > (uint64_t)INT64_MAX) return YO_ERR_INVALID_JSON;
+    double v = (double)sig;
+    if (v <= 9007199254740991.0) json_number(w, v);
+    else wb_i64(w, v >= 9223372036854775808.0 ? INT64_MAX : (int64_t)v); /* BigInt(v as f64 as i64) */
+    return 0;
+  }
+  int64_t neg = (int64_t)(0 - sig); /* (significand as i64).wrapping_neg() */
+  if (neg >= 0) {                   /* -0 or below i64::MIN: visit_f64(-(significand as f64)) */
+    json_number(w, -(double)sig);
+    return 0;
+  }
+  double v = (double)neg; /* visit_i64 -> From<i64> (impl_from_bigint) */
+  if (v >= -9007199254740991.0) json_number(w, v);
+  else wb_i64(w, neg);
+  return 0;
+}
+typedef struct {
+  wb_t key; /* unescaped key bytes */
+  wb_t val; /* canonical value text */
+} jent_t;
+static int jp_value(jp_t *j, wb_t *w) {
+  jp_ws(j);
+  int c = jp_peek(j);
+  switch (c) {
+  case 'n': case 't': case 'f': {
+    const char *lit = c == 'n' ? "null" : c == 't' ? "true" : "false";
+    size_t ln = strlen(lit);
+    if (j->n - j->i < ln || memcmp(j->p + j->i, lit, ln)) return YO_ERR_INVALID_JSON;
+    j->i += ln;
+    wb_bytes(w, (const uint8_t *)lit, ln);
+    return 0;
+  }
+  case '-': j->i++; return jp_number(j, false, w);
+  case '"': {
+    j->i++;
+    wb_t s = {0};
+    int e = jp_string(j, &s);
+    if (!e) json_str_out(w, s.d, s.n);
+    VFREE(s);
+    return e;
+  }
+  case '[': {
+    if (--j->remaining_depth == 0) return YO_ERR_INVALID_JSON;
+    j->i++;
+    wb_u8(w, '[');
+    jp_ws(j);
+    if (jp_peek(j) == ']') j->i++;
+    else
+      for (bool first = true;; first = false) {
+        if (!first) wb_u8(w, ',');
+        TRY(jp_value(j, w));
+        jp_ws(j);
+        c = jp_peek(j);
+        if (c == ']') {
+          j->i++;
+          break;
+        }
+        if (c != ',') return YO_ERR_INVALID_JSON;
+        j->i++;
+        jp_ws(j);
+        if (jp_peek(j) == ']') return YO_ERR_INVALID_JSON; /* trailing comma */
+      }
+    wb_u8(w, ']');
+    j->remaining_depth++;
+    return 0;
+  }
+  case '{': {
+    if (--j->remaining_depth == 0) return YO_ERR_INVALID_JSON;
+    j->i++;
+    VEC(jent_t) es = {0};
+    int err = 0;
+    jp_ws(j);
+    if (jp_peek(j) == '}') j->i++;
+    else
+      for (;;) {
+        jp_ws(j);
+        if (jp_peek(j) != '"') {
+          err = YO_ERR_INVALID_JSON;
+          break;
+        }
+        j->i++;
+        jent_t e = {{0}, {0}};
+        VPUSH(es, e);
+        jent_t *cur = &es.d[es.n - 1];
+        if ((err = jp_string(j, &cur->key))) break;
+        jp_ws(j);
+        if (jp_peek(j) != ':') {
+          err = YO_ERR_INVALID_JSON;
+          break;
+        }
+        j->i++;
+        if ((err = jp_value(j, &cur->val))) break;
+        jp_ws(j);
+        c = jp_peek(j);
+        if (c == '}') {
+          j->i++;
+          break;
+        }
+        if (c != ',') {
+          err = YO_ERR_INVALID_JSON;
+          break;
+        }
+        j->i++;
+        jp_ws(j);
+        if (jp_peek(j) == '}') {
+          err = YO_ERR_INVALID_JSON; /* trailing comma */
+          break;
+        }
+      }
+    if (!err) {
+      wb_u8(w, '{');
+      bool first = true;
+      for (size_t a = 0; a < es.n; a++) {
+        bool later = false;
+        for (size_t b = a + 1; b < es.n && !later; b++)
+          later = es.d[b].key.n == es.d[a].key.n && !memcmp(es.d[b].key.d, es.d[a].key.d, es.d[a].key.n);
+        if (later) continue; /* HashMap::insert: the last value of a key survives */
+        if (!first) wb_u8(w, ',');
+        first = false;
+        json_str_out(w, es.d[a].key.d, es.d[a].key.n);
+        wb_u8(w, ':');
+        wb_bytes(w, es.d[a].val.d, es.d[a].val.n);
+      }
+      wb_u8(w, '}');
+      j->remaining_depth++;
+    }
+    for (size_t a = 0; a < es.n; a++) {
+      VFREE(es.d[a].key);
+      VFREE(es.d[a].val);
+    }
+    VFREE(es);
+    return err;
+  }
+  default:
+    if (c >= '0' && c <= '9') return jp_number(j, true, w);
+    return YO_ERR_INVALID_JSON;
+  }
+}
+/* serde_json::from_str::<Any>(src) then Any::to_json: canonical text into w, or InvalidJSON */
+static int json_canon(const uint8_t *s, size_t n, wb_t *w) {
+  jp_t j = {s, n, 0, 128};
+  TRY(jp_value(&j, w));
+  jp_ws(&j);
+  return j.i == j.n ? 0 : YO_ERR_INVALID_JSON; /* TrailingCharacters */
+}
+/* test hooks: canonical JSON text, and ryu's format of one f64 */
+int yo_json_canon(const uint8_t *s, size_t n, uint8_t **out, size_t *out_len) {
+  wb_t w = {0};
+  int e = json_canon(s, n, &w);
+  if (e) {
+    VFREE(w);
+    return e;
+  }
+  wb_u8(&w, 0);
+  *out = w.d;
+  *out_len = w.n - 1;
+  return 0;
+}
+int yo_f64_ryu(double x, char *buf, size_t cap) {
+  wb_t w = {0};
+  f64_ryu(&w, x);
+  size_t n = w.n < cap - 1 ? w.n : cap - 1;
+  memcpy(buf, w.d, n);
+  buf[n] = 0;
+  VFREE(w);
+  return (int)n;
 }
 
 /* ------------------------------------------------------------------ content decode (block.rs:1786-1835) */
@@ -633,13 +1241,19 @@ static int content_decode(upd_t *u, rd_t *r, uint8_t ref, blk_t *b) {
   }
   case 3: TRY(rd_buf(r, &b->cs.p, &b->cs.n)); b->len = 1; return 0;
   case 4: TRY(rd_buf(r, &b->cs.p, &b->cs.n)); b->len = str_len16(b->cs.p, b->cs.n); return 0;
-  case 5: TRY(rd_buf(r, &b->cs.p, &b->cs.n)); b->len = 1; b->unsupported = 1; return 0;
-  case 6:
+  case 5: case 6: { /* read_json (decoder.rs:175-178): serde_json parse at decode time */
     TRY(rd_buf(r, &b->cs.p, &b->cs.n));
-    TRY(rd_buf(r, &b->cs2.p, &b->cs2.n));
+    span_t js = b->cs;
+    if (ref == 6) {
+      TRY(rd_buf(r, &b->cs2.p, &b->cs2.n));
+      js = b->cs2;
+    }
+    wb_t t = {0};
+    int e = json_canon(js.p, js.n, &t);
+    VFREE(t);
     b->len = 1;
-    b->unsupported = 1;
-    return 0;
+    return e;
+  }
   case 7: { /* TypeRef::decode (types/mod.rs:160-200), weak feature on (yffi) */
     TRY(rd_u8(r, &b->tref));
     b->len = 1;
@@ -1019,7 +1633,16 @@ static int encode_item(wb_t *w, const upd_t *u, const blk_t *b, uint32_t off) {
     wb_str(w, s, n);
     return 0;
   }
-  case 5: case 6: return YO_ERR_UNSUPPORTED;
+  case 5: /* ItemContent::Embed: write_json (encoder.rs:170-174) */
+  case 6: { /* ItemContent::Format: write_key + write_json */
+    if (b->ref == 6) wb_str(w, b->cs.p, b->cs.n);
+    const span_t js = b->ref == 6 ? b->cs2 : b->cs;
+    wb_t t = {0};
+    int e = json_canon(js.p, js.n, &t);
+    if (!e) wb_str(w, t.d, (uint32_t)t.n);
+    VFREE(t);
+    return e;
+  }
   case 7:
     wb_u8(w, b->tref);
     if (b->tref == 3) wb_str(w, b->cs.p, b->cs.n);

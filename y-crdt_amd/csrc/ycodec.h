@@ -8,9 +8,10 @@
 //   Any                yrs/src/any.rs:37-183 (number canonicalisation any.rs:136-154)
 //   TypeRef / Move / Doc options  types/mod.rs:118-200, moving.rs:277-333, doc.rs:814-872
 //   hashbrown order    std HashMap + ClientHasher (utils/client_hasher.rs)
-// Policies shared with the CPU oracle: allocation limit
-// 2^36 B, Any nesting <= 64, Any maps keep first-seen key order (duplicate keys
-// -> UNSUPPORTED on device), Embed/Format JSON -> UNSUPPORTED.
+//   Embed/Format JSON  serde_json + ryu round trip (yjson.h)
+// Policies shared with the CPU oracle: allocation limit 2^36 B, Any
+// nesting <= 64 (UNSUPPORTED beyond), Any/JSON maps with duplicate keys collapse to the
+// last value, written at the position of the key's last occurrence.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -149,6 +150,8 @@ template <class W> __device__ __forceinline__ void w_str(W &w, const uint8_t *s,
   w_var(w, n);
   w.bytes(s, n);
 }
+
+#include "yjson.h"
 
 // ------------------------------------------------------------------ UTF-8 (core::str next_code_point)
 __device__ __forceinline__ uint32_t utf8_next(const uint8_t *s, uint32_t n, uint32_t &i) {
@@ -314,28 +317,46 @@ __device__ __forceinline__ bool bytes_eq(const uint8_t *a, const uint8_t *b, uin
     if (a[i] != b[i]) return false;
   return true;
 }
-// key at [ks, ks+kn): is it equal to any previous key of the map starting at map_start?
-__device__ __forceinline__ bool map_key_dup(const Cur &c, uint32_t map_start, uint32_t nprev, uint32_t ks,
-                                            uint32_t kn) {
-  Cur s = c;
-  s.i = map_start;
-  for (uint32_t j = 0; j < nprev; j++) {
+// Does a later entry of the map repeat the key [ks, ks+kn)?  c.i = start of the current
+// entry's value, `rest` = entries after the current one.  Malformed tails answer false
+// (the walk itself reports the error).
+__device__ __noinline__ bool map_key_later(Cur c, uint64_t rest, uint32_t ks, uint32_t kn) {
+  if (any_skip(c)) return false;
+  for (uint64_t j = 0; j < rest; j++) {
     uint32_t l;
     bool cn;
-    rd_var_u32(s, l, cn);
-    if (l == kn && bytes_eq(s.p + s.i, c.p + ks, kn)) return true;
-    s.i += l;
-    any_skip(s);
+    if (rd_var_u32(c, l, cn) || l > c.n - c.i) return false;
+    if (l == kn && bytes_eq(c.p + c.i, c.p + ks, kn)) return true;
+    c.i += l;
+    if (any_skip(c)) return false;
   }
   return false;
 }
-template <bool CHECK_DUPS = true, class W> __device__ __noinline__ int any_walk(Cur &c, W &w, bool &reenc) {
+// Output sink that can be muted: the earlier entries of a repeated Any-map key.
+template <class W> struct MuteW {
+  W &w;
+  bool mute;
+  __device__ __forceinline__ void u8(uint8_t b) {
+    if (!mute) w.u8(b);
+  }
+  __device__ __forceinline__ void bytes(const uint8_t *s, uint32_t k) {
+    if (!mute) w.bytes(s, k);
+  }
+};
+// A map with duplicate keys holds each key once (HashMap::insert, any.rs:61-68): the entry
+// count is the distinct-key count and an entry is written at its key's last occurrence.
+template <bool CHECK_DUPS = true, class W> __device__ __noinline__ int any_walk(Cur &c, W &w0, bool &reenc) {
   AnyFrame st[ANY_MAX_DEPTH];
-  int depth = 0;
+  MuteW<W> w{w0, false};
+  int depth = 0, mute_at = -1; // frame depth whose current entry is muted
   for (;;) {
     // key of a map entry?
     if (depth > 0 && st[depth - 1].map_start != ~0u) {
       AnyFrame &f = st[depth - 1];
+      if (mute_at == depth) { // the muted entry's value is complete
+        mute_at = -1;
+        w.mute = false;
+      }
       if (f.remaining == 0) {
         depth--;
         if (depth == 0) return 0;
@@ -343,15 +364,16 @@ template <bool CHECK_DUPS = true, class W> __device__ __noinline__ int any_walk(
       }
       uint32_t kl;
       bool cn;
-      uint32_t kpos = c.i;
       YM_TRY(rd_var_u32(c, kl, cn));
       if (!cn) reenc = true;
       uint32_t ks = c.i;
       YM_TRY(rd_skip(c, kl));
-      if (CHECK_DUPS && map_key_dup(c, f.map_start, f.nkeys, ks, kl)) return E_UNSUPPORTED;
-      (void)kpos;
       f.nkeys++;
       f.remaining--;
+      if (CHECK_DUPS && f.remaining && mute_at < 0 && map_key_later(c, f.remaining, ks, kl)) {
+        mute_at = depth;
+        w.mute = true;
+      }
       w_str(w, c.p + ks, kl);
     } else if (depth > 0) {
       AnyFrame &f = st[depth - 1];
@@ -466,8 +488,24 @@ template <bool CHECK_DUPS = true, class W> __device__ __noinline__ int any_walk(
         return E_PANIC;
       }
       w.u8(tag);
-      w_var(w, n);
       if (depth >= ANY_MAX_DEPTH) return E_UNSUPPORTED;
+      if (CHECK_DUPS && tag == 118 && n >= 2) { // distinct keys (a malformed map fails in the walk)
+        Cur q = c;
+        uint64_t nd = 0;
+        for (uint64_t j = 0; j < n; j++) {
+          uint32_t l;
+          bool cn2;
+          if (rd_var_u32(q, l, cn2) || l > q.n - q.i) break;
+          const uint32_t ks = q.i;
+          q.i += l;
+          nd += !map_key_later(q, n - 1 - j, ks, l);
+          if (any_skip(q)) break;
+        }
+        if (nd != n) reenc = true;
+        w_var(w, nd < n ? nd : n);
+      } else {
+        w_var(w, n);
+      }
       st[depth].remaining = n;
       st[depth].map_start = tag == 118 ? c.i : ~0u;
       st[depth].nkeys = 0;
@@ -639,20 +677,19 @@ __device__ __noinline__ SlowRes parse_content_slow(const uint8_t *p, uint32_t n,
       }
       return 0;
     }
-    case 5:
+    case 5: case 6: { // Embed (json) / Format (key, json): re-serialised on encode
+      if (ref == 6) {
+        YM_TRY(rd_var_u32(c, v, cn));
+        YM_TRY(rd_skip(c, v));
+      }
       YM_TRY(rd_var_u32(c, v, cn));
       YM_TRY(rd_skip(c, v));
+      Counter cnt;
+      YM_TRY(json_canon(c.p + c.i - v, v, cnt));
       bi.len = 1;
-      bi.unsupported = true;
+      bi.reenc = true;
       return 0;
-    case 6:
-      YM_TRY(rd_var_u32(c, v, cn));
-      YM_TRY(rd_skip(c, v));
-      YM_TRY(rd_var_u32(c, v, cn));
-      YM_TRY(rd_skip(c, v));
-      bi.len = 1;
-      bi.unsupported = true;
-      return 0;
+    }
     case 7: {
       uint8_t tr;
       YM_TRY(rd_u8(c, tr));
@@ -931,7 +968,18 @@ __device__ __noinline__ int emit_block(const uint8_t *p, uint32_t n, uint32_t po
     w_str(w, s, sn);
     return 0;
   }
-  case 5: case 6: return E_UNSUPPORTED;
+  case 5: case 6: { // write_key + write_json (encoder.rs:170-179): canonical JSON text
+    if (ref == 6) {
+      rd_var_u32(c, v, cn);
+      w_str(w, p + c.i, v);
+      c.i += v;
+    }
+    rd_var_u32(c, v, cn);
+    Counter cnt;
+    YM_TRY(json_canon(p + c.i, v, cnt));
+    w_var(w, cnt.n);
+    return json_canon(p + c.i, v, w);
+  }
   case 7: {
     uint8_t tr;
     rd_u8(c, tr);

@@ -496,7 +496,9 @@ __global__ void __launch_bounds__(NT, 3) k_fast_merge(BatchIn b, FastCaps caps, 
       o.out_start[d] = slot;
     }
   };
-  if (B1 - B0 >= (1ull << 31)) {
+  // update indices are packed as (i << 8) into 31-bit LDS keys (first-occurrence order, first
+  // error): documents with 2^23 or more updates go to the exact engine
+  if (B1 - B0 >= (1ull << 31) || U >= (1u << 23)) {
     handover();
     return;
   }
@@ -561,6 +563,12 @@ __global__ void __launch_bounds__(NT, 3) k_fast_merge(BatchIn b, FastCaps caps, 
           snr = w3;
         }
       }
+      // one update above a cap can never fit; clamping each lane to its cap also keeps the
+      // 21-bit fields of the packed round scan below from wrapping (NT * cap < 2^21)
+      if (snb > caps.b_cap || sne > caps.e_cap || snr > caps.r_cap) {
+        flags |= 4;
+        snb = sne = snr = 0;
+      }
     }
     // packed scan: blocks | entries << 21 | ranges << 42 (each < 2^21 per round)
     uint64_t T;
@@ -571,9 +579,9 @@ __global__ void __launch_bounds__(NT, 3) k_fast_merge(BatchIn b, FastCaps caps, 
     NB += (uint32_t)(T & 0x1FFFFF);
     NE += (uint32_t)((T >> 21) & 0x1FFFFF);
     NR += (uint32_t)(T >> 42);
-    if (NB > caps.b_cap || NE > caps.e_cap || NR > caps.r_cap) {
+    if (NB > caps.b_cap || NE > caps.e_cap || NR > caps.r_cap || __syncthreads_or(flags & 4)) {
       flags |= 4;
-      break; // uniform: every lane sees the same totals
+      break; // uniform: every lane sees the same totals / the same OR
     }
     if (i < U && !e) {
       if (shape == REC_BLOCK) {

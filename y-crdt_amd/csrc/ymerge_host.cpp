@@ -44,6 +44,7 @@ struct DevBuf {
 };
 
 thread_local uint8_t g_last_error = 0;
+ymerge_batch_result *alloc_result(uint64_t n_docs, uint64_t out_bytes);
 
 } // namespace
 
@@ -57,6 +58,7 @@ struct ymerge_ctx {
   uint64_t *h_pinned = nullptr;
   hipEvent_t ev[6];
   ymerge_stats stats{};
+  uint64_t stamps_docs = 0; // documents covered by `stamps` (last merge batch)
   ym::FastCaps caps{0, 0, 1024, 512, 512}; // b_cap must equal FAST_BCAP (ymerge_fast.hip) // (unused), (unused), blocks, DS entries, DS ranges
   int fast_threads = 256;
   std::mutex mu;
@@ -158,12 +160,14 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     if (!c->stamps.ensure(nn * 16 * 8)) return YMERGE_ERR_DEVICE;
     hipMemsetAsync(c->stamps.p, 0, nn * 16 * 8, c->s);
     stamps = c->stamps.as<uint64_t>();
+    c->stamps_docs = n_docs;
   }
   ym::FastOut fo{arena, ostart, olen, status, path, stamps};
   if (c->fast_threads) {
     ym::launch_decode(d_bytes, d_upd_off, n_updates, c->rec.as<uint32_t>(), c->ovf.as<uint32_t>(), c->s);
     hipEventRecord(c->ev[5], c->s);
     ym::launch_fast_merge(b, c->caps, fo, c->fast_threads, c->s);
+    if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
   }
   else {
     hipEventRecord(c->ev[5], c->s);
@@ -192,6 +196,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     ym::launch_seq_merge(true, b, path, status, c->counts.as<uint32_t>(), c->scr_off.as<uint64_t>(),
                          c->scratch.as<uint32_t>(), nullptr, c->spill_off.as<uint64_t>(), arena, slots, ostart, olen,
                          nullptr, c->s);
+    if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
   }
   hipEventRecord(c->ev[2], c->s);
   // total output bytes (and packed offsets for host copies)
@@ -255,6 +260,7 @@ static int plan_exec(ymerge_ctx *c, bool diff, const uint8_t *d_bytes, const uin
   hipMemsetAsync(c->counter.p, 0, 64, c->s);
   hipEventRecord(c->ev[0], c->s);
   ym::launch_plan(diff, 0, b, ps, c->s);
+  if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
   hipEventRecord(c->ev[1], c->s);
   hipMemcpyAsync(c->h_pinned + 9, c->counter.p, 4, hipMemcpyDeviceToHost, c->s);
   if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
@@ -342,14 +348,20 @@ extern "C" int ymerge_result_to_host(ymerge_ctx *c, const ymerge_device_result *
 
 // diagnostic: copy per-document phase stamps (16 x u64 per document) of the last batch
 extern "C" int ymerge_debug_stamps(ymerge_ctx *c, uint64_t n_docs, uint64_t *dst) {
-  if (!c || !c->want_stamps || !c->stamps.p) return YMERGE_ERR_OTHER;
+  if (!c || !dst) return YMERGE_ERR_OTHER;
   std::lock_guard<std::mutex> g(c->mu);
+  if (!c->want_stamps || !c->stamps.p) return YMERGE_ERR_OTHER;
+  if (n_docs > c->stamps_docs) n_docs = c->stamps_docs; // never past the last batch's stamps
+  if (!n_docs) return 0;
+  hipSetDevice(c->device);
   if (hipMemcpy(dst, c->stamps.p, n_docs * 16 * 8, hipMemcpyDeviceToHost) != hipSuccess) return YMERGE_ERR_DEVICE;
   return 0;
 }
 
 extern "C" void ymerge_last_stats(ymerge_ctx *c, ymerge_stats *st) {
-  if (c && st) *st = c->stats;
+  if (!c || !st) return;
+  std::lock_guard<std::mutex> g(c->mu);
+  *st = c->stats;
 }
 
 extern "C" int ymerge_updates_v1_batch(ymerge_ctx *c, const uint8_t *bytes, const uint64_t *upd_off,
@@ -371,12 +383,8 @@ extern "C" int ymerge_updates_v1_batch(ymerge_ctx *c, const uint8_t *bytes, cons
   int st = merge_device(c, c->in_bytes.as<uint8_t>(), nbytes, c->in_upd_off.as<uint64_t>(), n_updates,
                         c->in_doc_upd.as<uint64_t>(), n_docs, &dr);
   if (st) return st;
-  auto *r = (ymerge_batch_result *)calloc(1, sizeof(ymerge_batch_result));
-  r->n_docs = n_docs;
-  r->out_bytes = dr.out_bytes;
-  r->out = (uint8_t *)malloc(dr.out_bytes + 1);
-  r->out_off = (uint64_t *)malloc((n_docs + 1) * 8);
-  r->status = (uint8_t *)malloc(n_docs + 1);
+  ymerge_batch_result *r = alloc_result(n_docs, dr.out_bytes);
+  if (!r) return YMERGE_ERR_NOT_ENOUGH_MEMORY;
   st = pack_to_host(c, &dr, n_docs, r->out, r->out_off, r->status);
   if (st) {
     ymerge_batch_result_destroy(r);
@@ -385,6 +393,23 @@ extern "C" int ymerge_updates_v1_batch(ymerge_ctx *c, const uint8_t *bytes, cons
   *out = r;
   return 0;
 }
+
+namespace {
+ymerge_batch_result *alloc_result(uint64_t n_docs, uint64_t out_bytes) {
+  auto *r = (ymerge_batch_result *)calloc(1, sizeof(ymerge_batch_result));
+  if (!r) return nullptr;
+  r->n_docs = n_docs;
+  r->out_bytes = out_bytes;
+  r->out = (uint8_t *)malloc(out_bytes + 1);
+  r->out_off = (uint64_t *)malloc((n_docs + 1) * 8);
+  r->status = (uint8_t *)malloc(n_docs + 1);
+  if (!r->out || !r->out_off || !r->status) {
+    ymerge_batch_result_destroy(r);
+    return nullptr;
+  }
+  return r;
+}
+} // namespace
 
 extern "C" void ymerge_batch_result_destroy(ymerge_batch_result *r) {
   if (!r) return;
@@ -395,12 +420,29 @@ extern "C" void ymerge_batch_result_destroy(ymerge_batch_result *r) {
 }
 
 // ---------------------------------------------------------------- single document API
+// The single-document calls run on one lazily created context per device; the device is
+// ymerge_set_default_device(), else env YMERGE_DEVICE, else 0.
 static std::mutex g_default_mu;
-static ymerge_ctx *g_default = nullptr;
+static std::vector<ymerge_ctx *> g_default;
+static int g_default_device = -1;
+extern "C" int ymerge_set_default_device(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return YMERGE_ERR_DEVICE;
+  std::lock_guard<std::mutex> g(g_default_mu);
+  g_default_device = device;
+  return 0;
+}
 static ymerge_ctx *default_ctx() {
   std::lock_guard<std::mutex> g(g_default_mu);
-  if (!g_default) g_default = ymerge_ctx_create(0);
-  return g_default;
+  if (g_default_device < 0) {
+    const char *v = getenv("YMERGE_DEVICE");
+    g_default_device = v ? atoi(v) : 0;
+  }
+  const int dev = g_default_device;
+  if (dev < 0) return nullptr;
+  if ((size_t)dev >= g_default.size()) g_default.resize(dev + 1, nullptr);
+  if (!g_default[dev]) g_default[dev] = ymerge_ctx_create(dev);
+  return g_default[dev];
 }
 
 extern "C" uint8_t ymerge_last_error(void) { return g_last_error; }
@@ -437,6 +479,11 @@ extern "C" char *ymerge_updates_v1(const char *const *updates, const uint32_t *u
   }
   uint64_t n = r->out_off[1] - r->out_off[0];
   char *res = (char *)malloc(n ? n : 1);
+  if (!res) {
+    g_last_error = YMERGE_ERR_NOT_ENOUGH_MEMORY;
+    ymerge_batch_result_destroy(r);
+    return nullptr;
+  }
   memcpy(res, r->out + r->out_off[0], n);
   *out_len = (uint32_t)n;
   ymerge_batch_result_destroy(r);
@@ -466,12 +513,8 @@ static int host_plan_exec(ymerge_ctx *c, bool diff, const uint8_t *bytes, const 
                      diff ? c->in_sv.as<uint8_t>() : nullptr, diff ? c->in_sv_off.as<uint64_t>() : nullptr, n_docs,
                      &dr);
   if (st) return st;
-  auto *r = (ymerge_batch_result *)calloc(1, sizeof(ymerge_batch_result));
-  r->n_docs = n_docs;
-  r->out_bytes = dr.out_bytes;
-  r->out = (uint8_t *)malloc(dr.out_bytes + 1);
-  r->out_off = (uint64_t *)malloc((n_docs + 1) * 8);
-  r->status = (uint8_t *)malloc(n_docs + 1);
+  ymerge_batch_result *r = alloc_result(n_docs, dr.out_bytes);
+  if (!r) return YMERGE_ERR_NOT_ENOUGH_MEMORY;
   st = pack_to_host(c, &dr, n_docs, r->out, r->out_off, r->status);
   if (st) {
     ymerge_batch_result_destroy(r);
@@ -502,6 +545,11 @@ static char *single_result(ymerge_batch_result *r, uint32_t *out_len) {
   }
   const uint64_t n = r->out_off[1] - r->out_off[0];
   char *res = (char *)malloc(n ? n : 1);
+  if (!res) {
+    g_last_error = YMERGE_ERR_NOT_ENOUGH_MEMORY;
+    ymerge_batch_result_destroy(r);
+    return nullptr;
+  }
   memcpy(res, r->out + r->out_off[0], n);
   *out_len = (uint32_t)n;
   ymerge_batch_result_destroy(r);
@@ -542,4 +590,8 @@ extern "C" char *yencode_state_vector_from_update_v1(const char *update, uint32_
   return single_result(r, out_len);
 }
 
-extern "C" void ybinary_destroy(char *ptr, uint32_t) { free(ptr); }
+extern "C" void ymerge_binary_destroy(char *ptr, uint32_t) { free(ptr); }
+// yffi-compatible name, exported WEAK: a process that also links yffi (whose strong
+// ybinary_destroy frees yrs' buffers) keeps yffi's definition and must free this library's
+// buffers with ymerge_binary_destroy; alone, ybinary_destroy resolves here.
+extern "C" __attribute__((weak)) void ybinary_destroy(char *ptr, uint32_t len) { ymerge_binary_destroy(ptr, len); }

@@ -62,6 +62,12 @@ class Batch:
         u0, u1 = int(self.doc_upd[d]), int(self.doc_upd[d + 1])
         return [self.data[int(self.upd_off[u]):int(self.upd_off[u + 1])].tobytes() for u in range(u0, u1)]
 
+    def prefix(self, n):
+        """The first n documents (views into the same arena; offsets start at 0)."""
+        u1 = int(self.doc_upd[n])
+        return Batch(self.data[:int(self.upd_off[u1])], self.upd_off[:u1 + 1], self.doc_upd[:n + 1],
+                     self.name + f"[:{n}]")
+
     def subset(self, docs):
         docs = list(docs)
         parts, offs, dus = [], [0], [0]
@@ -126,7 +132,8 @@ def zipf_counts(n_docs, alpha=1.5, kmax=10_000, seed=0x5EED):
 
 
 def zipf_docs(n_docs, seed=0x5EED, threads=None, ids=None):
-    """C3: Zipf(1.5)-skewed update counts on [1, 1e4] (ids: global doc ids of this shard)."""
+    """C3: Zipf(1.5)-skewed update counts on [1, 1e4].  With `ids` (global doc ids of this
+    shard) n_docs is the global document count and the shard's counts are drawn from it."""
     threads = threads or min(16, os.cpu_count() or 1)
     counts = zipf_counts(n_docs, seed=seed)
     if ids is not None:

@@ -73,7 +73,8 @@ def lib():
     L.ydiff_updates_v1.argtypes = [c.c_char_p, u32, c.c_char_p, u32, c.POINTER(u32)]
     L.yencode_state_vector_from_update_v1.restype = vp
     L.yencode_state_vector_from_update_v1.argtypes = [c.c_char_p, u32, c.POINTER(u32)]
-    L.ybinary_destroy.argtypes = [vp, u32]
+    L.ymerge_binary_destroy.argtypes = [vp, u32]
+    L.ymerge_set_default_device.argtypes = [c.c_int]
     L.ymerge_last_error.restype = c.c_uint8
     L.ydiff_updates_v1_batch.argtypes = [vp, vp, vp, vp, vp, u64, c.POINTER(c.c_void_p)]
     L.yencode_state_vector_from_update_v1_batch.argtypes = [vp, vp, vp, u64, c.POINTER(c.c_void_p)]
@@ -89,7 +90,7 @@ def _take(ptr, n):
             raise DeviceError("no usable MI355X (HIP)")
         raise YrsError(code)
     data = ctypes.string_at(ptr, n.value)
-    lib().ybinary_destroy(ptr, n.value)
+    lib().ymerge_binary_destroy(ptr, n.value)
     return data
 
 
