@@ -73,6 +73,9 @@ typedef struct {
   uint64_t docs_fast, docs_exact, docs_error;
   float ms_total, ms_fast, ms_exact, ms_tail;
   float ms_decode; /* merge: k_decode (ms_fast = k_fast_merge only) */
+  float ms_big;    /* merge: documents over the LDS capacities (k_big_count + k_big_merge) */
+  uint32_t reserved;
+  uint64_t docs_big; /* merge: documents written by the tiled kernel (docs_exact: exact engine) */
 } ymerge_stats;
 
 /* Device-resident result, owned by the context, valid until the next batch.
@@ -104,6 +107,20 @@ int yencode_state_vector_from_update_v1_batch_device(ymerge_ctx *ctx, const uint
 int ydiff_updates_v1_batch_device(ymerge_ctx *ctx, const uint8_t *d_bytes, const uint64_t *d_upd_off,
                                   const uint8_t *d_sv_bytes, const uint64_t *d_sv_off, uint64_t n_docs,
                                   ymerge_device_result *res);
+/* y-sync serving over the update algebra (yrs/src/sync/protocol.rs:62-69, 219-272), one
+ * compacted update per document:
+ *  ysync_step1_v1_*: Message::Sync(SyncStep1(sv)).encode = [0, 0, varbuf(sv)] with
+ *    sv = encode_state_vector_from_update_v1(update);
+ *  ysync_step2_v1_*: decodes each document's client message, which must be
+ *    Message::Sync(SyncStep1(remote sv)) (document d's message is msg[msg_off[d] ..
+ *    msg_off[d+1]); other messages -> status UNSUPPORTED, malformed ones the decode error),
+ *    and answers Message::Sync(SyncStep2(diff_updates_v1(update, remote sv))) =
+ *    [0, 1, varbuf(diff)]: what Protocol::handle_sync_step1 replies. */
+int ysync_step1_v1_batch_device(ymerge_ctx *ctx, const uint8_t *d_bytes, const uint64_t *d_upd_off, uint64_t n_docs,
+                                ymerge_device_result *res);
+int ysync_step2_v1_batch_device(ymerge_ctx *ctx, const uint8_t *d_bytes, const uint64_t *d_upd_off,
+                                const uint8_t *d_msg, const uint64_t *d_msg_off, uint64_t n_docs,
+                                ymerge_device_result *res);
 /* pack the last device result into host buffers: out (res->out_bytes), out_off (n_docs + 1,
  * document d at out[out_off[d] .. out_off[d+1])), status (n_docs) */
 int ymerge_result_to_host(ymerge_ctx *ctx, const ymerge_device_result *res, uint64_t n_docs, uint8_t *out,
@@ -128,6 +145,10 @@ int ydiff_updates_v1_batch(ymerge_ctx *ctx, const uint8_t *bytes, const uint64_t
 /* encode_state_vector_from_update_v1 over a batch (yrs/src/alt.rs:54-57) */
 int yencode_state_vector_from_update_v1_batch(ymerge_ctx *ctx, const uint8_t *bytes, const uint64_t *upd_off,
                                               uint64_t n_docs, ymerge_batch_result **res);
+int ysync_step1_v1_batch(ymerge_ctx *ctx, const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_docs,
+                         ymerge_batch_result **res);
+int ysync_step2_v1_batch(ymerge_ctx *ctx, const uint8_t *bytes, const uint64_t *upd_off, const uint8_t *msg,
+                         const uint64_t *msg_off, uint64_t n_docs, ymerge_batch_result **res);
 void ymerge_batch_result_destroy(ymerge_batch_result *res);
 
 #ifdef __cplusplus

@@ -102,6 +102,34 @@ def encode_state_vector_from_update_v1(update):
     return _take(out, olen)
 
 
+def sync_step1_v1(update):
+    a, an = _buf(update)
+    L = lib()
+    L.yo_sync_step1_v1.argtypes = [ctypes.POINTER(ctypes.c_uint8), ctypes.c_size_t,
+                                   ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)), ctypes.POINTER(ctypes.c_size_t)]
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    st = L.yo_sync_step1_v1(a, an, ctypes.byref(out), ctypes.byref(olen))
+    if st:
+        raise OracleError(st)
+    return _take(out, olen)
+
+
+def sync_step2_v1(update, msg):
+    a, an = _buf(update)
+    b, bn = _buf(msg)
+    L = lib()
+    P = ctypes.POINTER
+    L.yo_sync_step2_v1.argtypes = [P(ctypes.c_uint8), ctypes.c_size_t, P(ctypes.c_uint8), ctypes.c_size_t,
+                                   P(P(ctypes.c_uint8)), P(ctypes.c_size_t)]
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    st = L.yo_sync_step2_v1(a, an, b, bn, ctypes.byref(out), ctypes.byref(olen))
+    if st:
+        raise OracleError(st)
+    return _take(out, olen)
+
+
 def status_of(fn, *args, **kw):
     try:
         return 0, fn(*args, **kw)

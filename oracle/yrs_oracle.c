@@ -2332,6 +2332,47 @@ int yo_encode_state_vector_from_update_v1(const uint8_t *update, size_t len, uin
 
 void yo_free(void *p) { free(p); }
 
+/* ------------------------------------------------------------------ y-sync framing
+ * Message::encode / SyncMessage::encode (yrs/src/sync/protocol.rs:219-233, 245-258):
+ * [MSG_SYNC = 0, step tag, varbuf(payload)]; Message::decode + SyncMessage::decode
+ * (protocol.rs:179-203, 259-272) for the client's message, tags read as read_var::<u8>
+ * (varint.rs:92-106).  Only SyncStep1 requests are answered: other messages are not
+ * update-algebra work (UNSUPPORTED). */
+static int sync_frame(uint8_t tag, uint8_t *payload, size_t n, uint8_t **out, size_t *out_len) {
+  wb_t w = {0};
+  wb_u8(&w, 0);
+  wb_u8(&w, tag);
+  wb_var(&w, n);
+  wb_bytes(&w, payload, n);
+  yo_free(payload);
+  return finish(&w, out, out_len);
+}
+int yo_sync_step1_v1(const uint8_t *update, size_t len, uint8_t **out, size_t *out_len) {
+  uint8_t *sv;
+  size_t n;
+  TRY(yo_encode_state_vector_from_update_v1(update, len, &sv, &n));
+  return sync_frame(0, sv, n, out, out_len);
+}
+int yo_sync_step2_v1(const uint8_t *update, size_t len, const uint8_t *msg, size_t mlen, uint8_t **out,
+                     size_t *out_len) {
+  rd_t r = {msg, mlen, 0};
+  uint32_t tag, sub;
+  const uint8_t *sv;
+  uint32_t svn;
+  TRY(rd_var_u32(&r, &tag));
+  if (tag > 255) return YO_ERR_VAR_INT;
+  if (tag != 0) return YO_ERR_UNSUPPORTED;
+  TRY(rd_var_u32(&r, &sub));
+  if (sub > 255) return YO_ERR_VAR_INT;
+  if (sub == 1 || sub == 2) return YO_ERR_UNSUPPORTED;
+  if (sub != 0) return YO_ERR_UNEXPECTED_VALUE;
+  TRY(rd_buf(&r, &sv, &svn));
+  uint8_t *d;
+  size_t n;
+  TRY(yo_diff_updates_v1(update, len, sv, svn, &d, &n));
+  return sync_frame(1, d, n, out, out_len);
+}
+
 /* ------------------------------------------------------------------ batch + threads (CPU baseline) */
 typedef struct {
   const uint8_t *bytes, *svbytes;

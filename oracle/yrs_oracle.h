@@ -44,6 +44,11 @@ int yo_diff_updates_v1(const uint8_t *update, size_t update_len, const uint8_t *
 int yo_encode_state_vector_from_update_v1(const uint8_t *update, size_t len, uint8_t **out,
                                           size_t *out_len);
 void yo_free(void *p);
+/* y-sync (yrs/src/sync/protocol.rs:62-69, 219-272): SyncStep1 message of an update's state
+ * vector, and the SyncStep2 reply to a client's SyncStep1 message */
+int yo_sync_step1_v1(const uint8_t *update, size_t len, uint8_t **out, size_t *out_len);
+int yo_sync_step2_v1(const uint8_t *update, size_t len, const uint8_t *msg, size_t mlen, uint8_t **out,
+                     size_t *out_len);
 int yo_sv_roundtrip(const uint8_t *p, size_t n, uint8_t **out, size_t *out_len);
 int yo_ds_offset(const uint8_t *p, size_t n, size_t *off);
 

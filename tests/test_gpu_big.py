@@ -1,0 +1,103 @@
+"""GPU parity of the tiled kernel for documents above the fast path's LDS capacities
+(ymerge_big.hip: > 1024 blocks, > 512 DeleteSet entries / ranges, > 64 distinct
+DeleteSet clients) and the routing between the three device paths (fast, tiled, exact
+engine).  Reference semantics: yrs/src/update.rs:537-704, yrs/src/id_set.rs:129-164."""
+import numpy as np
+import pytest
+
+import workloads
+from test_gpu_parity import _ds_update, _root_text_update, _var, batch_of, check_batch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def engine():
+    import ymerge
+    e = ymerge.Engine(0)
+    yield e
+    e.close()
+
+
+def test_c3_zipf_tail_on_tiled_kernel(engine, oracle):
+    """C3 documents above 1024 blocks take the tiled kernel; none needs the exact engine."""
+    b = workloads.zipf_docs(4000, seed=0x5EED)
+    big = int((np.diff(b.doc_upd) > 1400).sum())  # > 1024 blocks (80% of the updates insert)
+    assert big > 10
+    check_batch(engine, oracle, b)
+    st = engine.stats()
+    assert st["docs_exact"] == 0, st
+    assert st["docs_big"] >= big, st
+
+
+def test_c1_trace_on_tiled_kernel(engine, oracle):
+    """The whole automerge-paper trace (259,778 per-op updates, one document)."""
+    b, _ = workloads.trace_updates()
+    check_batch(engine, oracle, b)
+    st = engine.stats()
+    assert st["docs_big"] == 1 and st["docs_exact"] == 0, st
+
+
+def test_large_multi_client_docs(engine, oracle):
+    """Interleaved clients (the tiled kernel's stable sort) at several sizes around the
+    2048-pair sort chunk and its merge passes."""
+    docs = []
+    for k, ops in enumerate((1100, 2047, 2049, 4100, 9000)):
+        b = workloads.text_docs(2, ops, seed=100 + k, min_clients=3, max_clients=4)
+        docs += [b.doc_updates(0), b.doc_updates(1)]
+    check_batch(engine, oracle, batch_of(docs))
+    assert engine.stats()["docs_exact"] == 0
+
+
+def test_shuffled_large_docs(engine, oracle):
+    """Updates in random order (clock order restored by the sort), duplicated updates."""
+    rng = np.random.default_rng(5)
+    docs = []
+    for n in (700, 1500, 3000):
+        ups = []
+        for c in (3, 9, 1 << 31):
+            clock = 0
+            for _ in range(n // 3):
+                s = "".join(chr(97 + int(x)) for x in rng.integers(0, 26, int(rng.integers(1, 5))))
+                ups.append(_root_text_update(c, clock, s))
+                clock += len(s)
+        ups += [ups[int(i)] for i in rng.integers(0, len(ups), len(ups) // 10)]
+        docs.append([ups[i] for i in rng.permutation(len(ups))])
+    check_batch(engine, oracle, batch_of(docs))
+    assert engine.stats()["docs_exact"] == 0
+
+
+def test_big_deletesets(engine, oracle):
+    """> 512 DeleteSet ranges / entries and > 64 distinct DeleteSet clients (tiled kernel's
+    hash table, hashbrown order over up to 1024 clients, range sort and union)."""
+    rng = np.random.default_rng(11)
+    docs = []
+    for n_cl, n_up, n_rng in ((3, 400, 3), (70, 80, 2), (300, 300, 1), (900, 1000, 1), (5, 2000, 4)):
+        ups = []
+        clients = [int(x) for x in rng.integers(0, 2 ** 32, n_cl)]
+        for _ in range(n_up):
+            ents = []
+            for c in rng.choice(clients, size=min(3, n_cl), replace=False):
+                rs = [(int(rng.integers(0, 5000)), int(rng.integers(1, 9))) for _ in range(n_rng)]
+                ents.append((int(c), rs))
+            ups.append(_ds_update(ents))
+        ups.append(_root_text_update(7, 0, "hello"))
+        docs.append(ups)
+    check_batch(engine, oracle, batch_of(docs))
+    st = engine.stats()
+    assert st["docs_big"] >= 4, st
+
+
+def test_big_doc_handovers(engine, oracle):
+    """Big documents that must still leave the tiled kernel: a partial overlap (exact
+    engine), a decode error in a late update (first error wins), > 1024 DeleteSet clients."""
+    docs = []
+    ups = [_root_text_update(5, i, "x") for i in range(1500)]
+    ups.append(_root_text_update(5, 700, "abc"))  # [700, 703) partially overlaps 701/702
+    docs.append(ups)
+    ups = [_root_text_update(5, i, "y") for i in range(1500)]
+    ups.insert(1400, b"\x01\x01")  # EndOfBuffer
+    docs.append(ups)
+    rng = np.random.default_rng(2)
+    docs.append([_ds_update([(int(c), [(0, 1)])]) for c in rng.integers(0, 2 ** 32, 1100)])
+    check_batch(engine, oracle, batch_of(docs))

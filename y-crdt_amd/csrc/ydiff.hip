@@ -472,6 +472,12 @@ __global__ void __launch_bounds__(64) k_plan(DiffBatch b, PlanScratch ps, int pa
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= b.n_docs) return;
   if (pass == 1 && !ps.big[d]) return;
+  if (b.pre_status && b.pre_status[d]) { // e.g. a y-sync message that is not SyncStep1
+    ps.big[d] = 0;
+    ps.status[d] = b.pre_status[d];
+    ps.size[d] = 0;
+    return;
+  }
   const uint64_t o0 = b.upd_off[d], o1 = b.upd_off[d + 1];
   const uint8_t *up = b.bytes + o0;
   const uint32_t un = (uint32_t)(o1 - o0);
@@ -479,7 +485,7 @@ __global__ void __launch_bounds__(64) k_plan(DiffBatch b, PlanScratch ps, int pa
   uint32_t svn = 0;
   if (DIFF) {
     svp = b.sv + b.sv_off[d];
-    svn = (uint32_t)(b.sv_off[d + 1] - b.sv_off[d]);
+    svn = (uint32_t)((b.sv_end ? b.sv_end[d] : b.sv_off[d + 1]) - b.sv_off[d]);
   }
   uint32_t *scr;
   PlanCaps cap;
@@ -502,8 +508,37 @@ __global__ void __launch_bounds__(64) k_plan(DiffBatch b, PlanScratch ps, int pa
     return;
   }
   if (pass == 0) ps.big[d] = 0;
+  // y-sync message: [MSG_SYNC, SyncStep2 | SyncStep1, varbuf(payload)] (protocol.rs:219-233)
+  if (b.frame && !st) sz += 2 + varlen(sz);
   ps.status[d] = (uint8_t)st;
   ps.size[d] = st ? 0 : sz;
+}
+
+// y-sync client message -> state vector slice (Message::decode + SyncMessage::decode,
+// yrs/src/sync/protocol.rs:179-203, 245-272; tags are read_var::<u8>)
+__global__ void k_sync_parse(const uint8_t *msg, const uint64_t *msg_off, uint32_t n, uint64_t *sv_off,
+                             uint64_t *sv_end, uint8_t *status) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= n) return;
+  Cur c{msg + msg_off[d], (uint32_t)(msg_off[d + 1] - msg_off[d]), 0};
+  bool cn;
+  uint32_t tag = 0, sub = 0, len = 0;
+  int e = rd_var_u32(c, tag, cn);
+  if (!e && tag > 255) e = E_VARINT;
+  if (!e && tag != 0) e = E_UNSUPPORTED; // awareness / auth / query / custom: not update algebra
+  if (!e) e = rd_var_u32(c, sub, cn);
+  if (!e && sub > 255) e = E_VARINT;
+  if (!e && (sub == 1 || sub == 2)) e = E_UNSUPPORTED; // SyncStep2 / Update: applied, not answered
+  if (!e && sub != 0) e = E_UNEXPECTED;
+  if (!e) e = rd_var_u32(c, len, cn);
+  if (!e && len > c.n - c.i) e = E_EOS;
+  sv_off[d] = msg_off[d] + c.i;
+  sv_end[d] = e ? msg_off[d] + c.i : msg_off[d] + c.i + len;
+  status[d] = (uint8_t)e;
+}
+void launch_sync_parse(const uint8_t *msg, const uint64_t *msg_off, uint32_t n, uint64_t *sv_off, uint64_t *sv_end,
+                       uint8_t *status, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_sync_parse, dim3((n + 255) / 256), dim3(256), 0, s, msg, msg_off, n, sv_off, sv_end, status);
 }
 
 __global__ void k_big_need(const uint64_t *upd_off, const uint8_t *big, uint32_t n, uint64_t *need) {
@@ -552,7 +587,7 @@ __global__ void __launch_bounds__(256) k_exec(DiffBatch b, PlanScratch ps, const
   uint32_t *ops = (uint32_t *)scr + L.ops;
   const uint32_t nops = scr[0];
   uint8_t *dst = out + out_off[d];
-  // op offsets: wave-wide exclusive scan of the sizes
+  // op offsets: wave-wide exclusive scan of the sizes (acc = the unframed payload size)
   uint32_t acc = 0;
   for (uint32_t r = 0; r < nops; r += 64) {
     const uint32_t k = r + lane;
@@ -565,6 +600,16 @@ __global__ void __launch_bounds__(256) k_exec(DiffBatch b, PlanScratch ps, const
     }
     if (k < nops) ops[OPW * k + 7] = acc + x - sz;
     acc += __shfl(x, 63, 64);
+  }
+  if (b.frame) { // y-sync header [MSG_SYNC, step tag, varbuf length]
+    const uint32_t hl = 2 + varlen(acc);
+    if (lane == 0) {
+      Writer w{dst, 0};
+      w.u8(0);
+      w.u8(b.frame == 1 ? 1 : 0);
+      w_var(w, acc);
+    }
+    dst += hl;
   }
   // header / re-encode ops: one lane each
   for (uint32_t k = lane; k < nops; k += 64) {

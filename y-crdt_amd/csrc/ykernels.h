@@ -35,7 +35,8 @@ void launch_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_upd
 struct FastCaps {
   uint32_t in_cap, u_cap, b_cap, e_cap, r_cap;
 };
-// per-document results; path 0 = written by the fast path, 1 = needs the exact engine
+// per-document results; path 0 = written, 1 = needs the exact engine, 2 = needs the tiled
+// kernel for documents above the LDS capacities
 struct FastOut {
   uint8_t *out; // output arena: document d's slot starts at 2*byte_start(d) + 64*d
   uint64_t *out_start, *out_len;
@@ -44,6 +45,12 @@ struct FastOut {
 };
 size_t fast_lds_bytes(const FastCaps &c);
 void launch_fast_merge(const BatchIn &b, const FastCaps &caps, const FastOut &o, int nt, hipStream_t s);
+
+// documents over the fast path's LDS capacities (path == 2): tiled, HBM scratch
+void launch_big_count(const BatchIn &b, const FastOut &o, uint32_t *counts, uint64_t *need, uint32_t *n_big,
+                      hipStream_t s);
+void launch_big_merge(const BatchIn &b, const uint32_t *counts, const uint64_t *scr_off, uint32_t *scratch,
+                      const FastOut &o, hipStream_t s);
 
 // exact per-document engine; `path` (optional) restricts it to documents with path == 1
 void launch_seq_count(const BatchIn &b, const uint8_t *path, uint8_t *status, uint32_t *counts, uint64_t *need,
@@ -67,7 +74,14 @@ struct DiffBatch {
   const uint8_t *sv;       // remote state vectors (diff only)
   const uint64_t *sv_off;  // n_docs + 1 (diff only)
   uint32_t n_docs;
+  const uint64_t *sv_end = nullptr;       // optional: doc d's SV is [sv_off[d], sv_end[d])
+  const uint8_t *pre_status = nullptr;    // optional: nonzero = the document failed before planning
+  uint32_t frame = 0;                     // y-sync framing: 0 none, 1 SyncStep2, 2 SyncStep1
 };
+// y-sync: parse one client message per document (must be Message::Sync(SyncStep1(sv)),
+// yrs/src/sync/protocol.rs:179-203, 245-272) -> SV slice [sv_off, sv_end) + status
+void launch_sync_parse(const uint8_t *msg, const uint64_t *msg_off, uint32_t n, uint64_t *sv_off, uint64_t *sv_end,
+                       uint8_t *status, hipStream_t s);
 struct PlanCaps {
   uint32_t C, E, R, O; // client sections, DeleteSet entries, squash ranges, output ops
 };

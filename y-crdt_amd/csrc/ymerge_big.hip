@@ -1,0 +1,858 @@
+// ymerge_big.hip — merge_updates_v1 for documents above the fast path's LDS capacities.
+//
+// The fast path (ymerge_fast.hip) keeps a whole document in LDS: at most 1024 blocks,
+// 512 DeleteSet entries / ranges, 64 distinct DeleteSet clients.  Documents beyond
+// that (Zipf-tail tenants of C3, long per-op logs such as the automerge-paper trace,
+// delete-heavy logs) run here with the same semantics, one 1024-lane workgroup per
+// document, the SoA block / DeleteSet tables in HBM scratch and every phase a loop
+// over tiles of 1024 elements with a carry between tiles:
+//   k_big_count  per document: counts (blocks, entries, ranges) from the k_decode
+//                records, first decode error, scratch words
+//   k_big_merge  gather records -> sort blocks by (client desc, clock asc, input order)
+//                (skipped when already ordered; else LDS bitonic chunks + stable merge
+//                passes) -> classify (segmented max-scan of block ends: keep / Skip gap /
+//                violation, duplicate check) -> sizes + offsets -> write (LDS-staged
+//                tiles) -> DeleteSet: distinct clients + first occurrence (LDS hash),
+//                hashbrown iteration order, ranges sorted by (client, start), segmented
+//                union, write.
+// Same fast-path precondition as the LDS kernel: a partial overlap or a
+// same-clock mismatch hands the document to the exact engine (path = 1).
+// Reference semantics: yrs/src/update.rs:537-704 (merge), :490-535 (encode),
+// yrs/src/id_set.rs:129-164, 385-410 (DeleteSet union and order).
+#include "yblock.h"
+
+namespace ym {
+
+constexpr int BIG_NT = 1024;
+constexpr uint32_t BIG_DCAP = 1024;   // distinct DeleteSet clients per document
+constexpr uint32_t BIG_DTAB = 2048;   // LDS hash slots for them (u64)
+constexpr uint32_t BIG_CHUNK = 2048;  // LDS bitonic chunk of the sort (key u64 + value u32)
+// LDS union region (phase-local): sort chunk (24 KB) / output stage / DeleteSet tables:
+//   [0, 16K) client hash table  [16K, 44K) 7 per-client arrays  [44K, 68K) sort chunk / slots
+constexpr uint32_t BIG_OFF_DARR = 8 * BIG_DTAB, BIG_OFF_SCR = BIG_OFF_DARR + 7 * 4 * BIG_DCAP;
+constexpr uint32_t BIG_UNION = BIG_OFF_SCR + 12 * BIG_CHUNK;
+
+struct BigMem {
+  uint32_t *bc, *bk, *bl, *bp, *bm; // [NB] blocks in input order
+  uint64_t *k0, *k1;                // [M] sort keys (ping-pong)
+  uint32_t *v0, *v1;                // [M] sort values
+  uint32_t *fE, *fF, *sseg;         // [NB] per sorted position: running end, flags; per client segment counts
+  uint32_t *ec, *et;                // [NE] DeleteSet entries
+  uint32_t *rs, *re, *ri;           // [NR] DeleteSet ranges
+  uint32_t *chead, *cend, *coff, *cpre; // [NR + 1] union of sorted live ranges
+};
+__host__ __device__ inline uint64_t big_words(uint32_t NB, uint32_t NE, uint32_t NR) {
+  const uint64_t M = (uint64_t)(NB > NR ? NB : NR) + 2;
+  return 4 * M + 2 * M + 8ull * NB + 2ull * NE + 3ull * NR + 4ull * (NR + 2) + 64;
+}
+__device__ inline BigMem big_carve(uint32_t *w, uint32_t NB, uint32_t NE, uint32_t NR) {
+  BigMem m;
+  const uint64_t M = (uint64_t)(NB > NR ? NB : NR) + 2;
+  uint64_t o = 0;
+  auto take = [&](uint64_t k) {
+    uint32_t *p = w + o;
+    o += (k + 1) & ~1ull; // keep 8-byte alignment
+    return p;
+  };
+  m.k0 = (uint64_t *)take(2 * M);
+  m.k1 = (uint64_t *)take(2 * M);
+  m.v0 = take(M);
+  m.v1 = take(M);
+  m.bc = take(NB);
+  m.bk = take(NB);
+  m.bl = take(NB);
+  m.bp = take(NB);
+  m.bm = take(NB);
+  m.fE = take(NB);
+  m.fF = take(NB);
+  m.sseg = take(NB);
+  m.ec = take(NE);
+  m.et = take(NE);
+  m.rs = take(NR);
+  m.re = take(NR);
+  m.ri = take(NR);
+  m.chead = take(NR + 2);
+  m.cend = take(NR + 2);
+  m.coff = take(NR + 2);
+  m.cpre = take(NR + 2);
+  return m;
+}
+
+// ------------------------------------------------------------------ k_big_count
+// One workgroup per document with path == 2 (handed over by k_fast_merge for capacity):
+// counts, first decode error in update order (yrs/src/alt.rs:21-25), scratch words.
+template <int NT>
+__global__ void __launch_bounds__(NT) k_big_count(BatchIn b, uint8_t *path, uint8_t *status, uint64_t *out_start,
+                                                  uint64_t *out_len, uint32_t *counts, uint64_t *need,
+                                                  uint32_t *n_big) {
+  const uint32_t d = blockIdx.x;
+  if (d >= b.n_docs) return;
+  const uint32_t t = threadIdx.x;
+  if (path[d] != 2) {
+    if (t == 0) need[d] = 0;
+    return;
+  }
+  __shared__ unsigned long long s_err, s_nb, s_ne, s_nr;
+  __shared__ uint32_t s_flags;
+  if (t == 0) {
+    s_err = ~0ull;
+    s_nb = s_ne = s_nr = 0;
+    s_flags = 0;
+  }
+  __syncthreads();
+  const uint64_t u0 = b.doc_upd[d], u1 = b.doc_upd[d + 1];
+  const uint32_t U = (uint32_t)(u1 - u0);
+  const uint64_t B0 = b.upd_off[u0];
+  uint64_t nb = 0, ne = 0, nr = 0;
+  uint32_t flags = 0;
+  for (uint32_t i = t; i < U; i += NT) {
+    const uint64_t a0 = b.upd_off[u0 + i], a1 = b.upd_off[u0 + i + 1];
+    const uint32_t ulen = (uint32_t)(a1 - a0);
+    const uint2 *rp = (const uint2 *)(b.rec + (size_t)(u0 + i) * REC_WORDS);
+    const uint2 x0 = rp[0], x1 = rp[1];
+    uint32_t w0 = x0.x, w1 = x0.y, w2 = x1.x, w3 = x1.y, w4 = 0, w5 = 0;
+    if (w0 & REC_SLOW) {
+      RegSink s;
+      s.nb = s.ne = s.nr = 0;
+      s.unsupported = s.big_ds = false;
+      s.ubase = 0;
+      WCur c;
+      wc_init(c, b.bytes + a0, ulen);
+      const int es = smwalk_update(c, s);
+      rec_pack(s, es, w0, w1, w2, w3, w4, w5);
+    }
+    const uint32_t e = w0 & 0xFF, shape = (w0 >> 10) & 3;
+    if (e) atomicMin(&s_err, ((unsigned long long)i << 8) | e);
+    if (w0 & REC_BIGDS) flags |= 2;
+    if (ulen >= (1u << 24)) flags |= 8;
+    if (!e) {
+      if (shape == REC_BLOCK) nb += 1;
+      else if (shape == REC_DS) {
+        ne += 1;
+        nr += (w0 >> 12) & 3;
+      } else if (shape == REC_COMPLEX) {
+        nb += w1;
+        ne += w2;
+        nr += w3;
+      }
+    }
+  }
+  atomicAdd(&s_nb, (unsigned long long)nb);
+  atomicAdd(&s_ne, (unsigned long long)ne);
+  atomicAdd(&s_nr, (unsigned long long)nr);
+  if (flags) atomicOr(&s_flags, flags);
+  __syncthreads();
+  if (t != 0) return;
+  const uint64_t slot = 2 * B0 + 64ull * d;
+  need[d] = 0;
+  if (s_err != ~0ull) { // the first failing update decides the document (yrs/src/alt.rs:21-25)
+    status[d] = (uint8_t)(s_err & 0xFF);
+    path[d] = 0;
+    out_len[d] = 0;
+    out_start[d] = slot;
+    return;
+  }
+  // per-update DeleteSet tables beyond DS_SMALL entries, blocks over 16 MB, documents
+  // whose offsets do not fit the 32-bit tables: exact engine
+  if (s_flags || s_nb >= (1ull << 28) || s_ne >= (1ull << 28) || s_nr >= (1ull << 28) ||
+      b.upd_off[u1] - B0 >= (1ull << 30)) {
+    path[d] = 1;
+    return;
+  }
+  counts[4 * d + 1] = (uint32_t)s_nb;
+  counts[4 * d + 2] = (uint32_t)s_ne;
+  counts[4 * d + 3] = (uint32_t)s_nr;
+  need[d] = (big_words((uint32_t)s_nb, (uint32_t)s_ne, (uint32_t)s_nr) + 1) & ~1ull;
+  atomicAdd(n_big, 1u);
+}
+
+// ------------------------------------------------------------------ workgroup sort
+// Stable sort of (key, value) pairs in HBM by key; values are distinct and ascending in
+// input order.  Chunks of BIG_CHUNK pairs are bitonic-sorted in LDS by (key, value) —
+// which equals the stable order — then bottom-up merge passes place every element at
+// base + i + (rank in the partner run): left-run elements count partner keys < k,
+// right-run elements count partner keys <= k (equal keys keep input order).
+// Returns the buffer pair holding the result (0: k0/v0, 1: k1/v1).
+template <int NT>
+__device__ int wg_sort(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1, uint32_t n, uint8_t *lds) {
+  uint64_t *ck = (uint64_t *)lds;
+  uint32_t *cv = (uint32_t *)(lds + 8 * BIG_CHUNK);
+  for (uint32_t c0 = 0; c0 < n; c0 += BIG_CHUNK) {
+    for (uint32_t j = threadIdx.x; j < BIG_CHUNK; j += NT) {
+      const uint32_t g = c0 + j;
+      ck[j] = g < n ? k0[g] : ~0ull;
+      cv[j] = g < n ? v0[g] : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    bitonic<NT>(ck, cv, BIG_CHUNK);
+    for (uint32_t j = threadIdx.x; j < BIG_CHUNK; j += NT) {
+      const uint32_t g = c0 + j;
+      if (g < n) {
+        k0[g] = ck[j];
+        v0[g] = cv[j];
+      }
+    }
+    __syncthreads();
+  }
+  uint64_t *ka = k0, *kb = k1;
+  uint32_t *va = v0, *vb = v1;
+  int which = 0;
+  for (uint32_t w = BIG_CHUNK; w < n; w <<= 1) {
+    for (uint32_t j = threadIdx.x; j < n; j += NT) {
+      const uint64_t kj = ka[j];
+      const uint32_t run = j / w, i = j - run * w;
+      const bool left = !(run & 1);
+      const uint32_t base = (left ? run : run - 1) * w;
+      uint32_t lo = left ? base + w : base, hi = left ? base + 2 * w : base + w;
+      if (lo > n) lo = n;
+      if (hi > n) hi = n;
+      const uint32_t b0 = lo;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const uint64_t km = ka[mid];
+        if (left ? (km < kj) : (km <= kj)) lo = mid + 1;
+        else hi = mid;
+      }
+      const uint32_t dst = base + i + (lo - b0);
+      kb[dst] = kj;
+      vb[dst] = va[j];
+    }
+    __syncthreads();
+    uint64_t *tk = ka;
+    ka = kb;
+    kb = tk;
+    uint32_t *tv = va;
+    va = vb;
+    vb = tv;
+    which ^= 1;
+  }
+  return which;
+}
+
+// ------------------------------------------------------------------ k_big_merge
+template <int NT> struct BigShared {
+  uint32_t ws[2 * (NT / 64) + 8];
+  uint64_t ws64[NT / 64 + 2];
+  uint32_t sc[32];
+  unsigned long long err;
+  __align__(16) uint8_t un[BIG_UNION + 64];
+};
+
+template <int NT>
+__global__ void __launch_bounds__(NT) k_big_merge(BatchIn b, const uint32_t *counts, const uint64_t *scr_off,
+                                                  uint32_t *scratch, FastOut o) {
+  const uint32_t d = blockIdx.x;
+  if (d >= b.n_docs || o.path[d] != 2) return;
+  __shared__ BigShared<NT> S;
+  const uint32_t t = threadIdx.x;
+  uint32_t *ws = S.ws, *sc = S.sc;
+  const uint32_t NB = counts[4 * d + 1], NE = counts[4 * d + 2], NR = counts[4 * d + 3];
+  BigMem m = big_carve(scratch + scr_off[d], NB, NE, NR);
+  const uint64_t u0 = b.doc_upd[d], u1 = b.doc_upd[d + 1];
+  const uint32_t U = (uint32_t)(u1 - u0);
+  const uint64_t B0 = b.upd_off[u0];
+  const uint32_t nbytes = (uint32_t)(b.upd_off[u1] - B0);
+  const uint8_t *in = b.bytes + B0;
+  const uint64_t slot = 2 * B0 + 64ull * d;
+  const uint64_t cap = 2ull * nbytes + 64;
+  uint8_t *out = o.out + slot;
+  auto finish = [&](uint8_t p, uint8_t st, uint64_t len) {
+    if (t == 0) {
+      o.path[d] = p;
+      o.status[d] = st;
+      o.out_len[d] = len;
+      o.out_start[d] = slot;
+    }
+  };
+
+  // ---- 1 gather: rounds of NT updates; the round's counts are scanned and every lane
+  //      writes its records at the scanned positions (records of k_decode, overflow words,
+  //      or a walk of the update for the shapes k_decode left to a later pass)
+  {
+    uint32_t NBr = 0, NEr = 0, NRr = 0;
+    for (uint32_t r0 = 0; r0 < U; r0 += NT) {
+      const uint32_t i = r0 + t;
+      uint32_t ubase = 0, ulen = 0, shape = 0, w0 = 0, w1 = 0, w2 = 0, w3 = 0, w4 = 0, w5 = 0;
+      uint32_t snb = 0, sne = 0, snr = 0;
+      bool walk = false;
+      if (i < U) {
+        const uint64_t a0 = b.upd_off[u0 + i], a1 = b.upd_off[u0 + i + 1];
+        ubase = (uint32_t)(a0 - B0);
+        ulen = (uint32_t)(a1 - a0);
+        const uint2 *rp = (const uint2 *)(b.rec + (size_t)(u0 + i) * REC_WORDS);
+        const uint2 x0 = rp[0], x1 = rp[1], x2 = rp[2];
+        w0 = x0.x;
+        w1 = x0.y;
+        w2 = x1.x;
+        w3 = x1.y;
+        w4 = x2.x;
+        w5 = x2.y;
+        if (w0 & REC_SLOW) {
+          RegSink s;
+          s.nb = s.ne = s.nr = 0;
+          s.unsupported = s.big_ds = false;
+          s.ubase = 0;
+          WCur c;
+          wc_init(c, in + ubase, ulen);
+          const int es = smwalk_update(c, s);
+          rec_pack(s, es, w0, w1, w2, w3, w4, w5);
+        }
+        shape = (w0 >> 10) & 3;
+        if (shape == REC_BLOCK) snb = 1;
+        else if (shape == REC_DS) {
+          sne = 1;
+          snr = (w0 >> 12) & 3;
+        } else if (shape == REC_COMPLEX) {
+          snb = w1;
+          sne = w2;
+          snr = w3;
+          walk = !(w0 & REC_OVF);
+        }
+      }
+      uint64_t T0, T1;
+      const uint64_t p0 = bscan_sum64<NT>((uint64_t)snb | ((uint64_t)sne << 32), S.ws64, T0);
+      const uint64_t p1 = bscan_sum64<NT>((uint64_t)snr, S.ws64, T1);
+      const uint32_t pb = NBr + (uint32_t)p0, pe = NEr + (uint32_t)(p0 >> 32), pr = NRr + (uint32_t)p1;
+      NBr += (uint32_t)T0;
+      NEr += (uint32_t)(T0 >> 32);
+      NRr += (uint32_t)T1;
+      if (i >= U) continue;
+      if (shape == REC_BLOCK) {
+        m.bc[pb] = w1;
+        m.bk[pb] = w2;
+        m.bl[pb] = w3;
+        m.bp[pb] = ubase + w4;
+        m.bm[pb] = w5;
+      } else if (shape == REC_DS) {
+        m.ec[pe] = w1;
+        m.et[pe] = 0x80000000u | (i << 8);
+        if (snr > 0) {
+          m.rs[pr] = w2;
+          m.re[pr] = w3;
+          m.ri[pr] = pe;
+        }
+        if (snr > 1) {
+          m.rs[pr + 1] = w4;
+          m.re[pr + 1] = w5;
+          m.ri[pr + 1] = pe;
+        }
+      } else if (shape == REC_COMPLEX && !walk) {
+        const uint32_t *ov = b.ovf + w4;
+        for (uint32_t k = 0; k < snb; k++) {
+          m.bc[pb + k] = ov[5 * k];
+          m.bk[pb + k] = ov[5 * k + 1];
+          m.bl[pb + k] = ov[5 * k + 2];
+          m.bp[pb + k] = ubase + ov[5 * k + 3];
+          m.bm[pb + k] = ov[5 * k + 4];
+        }
+        ov += 5 * snb;
+        for (uint32_t k = 0; k < sne; k++) {
+          m.ec[pe + k] = ov[k];
+          m.et[pe + k] = 0x80000000u | (i << 8);
+        }
+        if (sne >= 2) ds_order_packed(m.ec + pe, sne, m.et + pe, i << 8);
+        ov += sne;
+        for (uint32_t k = 0; k < snr; k++) {
+          m.rs[pr + k] = ov[3 * k];
+          m.re[pr + k] = ov[3 * k + 1];
+          m.ri[pr + k] = pe + ov[3 * k + 2];
+        }
+      } else if (shape == REC_COMPLEX) {
+        FastFill f{m.bc, m.bk, m.bl, m.bp, m.bm, m.ec, m.et, m.rs, m.re, m.ri, i, ubase, pb, pe, pr, 0};
+        WCur c;
+        wc_init(c, in + ubase, ulen);
+        smwalk_update(c, f);
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- 2 sort blocks by (client desc, clock asc, input order)
+  const uint32_t *sval = m.v0;
+  bool ident = true;
+  {
+    uint32_t bad = 0;
+    for (uint32_t j = t; j + 1 < NB; j += NT) {
+      const uint64_t a = ((uint64_t)(~m.bc[j]) << 32) | m.bk[j], c = ((uint64_t)(~m.bc[j + 1]) << 32) | m.bk[j + 1];
+      if (a > c) bad = 1;
+    }
+    ident = !__syncthreads_or(bad);
+    if (!ident) {
+      for (uint32_t j = t; j < NB; j += NT) {
+        m.k0[j] = ((uint64_t)(~m.bc[j]) << 32) | m.bk[j];
+        m.v0[j] = j;
+      }
+      __syncthreads();
+      if (wg_sort<NT>(m.k0, m.v0, m.k1, m.v1, NB, S.un)) sval = m.v1;
+    }
+  }
+  auto srt = [&](uint32_t j) -> uint32_t { return ident ? j : sval[j]; };
+
+  // ---- 3 classify (tiles of NT sorted positions, carries between tiles):
+  //      running end E (segmented max), keep / Skip / violation, duplicate check against
+  //      the last kept block, emitted blocks per client segment
+  uint32_t NC = 0; // client segments
+  {
+    uint32_t cE = 0, cK = 0, cS = 0, cH = 0; // carries: running end, last kept (j+1), emitted count, heads
+    uint32_t viol = 0, pan = 0;
+    for (uint32_t base = 0; base < NB; base += NT) {
+      const uint32_t j = base + t;
+      const bool valid = j < NB;
+      uint32_t r = 0, c = 0, k = 0, l = 0, mt = 0;
+      bool hd = false;
+      if (valid) {
+        r = srt(j);
+        c = m.bc[r];
+        k = m.bk[r];
+        l = m.bl[r];
+        mt = m.bm[r];
+        hd = j == 0 || m.bc[srt(j - 1)] != c;
+      }
+      const uint32_t e = k + l;
+      uint32_t pf, pv;
+      bscan_seg<NT, OpMax>(valid && hd, valid ? e : 0, ws, pf, pv);
+      const uint32_t E = hd ? 0 : (pf ? pv : (cE > pv ? cE : pv));
+      uint32_t flag = 0;
+      if (valid) {
+        if (l == 0) viol = 1; // zero-length GC: exact engine
+        if (hd || k >= E) {
+          flag = 1;
+          if (!hd && k > E) flag |= 2;
+        } else if (e > E) {
+          viol = 1; // partial overlap
+        }
+      }
+      // last kept position (j + 1) before j within the segment
+      uint32_t qf, qv;
+      bscan_seg<NT, OpMax>(valid && hd, (flag & 1) ? j + 1 : 0, ws, qf, qv);
+      const uint32_t last = hd ? 0 : (qf ? qv : (cK > qv ? cK : qv));
+      if (valid && !(flag & 1) && last) {
+        const uint32_t kr = srt(last - 1);
+        if (m.bk[kr] == k) { // same start: must be an exact duplicate (kind, length, bytes)
+          const uint32_t la = m.bm[kr] >> 8, lb = mt >> 8;
+          bool same = la == lb && (m.bm[kr] & 3) == (mt & 3) && m.bl[kr] == l;
+          if (same) same = equal_window(in + m.bp[kr], in + m.bp[r], la);
+          if (!same) viol = 1;
+        }
+      }
+      if (valid && (flag & 1) && (mt & 8)) pan = 1; // yrs panics encoding a kept String off a char boundary
+      // emitted blocks per client segment (kept + Skips) and the segment rank
+      const uint32_t cnt = (flag & 1) + ((flag >> 1) & 1);
+      uint32_t sf, sv2;
+      bscan_seg<NT, OpSum>(valid && hd, cnt, ws, sf, sv2);
+      const uint32_t run_before = hd ? 0 : (sf ? sv2 : cS + sv2);
+      uint32_t HT;
+      const uint32_t hpre = bscan_sum<NT>(valid && hd ? 1u : 0u, ws, HT);
+      const uint32_t rank = cH + hpre + (hd ? 1 : 0); // 1-based rank of j's segment
+      if (valid) {
+        m.fE[j] = E;
+        m.fF[j] = flag;
+        const bool tail = j + 1 == NB || m.bc[srt(j + 1)] != c;
+        if (tail) m.sseg[rank - 1] = run_before + cnt;
+      }
+      // carries for the next tile: values after the last element of this tile
+      const uint32_t lastj = (NB - base < (uint32_t)NT ? NB - base : (uint32_t)NT) - 1;
+      if (t == lastj) {
+        sc[0] = hd ? e : (E > e ? E : e);
+        sc[1] = (flag & 1) ? j + 1 : last;
+        sc[2] = run_before + cnt;
+      }
+      __syncthreads();
+      cE = sc[0];
+      cK = sc[1];
+      cS = sc[2];
+      cH += HT;
+      __syncthreads();
+    }
+    NC = cH;
+    const uint32_t vp = __syncthreads_or(viol | (pan << 1));
+    if (vp & 1) { // partial overlap / same-clock mismatch: exact engine
+      finish(1, 0, 0);
+      return;
+    }
+    if (vp & 2) {
+      finish(0, E_PANIC, 0);
+      return;
+    }
+  }
+
+  // ---- 4 sizes, offsets, write (LDS-staged per tile when the tile's bytes fit)
+  uint64_t blocks_size = varlen(NC);
+  bool ovf = false;
+  {
+    if (t == 0 && blocks_size <= cap) {
+      Writer w{out, 0};
+      w_var(w, NC);
+    }
+    uint32_t cH = 0;
+    for (uint32_t base = 0; base < NB; base += NT) {
+      const uint32_t j = base + t;
+      const bool valid = j < NB;
+      uint32_t r = 0, c = 0, k = 0, l = 0, mt = 0, p = 0, E = 0, flag = 0, s = 0, cnt = 0;
+      bool hd = false;
+      if (valid) {
+        r = srt(j);
+        c = m.bc[r];
+        k = m.bk[r];
+        l = m.bl[r];
+        mt = m.bm[r];
+        p = m.bp[r];
+        E = m.fE[j];
+        flag = m.fF[j];
+        hd = j == 0 || m.bc[srt(j - 1)] != c;
+      }
+      uint32_t HT;
+      const uint32_t hpre = bscan_sum<NT>(valid && hd ? 1u : 0u, ws, HT);
+      if (valid) {
+        if (hd) {
+          cnt = m.sseg[cH + hpre];
+          s += varlen(cnt) + varlen(c) + varlen(k);
+        }
+        if (flag & 2) s += 1 + varlen(k - E);
+        if (flag & 1) s += canon_size(in, nbytes, p, c, k, l, mt);
+      }
+      cH += HT;
+      uint64_t TT;
+      const uint64_t pre = bscan_sum64<NT>((uint64_t)s, S.ws64, TT);
+      const uint64_t o0 = blocks_size; // offset of this tile's first byte
+      blocks_size += TT;
+      if (blocks_size > cap) {
+        ovf = true;
+        break; // uniform
+      }
+      // stage the tile's bytes in LDS at the destination's 16-byte phase when they fit
+      const uint32_t phase = (uint32_t)((uintptr_t)(out + o0) & 15);
+      const bool staged = phase + TT <= BIG_UNION;
+      uint8_t *dst = staged ? S.un + phase : out + o0;
+      if (valid && s) {
+        Writer w{dst, pre};
+        if (hd) {
+          w_var(w, cnt);
+          w_var(w, c);
+          w_var(w, k);
+        }
+        if (flag & 2) {
+          w.u8(10);
+          w_var(w, k - E);
+        }
+        if (flag & 1) {
+          if ((mt & 4) && !(mt & 8)) {
+            Writer w2 = w;
+            emit_block(in, nbytes, p, c, k, l, 0, w2);
+          } else {
+            copy_window(w.p + w.n, in + p, mt >> 8);
+          }
+        }
+      }
+      if (staged) {
+        __syncthreads();
+        uint8_t *gbase = out + o0 - phase;
+        const uint32_t span = phase + (uint32_t)TT, nch = (span + 15) >> 4;
+        for (uint32_t q = t; q < nch; q += NT) {
+          const uint32_t b0 = q << 4, lo = b0 < phase ? phase : b0, hi = b0 + 16 < span ? b0 + 16 : span;
+          if (lo == b0 && hi == b0 + 16) *(uint4 *)(gbase + b0) = *(const uint4 *)(S.un + b0);
+          else
+            for (uint32_t z = lo; z < hi; z++) gbase[z] = S.un[z];
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (ovf) { // output larger than the slot: the exact engine writes it to the spill region
+    finish(1, 0, 0);
+    return;
+  }
+
+  // ---- 5 DeleteSet: distinct clients and first occurrence (LDS hash, 64-bit CAS insert,
+  //      atomicMin on a hit), sorted by client; yrs' table order (IdSet::merge inserts in
+  //      first-occurrence order, hashbrown layout); live ranges sorted by (client, start);
+  //      segmented union; write
+  uint64_t *dtab = (uint64_t *)S.un;                              // [BIG_DTAB]
+  uint32_t *d_client = (uint32_t *)(S.un + BIG_OFF_DARR);         // 7 x [BIG_DCAP]
+  uint32_t *d_first = d_client + BIG_DCAP, *d_ord = d_first + BIG_DCAP, *d_beg = d_ord + BIG_DCAP;
+  uint32_t *r_ncomp = d_beg + BIG_DCAP, *r_off = r_ncomp + BIG_DCAP, *r_end = r_off + BIG_DCAP;
+  uint8_t *lscr = S.un + BIG_OFF_SCR; // sort chunk / bitonic values / table slots
+  for (uint32_t j = t; j < BIG_DTAB; j += NT) dtab[j] = ~0ull;
+  __syncthreads();
+  uint32_t tovf = 0;
+  for (uint32_t j = t; j < NE && !tovf; j += NT) {
+    const uint32_t et = m.et[j];
+    if (!(et & 0x80000000u)) continue;
+    const uint32_t c = m.ec[j];
+    const uint64_t v = ((uint64_t)c << 32) | (et & 0x7FFFFFFFu);
+    const uint32_t h0 = mix32(c) & (BIG_DTAB - 1);
+    uint32_t h = h0;
+    for (;;) {
+      uint64_t cur = dtab[h];
+      if (cur == ~0ull) {
+        cur = atomicCAS((unsigned long long *)&dtab[h], ~0ull, (unsigned long long)v);
+        if (cur == ~0ull) break;
+      }
+      if ((uint32_t)(cur >> 32) == c) {
+        atomicMin((unsigned long long *)&dtab[h], (unsigned long long)v);
+        break;
+      }
+      h = (h + 1) & (BIG_DTAB - 1);
+      if (h == h0) {
+        tovf = 1;
+        break;
+      }
+    }
+  }
+  if (__syncthreads_or(tovf)) {
+    finish(1, 0, 0);
+    return;
+  }
+  // sort the table (occupied slots first, by client); D distinct clients
+  {
+    uint32_t *tv = (uint32_t *)lscr; // values (unused by the order)
+    for (uint32_t j = t; j < BIG_DTAB; j += NT) tv[j] = j;
+    __syncthreads();
+    bitonic<NT>(dtab, tv, BIG_DTAB);
+  }
+  uint32_t D;
+  {
+    uint32_t c = 0;
+    for (uint32_t j = t; j < BIG_DTAB; j += NT) c += dtab[j] != ~0ull;
+    bscan_sum<NT>(c, ws, D);
+  }
+  if (D > BIG_DCAP) {
+    finish(1, 0, 0);
+    return;
+  }
+  for (uint32_t j = t; j < D; j += NT) {
+    d_client[j] = (uint32_t)(dtab[j] >> 32);
+    d_first[j] = (uint32_t)dtab[j];
+  }
+  __syncthreads();
+  // first-occurrence order of the ranks (dtab reused as keys: first << 32 | rank)
+  for (uint32_t j = t; j < BIG_DTAB; j += NT) dtab[j] = j < D ? ((uint64_t)d_first[j] << 32) | j : ~0ull;
+  {
+    uint32_t *tv = (uint32_t *)lscr;
+    for (uint32_t j = t; j < BIG_DTAB; j += NT) tv[j] = j;
+    __syncthreads();
+    bitonic<NT>(dtab, tv, BIG_DTAB);
+  }
+  // hashbrown emulation (single lane; D <= BIG_DCAP): slots hold rank + 1
+  if (t == 0) {
+    uint32_t *slot_arr = (uint32_t *)lscr; // 2 * BIG_DTAB u32
+    uint32_t *tmp = slot_arr + BIG_DTAB;
+    uint32_t buckets = 0, items = 0, growth = 0;
+    auto ctrl_empty = [&](uint32_t idx) -> bool {
+      if (idx < buckets) return slot_arr[idx] == 0;
+      if (buckets < 16) return idx < 16 ? true : slot_arr[idx - 16] == 0;
+      return slot_arr[idx - buckets] == 0;
+    };
+    auto find_slot = [&](uint32_t key) -> uint32_t {
+      uint32_t mask = buckets - 1, pos = key & mask, stride = 0;
+      for (;;) {
+        for (uint32_t j = 0; j < 16; j++) {
+          if (ctrl_empty(pos + j)) {
+            const uint32_t index = (pos + j) & mask;
+            if (slot_arr[index] != 0)
+              for (uint32_t k = 0; k < buckets; k++)
+                if (slot_arr[k] == 0) return k;
+            return index;
+          }
+        }
+        stride += 16;
+        pos = (pos + stride) & mask;
+      }
+    };
+    for (uint32_t i = 0; i < D; i++) {
+      if (growth == 0) {
+        const uint64_t full = buckets ? mask_to_cap(buckets - 1) : 0;
+        const uint64_t need = items + 1;
+        const uint32_t nb = (uint32_t)cap_to_buckets(need > full + 1 ? need : full + 1);
+        for (uint32_t q = 0; q < buckets; q++) tmp[q] = slot_arr[q];
+        const uint32_t ob = buckets;
+        buckets = nb;
+        for (uint32_t q = 0; q < buckets; q++) slot_arr[q] = 0;
+        for (uint32_t q = 0; q < ob; q++)
+          if (tmp[q]) slot_arr[find_slot(d_client[tmp[q] - 1])] = tmp[q];
+        growth = (uint32_t)mask_to_cap(buckets - 1) - items;
+      }
+      const uint32_t rk = (uint32_t)dtab[i]; // rank of the i-th first occurrence
+      slot_arr[find_slot(d_client[rk])] = rk + 1;
+      items++;
+      growth--;
+    }
+    uint32_t k = 0;
+    for (uint32_t q = 0; q < buckets; q++)
+      if (slot_arr[q]) d_ord[k++] = slot_arr[q] - 1;
+  }
+  __syncthreads();
+  // live ranges sorted by (client, start, index)
+  const uint64_t *dkey = m.k0;
+  const uint32_t *dval = m.v0;
+  {
+    uint32_t bad = 0;
+    for (uint32_t j = t; j < NR; j += NT) {
+      const bool live = m.et[m.ri[j]] & 0x80000000u;
+      m.k0[j] = live ? (((uint64_t)m.ec[m.ri[j]] << 32) | m.rs[j]) : ~0ull;
+      m.v0[j] = j;
+    }
+    __syncthreads();
+    for (uint32_t j = t; j + 1 < NR; j += NT)
+      if (m.k0[j] > m.k0[j + 1]) bad = 1;
+    if (__syncthreads_or(bad) && wg_sort<NT>(m.k0, m.v0, m.k1, m.v1, NR, lscr)) {
+      dkey = m.k1;
+      dval = m.v1;
+    }
+  }
+  uint64_t *dk = (uint64_t *)dkey; // the component starts are stashed in the keys' low halves
+  uint32_t NL;
+  {
+    uint32_t c = 0;
+    for (uint32_t j = t; j < NR; j += NT) c += dkey[j] != ~0ull;
+    bscan_sum<NT>(c, ws, NL);
+  }
+  // union pass 1: component heads (start after the running end of the client) and the
+  // inclusive running end; pass 2: component starts, sizes, offsets, head prefix counts
+  {
+    uint32_t cE = 0;
+    for (uint32_t base = 0; base < NL; base += NT) {
+      const uint32_t j = base + t;
+      const bool valid = j < NL;
+      bool ch = false;
+      uint32_t s0 = 0, e = 0;
+      if (valid) {
+        ch = j == 0 || (dkey[j] >> 32) != (dkey[j - 1] >> 32);
+        s0 = (uint32_t)dkey[j];
+        e = m.re[dval[j]];
+      }
+      uint32_t pf, pv;
+      bscan_seg<NT, OpMax>(valid && ch, e, ws, pf, pv);
+      const uint32_t before = ch ? 0 : (pf ? pv : (cE > pv ? cE : pv));
+      const uint32_t run = ch ? e : (before > e ? before : e);
+      if (valid) {
+        m.chead[j] = ch ? 3u : (s0 > before ? 1u : 0u);
+        m.cend[j] = run;
+      }
+      const uint32_t lastj = (NL - base < (uint32_t)NT ? NL - base : (uint32_t)NT) - 1;
+      if (t == lastj) sc[0] = run;
+      __syncthreads();
+      cE = sc[0];
+      __syncthreads();
+    }
+  }
+  uint32_t ds_comp_total = 0;
+  {
+    uint32_t cS = 0, cO = 0, cP = 0; // carries: component start, byte offset, component heads
+    for (uint32_t base = 0; base < NL; base += NT) {
+      const uint32_t j = base + t;
+      const bool valid = j < NL;
+      const bool hh = valid && (m.chead[j] & 1);
+      const uint32_t s0 = valid ? (uint32_t)dkey[j] : 0;
+      uint32_t pf, pv;
+      bscan_seg<NT, OpFirst>(hh, hh ? s0 : 0, ws, pf, pv);
+      // OpFirst keeps the value of the first flagged lane of a run: the exclusive prefix's
+      // component start is that of the last head before j
+      uint32_t cs = hh ? s0 : (pf ? pv : cS);
+      const bool tail = valid && (j + 1 == NL || (m.chead[j + 1] & 1));
+      const uint32_t sz = tail ? varlen(cs) + varlen(m.cend[j] - cs) : 0;
+      uint32_t TS, TP;
+      const uint32_t pre = bscan_sum<NT>(sz, ws, TS);
+      const uint32_t hp = bscan_sum<NT>(hh ? 1u : 0u, ws, TP);
+      if (valid) {
+        m.coff[j] = cO + pre;
+        m.cpre[j] = cP + hp;
+        if (tail) dk[j] = (dkey[j] & 0xFFFFFFFF00000000ull) | cs;
+      }
+      const uint32_t lastj = (NL - base < (uint32_t)NT ? NL - base : (uint32_t)NT) - 1;
+      if (t == lastj) sc[0] = cs;
+      __syncthreads();
+      cS = sc[0];
+      cO += TS;
+      cP += TP;
+      __syncthreads();
+    }
+    ds_comp_total = cO;
+    if (t == 0) {
+      m.coff[NL] = cO;
+      m.cpre[NL] = cP;
+    }
+  }
+  __syncthreads();
+  // per distinct client (rank r, ascending client): [a, b) of the sorted live ranges
+  for (uint32_t r = t; r < D; r += NT) {
+    const uint32_t c = d_client[r];
+    uint32_t lo = 0, hi = NL;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) / 2;
+      if ((uint32_t)(dkey[mid] >> 32) < c) lo = mid + 1;
+      else hi = mid;
+    }
+    const uint32_t a = lo;
+    hi = NL;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) / 2;
+      if ((uint32_t)(dkey[mid] >> 32) <= c) lo = mid + 1;
+      else hi = mid;
+    }
+    d_beg[r] = a;
+    r_end[r] = lo;
+    r_ncomp[r] = m.cpre[lo] - m.cpre[a];
+  }
+  __syncthreads();
+  if (t == 0) { // header offsets in iteration order (D is small)
+    uint32_t pos = varlen(D);
+    for (uint32_t i = 0; i < D; i++) {
+      const uint32_t r = d_ord[i];
+      const uint32_t bytes = m.coff[r_end[r]] - m.coff[d_beg[r]];
+      r_off[r] = pos;
+      pos += varlen(d_client[r]) + varlen(r_ncomp[r]) + bytes;
+    }
+    sc[2] = pos;
+  }
+  __syncthreads();
+  const uint32_t ds_size = sc[2];
+  (void)ds_comp_total;
+  const uint64_t total = blocks_size + ds_size;
+  if (total > cap) {
+    finish(1, 0, 0);
+    return;
+  }
+  uint8_t *dso = out + blocks_size;
+  if (t == 0) {
+    Writer w{dso, 0};
+    w_var(w, D);
+  }
+  for (uint32_t r = t; r < D; r += NT) {
+    Writer w{dso, r_off[r]};
+    w_var(w, d_client[r]);
+    w_var(w, r_ncomp[r]);
+  }
+  for (uint32_t j = t; j < NL; j += NT) {
+    const bool tail = j + 1 == NL || (m.chead[j + 1] & 1);
+    if (!tail) continue;
+    const uint32_t c = (uint32_t)(dkey[j] >> 32);
+    uint32_t lo = 0, hi = D;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) / 2;
+      if (d_client[mid] < c) lo = mid + 1;
+      else hi = mid;
+    }
+    const uint32_t r = lo;
+    Writer w{dso, r_off[r] + varlen(c) + varlen(r_ncomp[r]) + (m.coff[j] - m.coff[d_beg[r]])};
+    const uint32_t cs = (uint32_t)dkey[j];
+    w_var(w, cs);
+    w_var(w, m.cend[j] - cs);
+  }
+  finish(0, 0, total);
+}
+
+// ------------------------------------------------------------------ launchers
+void launch_big_count(const BatchIn &b, const FastOut &o, uint32_t *counts, uint64_t *need, uint32_t *n_big,
+                      hipStream_t s) {
+  if (!b.n_docs) return;
+  hipLaunchKernelGGL((k_big_count<256>), dim3(b.n_docs), dim3(256), 0, s, b, o.path, o.status, o.out_start,
+                     o.out_len, counts, need, n_big);
+}
+void launch_big_merge(const BatchIn &b, const uint32_t *counts, const uint64_t *scr_off, uint32_t *scratch,
+                      const FastOut &o, hipStream_t s) {
+  if (!b.n_docs) return;
+  hipLaunchKernelGGL((k_big_merge<BIG_NT>), dim3(b.n_docs), dim3(BIG_NT), 0, s, b, counts, scr_off, scratch, o);
+}
+
+} // namespace ym

@@ -182,9 +182,11 @@ __global__ void __launch_bounds__(NT, 3) k_fast_merge(BatchIn b, FastCaps caps, 
   const uint64_t slot = 2 * B0 + 64ull * d;
   const uint64_t cap = 2ull * nbytes + 64;
   const uint8_t *in = b.bytes + B0; // document bytes stay in HBM; lanes read them through WCur
-  auto handover = [&]() {
+  // path 1: exact engine (partial overlaps, comparator anomalies, ...); path 2: over the
+  // LDS capacities only -> the tiled HBM-scratch kernel (ymerge_big.hip)
+  auto handover = [&](uint8_t p = 1) {
     if (t == 0) {
-      o.path[d] = 1;
+      o.path[d] = p;
       o.status[d] = 0;
       o.out_len[d] = 0;
       o.out_start[d] = slot;
@@ -335,8 +337,8 @@ __global__ void __launch_bounds__(NT, 3) k_fast_merge(BatchIn b, FastCaps caps, 
   YM_STAMP(1);
   {
     const uint32_t ek = misc[0], fl = misc[1];
-    if (ek == 0xFFFFFFFFu && (fl & 14)) { // big DS table, capacity, huge block: exact engine
-      handover();
+    if (ek == 0xFFFFFFFFu && (fl & 14)) { // capacity: tiled kernel; big DS table, huge block: exact engine
+      handover((fl & 4) ? 2 : 1);
       return;
     }
     if (ek != 0xFFFFFFFFu || fl) {
@@ -741,7 +743,7 @@ __global__ void __launch_bounds__(NT, 3) k_fast_merge(BatchIn b, FastCaps caps, 
     }
   }
   if (__syncthreads_or(tovf)) {
-    handover();
+    handover(2);
     return;
   }
   // compact the occupied slots, then order them by client (rank sort: D is small)
@@ -755,7 +757,7 @@ __global__ void __launch_bounds__(NT, 3) k_fast_merge(BatchIn b, FastCaps caps, 
       if (dtab[j] != ~0ull && pre < DCAP) dkey[pre++] = dtab[j];
   }
   if (D > DCAP) {
-    handover();
+    handover(2);
     return;
   }
   __syncthreads();
@@ -837,12 +839,7 @@ __global__ void __launch_bounds__(NT, 3) k_fast_merge(BatchIn b, FastCaps caps, 
   }
   __syncthreads();
   if (!sc[1]) {
-    if (t == 0) {
-      o.path[d] = 1;
-      o.status[d] = 0;
-      o.out_len[d] = 0;
-      o.out_start[d] = slot;
-    }
+    handover(2);
     return;
   }
   YM_STAMP(8);

@@ -51,12 +51,12 @@ ymerge_batch_result *alloc_result(uint64_t n_docs, uint64_t out_bytes);
 struct ymerge_ctx {
   int device = 0;
   hipStream_t s = nullptr;
-  DevBuf in_bytes, in_upd_off, in_doc_upd, in_sv, in_sv_off;
+  DevBuf in_bytes, in_upd_off, in_doc_upd, in_sv, in_sv_off, sync_off, sync_end, sync_st;
   DevBuf status, path, out_start, out_len, pack_off, counts, need, scr_off, scratch, sizes, spill_off, scan_tmp;
-  DevBuf arena, packed, counter, stamps, plan_small, plan_big, rec, ovf;
+  DevBuf arena, packed, counter, stamps, plan_small, plan_big, rec, ovf, big_scratch;
   bool want_stamps = false;
   uint64_t *h_pinned = nullptr;
-  hipEvent_t ev[6];
+  hipEvent_t ev[8];
   ymerge_stats stats{};
   uint64_t stamps_docs = 0; // documents covered by `stamps` (last merge batch)
   ym::FastCaps caps{0, 0, 1024, 512, 512}; // b_cap must equal FAST_BCAP (ymerge_fast.hip) // (unused), (unused), blocks, DS entries, DS ranges
@@ -100,10 +100,11 @@ extern "C" void ymerge_ctx_destroy(ymerge_ctx *c) {
   if (!c) return;
   hipSetDevice(c->device);
   if (c->s) hipStreamSynchronize(c->s);
-  for (DevBuf *b : {&c->in_bytes, &c->in_upd_off, &c->in_doc_upd, &c->in_sv, &c->in_sv_off, &c->rec, &c->ovf, &c->status, &c->path,
+  for (DevBuf *b : {&c->in_bytes, &c->in_upd_off, &c->in_doc_upd, &c->in_sv, &c->in_sv_off, &c->sync_off,
+                    &c->sync_end, &c->sync_st, &c->rec, &c->ovf, &c->status, &c->path,
                     &c->out_start, &c->out_len, &c->pack_off, &c->counts, &c->need, &c->scr_off, &c->scratch,
                     &c->sizes, &c->spill_off, &c->scan_tmp, &c->arena, &c->packed, &c->counter, &c->stamps,
-                    &c->plan_small, &c->plan_big})
+                    &c->plan_small, &c->plan_big, &c->big_scratch})
     b->release();
   if (c->h_pinned) hipHostFree(c->h_pinned);
   for (auto &e : c->ev)
@@ -168,13 +169,31 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     hipEventRecord(c->ev[5], c->s);
     ym::launch_fast_merge(b, c->caps, fo, c->fast_threads, c->s);
     if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
+    hipEventRecord(c->ev[6], c->s);
   }
   else {
     hipEventRecord(c->ev[5], c->s);
+    hipEventRecord(c->ev[6], c->s);
     hipMemsetAsync(path, 1, n, c->s);
   }
+  // documents over the LDS capacities (path == 2): count, scratch offsets, tiled kernel
+  uint32_t n_big = 0;
+  if (c->fast_threads) {
+    ym::launch_big_count(b, fo, c->counts.as<uint32_t>(), c->need.as<uint64_t>(), c->counter.as<uint32_t>() + 2, c->s);
+    ym::launch_scan_u64(c->need.as<uint64_t>(), c->scr_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
+    hipMemcpyAsync(c->h_pinned + 10, c->scr_off.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, c->s);
+    hipMemcpyAsync(c->h_pinned + 11, c->counter.as<uint32_t>() + 2, 4, hipMemcpyDeviceToHost, c->s);
+    if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
+    n_big = (uint32_t)(c->h_pinned[11] & 0xFFFFFFFFu);
+    if (n_big) {
+      if (!c->big_scratch.ensure((size_t)c->h_pinned[10] * 4 + 64)) return YMERGE_ERR_DEVICE;
+      ym::launch_big_merge(b, c->counts.as<uint32_t>(), c->scr_off.as<uint64_t>(), c->big_scratch.as<uint32_t>(), fo,
+                           c->s);
+      if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
+    }
+  }
   hipEventRecord(c->ev[1], c->s);
-  // exact engine for documents the fast path handed over (path == 1)
+  // exact engine for documents the fast or tiled path handed over (path == 1)
   ym::launch_seq_count(b, path, status, c->counts.as<uint32_t>(), c->need.as<uint64_t>(), c->counter.as<uint32_t>(),
                        c->s);
   ym::launch_scan_u64(c->need.as<uint64_t>(), c->scr_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
@@ -205,9 +224,10 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   uint64_t total = 0;
   if (!read_words(c, c->pack_off.as<uint64_t>() + n, 8, &total)) return YMERGE_ERR_DEVICE;
   if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
-  float t01 = 0, t12 = 0, t23 = 0, t03 = 0, t05 = 0;
+  float t01 = 0, t12 = 0, t23 = 0, t03 = 0, t05 = 0, t61 = 0;
   hipEventElapsedTime(&t05, c->ev[0], c->ev[5]);
-  hipEventElapsedTime(&t01, c->ev[5], c->ev[1]);
+  hipEventElapsedTime(&t01, c->ev[5], c->ev[6]);
+  hipEventElapsedTime(&t61, c->ev[6], c->ev[1]);
   hipEventElapsedTime(&t12, c->ev[1], c->ev[2]);
   hipEventElapsedTime(&t23, c->ev[2], c->ev[3]);
   hipEventElapsedTime(&t03, c->ev[0], c->ev[3]);
@@ -216,7 +236,9 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   c->stats.bytes_in = n_bytes;
   c->stats.bytes_out = total;
   c->stats.docs_exact = n_exact;
-  c->stats.docs_fast = n_docs - n_exact;
+  c->stats.docs_big = n_big;
+  c->stats.docs_fast = n_docs - n_exact - n_big;
+  c->stats.ms_big = t61;
   c->stats.ms_fast = t01;
   c->stats.ms_exact = t12;
   c->stats.ms_tail = t23;
@@ -242,18 +264,31 @@ extern "C" int ymerge_updates_v1_batch_device(ymerge_ctx *c, const uint8_t *d_by
 // diff_updates_v1 / encode_state_vector_from_update_v1 over a batch (one update per document):
 // plan (small scratch) -> re-plan the overflowing documents with length-sized scratch ->
 // output offsets (scan) -> execute.
+// frame: 0 plain, 1 y-sync SyncStep2 reply (diff; d_sv = client messages, parsed here),
+// 2 y-sync SyncStep1 message (state vector)
 static int plan_exec(ymerge_ctx *c, bool diff, const uint8_t *d_bytes, const uint64_t *d_upd_off,
-                     const uint8_t *d_sv, const uint64_t *d_sv_off, uint64_t n_docs, ymerge_device_result *res) {
+                     const uint8_t *d_sv, const uint64_t *d_sv_off, uint64_t n_docs, ymerge_device_result *res,
+                     uint32_t frame = 0) {
   if (hipSetDevice(c->device) != hipSuccess) return YMERGE_ERR_DEVICE;
   if (n_docs > 0xFFFFFFFFull) return YMERGE_ERR_OTHER;
   const uint32_t n = (uint32_t)n_docs;
+  ym::DiffBatch b{d_bytes, d_upd_off, d_sv, d_sv_off, n};
+  b.frame = frame;
+  if (frame == 1) {
+    if (!c->sync_off.ensure((n + 1) * 8) || !c->sync_end.ensure((n + 1) * 8) || !c->sync_st.ensure(n + 1))
+      return YMERGE_ERR_DEVICE;
+    ym::launch_sync_parse(d_sv, d_sv_off, n, c->sync_off.as<uint64_t>(), c->sync_end.as<uint64_t>(),
+                          c->sync_st.as<uint8_t>(), c->s);
+    b.sv_off = c->sync_off.as<uint64_t>();
+    b.sv_end = c->sync_end.as<uint64_t>();
+    b.pre_status = c->sync_st.as<uint8_t>();
+  }
   const size_t nn = (size_t)n + 1;
   const uint64_t sw = ym::plan_small_words();
   if (!c->status.ensure(nn) || !c->path.ensure(nn) || !c->out_len.ensure(nn * 8) || !c->pack_off.ensure(nn * 8) ||
       !c->need.ensure(nn * 8) || !c->spill_off.ensure(nn * 8) || !c->scan_tmp.ensure(ym::scan_tmp_elems(n) * 8 + 64) ||
       !c->counter.ensure(64) || !c->plan_small.ensure(nn * sw * 4))
     return YMERGE_ERR_DEVICE;
-  ym::DiffBatch b{d_bytes, d_upd_off, d_sv, d_sv_off, n};
   ym::PlanScratch ps{c->plan_small.as<uint32_t>(), sw,       nullptr,
                      c->spill_off.as<uint64_t>(), c->path.as<uint8_t>(), c->status.as<uint8_t>(),
                      c->out_len.as<uint64_t>(),    c->counter.as<uint32_t>()};
@@ -305,6 +340,20 @@ static int plan_exec(ymerge_ctx *c, bool diff, const uint8_t *d_bytes, const uin
   res->arena_bytes = c->arena.cap;
   res->out_bytes = total;
   return 0;
+}
+
+extern "C" int ysync_step1_v1_batch_device(ymerge_ctx *c, const uint8_t *d_bytes, const uint64_t *d_upd_off,
+                                           uint64_t n_docs, ymerge_device_result *res) {
+  if (!c || !res) return YMERGE_ERR_OTHER;
+  std::lock_guard<std::mutex> g(c->mu);
+  return plan_exec(c, false, d_bytes, d_upd_off, nullptr, nullptr, n_docs, res, 2);
+}
+extern "C" int ysync_step2_v1_batch_device(ymerge_ctx *c, const uint8_t *d_bytes, const uint64_t *d_upd_off,
+                                           const uint8_t *d_msg, const uint64_t *d_msg_off, uint64_t n_docs,
+                                           ymerge_device_result *res) {
+  if (!c || !res) return YMERGE_ERR_OTHER;
+  std::lock_guard<std::mutex> g(c->mu);
+  return plan_exec(c, true, d_bytes, d_upd_off, d_msg, d_msg_off, n_docs, res, 1);
 }
 
 extern "C" int yencode_state_vector_from_update_v1_batch_device(ymerge_ctx *c, const uint8_t *d_bytes,
@@ -492,7 +541,8 @@ extern "C" char *ymerge_updates_v1(const char *const *updates, const uint32_t *u
 
 // host buffers of one (or more) documents -> device -> plan/exec -> host
 static int host_plan_exec(ymerge_ctx *c, bool diff, const uint8_t *bytes, const uint64_t *upd_off,
-                          const uint8_t *sv, const uint64_t *sv_off, uint64_t n_docs, ymerge_batch_result **out) {
+                          const uint8_t *sv, const uint64_t *sv_off, uint64_t n_docs, ymerge_batch_result **out,
+                          uint32_t frame = 0) {
   std::lock_guard<std::mutex> g(c->mu);
   hipSetDevice(c->device);
   const uint64_t nbytes = upd_off[n_docs], nsv = diff ? sv_off[n_docs] : 0;
@@ -511,7 +561,7 @@ static int host_plan_exec(ymerge_ctx *c, bool diff, const uint8_t *bytes, const 
   ymerge_device_result dr{};
   int st = plan_exec(c, diff, c->in_bytes.as<uint8_t>(), c->in_upd_off.as<uint64_t>(),
                      diff ? c->in_sv.as<uint8_t>() : nullptr, diff ? c->in_sv_off.as<uint64_t>() : nullptr, n_docs,
-                     &dr);
+                     &dr, frame);
   if (st) return st;
   ymerge_batch_result *r = alloc_result(n_docs, dr.out_bytes);
   if (!r) return YMERGE_ERR_NOT_ENOUGH_MEMORY;
@@ -529,6 +579,16 @@ extern "C" int ydiff_updates_v1_batch(ymerge_ctx *c, const uint8_t *bytes, const
                                       ymerge_batch_result **res) {
   if (!c || !res) return YMERGE_ERR_OTHER;
   return host_plan_exec(c, true, bytes, upd_off, sv, sv_off, n_docs, res);
+}
+extern "C" int ysync_step1_v1_batch(ymerge_ctx *c, const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_docs,
+                                    ymerge_batch_result **res) {
+  if (!c || !res) return YMERGE_ERR_OTHER;
+  return host_plan_exec(c, false, bytes, upd_off, nullptr, nullptr, n_docs, res, 2);
+}
+extern "C" int ysync_step2_v1_batch(ymerge_ctx *c, const uint8_t *bytes, const uint64_t *upd_off, const uint8_t *msg,
+                                    const uint64_t *msg_off, uint64_t n_docs, ymerge_batch_result **res) {
+  if (!c || !res) return YMERGE_ERR_OTHER;
+  return host_plan_exec(c, true, bytes, upd_off, msg, msg_off, n_docs, res, 1);
 }
 extern "C" int yencode_state_vector_from_update_v1_batch(ymerge_ctx *c, const uint8_t *bytes,
                                                          const uint64_t *upd_off, uint64_t n_docs,

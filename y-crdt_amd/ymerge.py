@@ -35,7 +35,8 @@ class _Stats(ctypes.Structure):
     _fields_ = [("n_docs", ctypes.c_uint64), ("bytes_in", ctypes.c_uint64), ("bytes_out", ctypes.c_uint64),
                 ("docs_fast", ctypes.c_uint64), ("docs_exact", ctypes.c_uint64), ("docs_error", ctypes.c_uint64),
                 ("ms_total", ctypes.c_float), ("ms_fast", ctypes.c_float), ("ms_exact", ctypes.c_float),
-                ("ms_tail", ctypes.c_float), ("ms_decode", ctypes.c_float)]
+                ("ms_tail", ctypes.c_float), ("ms_decode", ctypes.c_float), ("ms_big", ctypes.c_float),
+                ("reserved", ctypes.c_uint32), ("docs_big", ctypes.c_uint64)]
 
 
 class _DevRes(ctypes.Structure):
@@ -64,6 +65,8 @@ def lib():
     L.ymerge_ctx_destroy.argtypes = [vp]
     L.ymerge_updates_v1_batch_device.argtypes = [vp, vp, u64, vp, u64, vp, u64, c.POINTER(_DevRes)]
     L.ydiff_updates_v1_batch_device.argtypes = [vp, vp, vp, vp, vp, u64, c.POINTER(_DevRes)]
+    L.ysync_step2_v1_batch_device.argtypes = [vp, vp, vp, vp, vp, u64, c.POINTER(_DevRes)]
+    L.ysync_step1_v1_batch_device.argtypes = [vp, vp, vp, u64, c.POINTER(_DevRes)]
     L.yencode_state_vector_from_update_v1_batch_device.argtypes = [vp, vp, vp, u64, c.POINTER(_DevRes)]
     L.ymerge_result_to_host.argtypes = [vp, c.POINTER(_DevRes), u64, vp, vp, vp]
     L.ymerge_last_stats.argtypes = [vp, c.POINTER(_Stats)]
@@ -173,6 +176,36 @@ class Engine:
         if rc:
             raise DeviceError(f"diff batch failed ({rc})")
         return DeviceResult(self, res, n_docs)
+
+    def sync_step2_device(self, d_bytes, d_upd_off, d_msg, d_msg_off, n_docs):
+        """y-sync SyncStep2 replies to SyncStep1 client messages (yrs/src/sync/protocol.rs:62-69)."""
+        res = _DevRes()
+        rc = lib().ysync_step2_v1_batch_device(self._ctx, d_bytes, d_upd_off, d_msg, d_msg_off, n_docs,
+                                               ctypes.byref(res))
+        if rc:
+            raise DeviceError(f"sync-step-2 batch failed ({rc})")
+        return DeviceResult(self, res, n_docs)
+
+    def sync_step1_device(self, d_bytes, d_upd_off, n_docs):
+        res = _DevRes()
+        rc = lib().ysync_step1_v1_batch_device(self._ctx, d_bytes, d_upd_off, n_docs, ctypes.byref(res))
+        if rc:
+            raise DeviceError(f"sync-step-1 batch failed ({rc})")
+        return DeviceResult(self, res, n_docs)
+
+    def sync_step2_host(self, ubytes, u_off, msg, msg_off):
+        n = len(u_off) - 1
+        ub = np.ascontiguousarray(ubytes, dtype=np.uint8)
+        mb = np.ascontiguousarray(msg, dtype=np.uint8)
+        args = [ub if len(ub) else np.zeros(1, np.uint8), np.asarray(u_off, np.uint64).view(np.int64),
+                mb if len(mb) else np.zeros(1, np.uint8), np.asarray(msg_off, np.uint64).view(np.int64)]
+        return self._host_batch(args, lambda a, b, c, d: self.sync_step2_device(a, b, c, d, n))
+
+    def sync_step1_host(self, ubytes, u_off):
+        n = len(u_off) - 1
+        ub = np.ascontiguousarray(ubytes, dtype=np.uint8)
+        args = [ub if len(ub) else np.zeros(1, np.uint8), np.asarray(u_off, np.uint64).view(np.int64)]
+        return self._host_batch(args, lambda a, b: self.sync_step1_device(a, b, n))
 
     def state_vector_device(self, d_bytes, d_upd_off, n_docs):
         res = _DevRes()
