@@ -163,7 +163,7 @@ def run_merge(a, rank, world, dev):
     import dist
     import ymerge
     batch, desc, scaling, cfg = build_merge(a, rank, world)
-    t_b = torch.from_numpy(batch.data if batch.n_bytes else np.zeros(1, np.uint8)).to(dev)
+    t_b = torch.from_numpy(ymerge.padded(batch.data)).to(dev)  # 16-byte reads past the end
     t_u = torch.from_numpy(batch.upd_off.view(np.int64)).to(dev)
     t_d = torch.from_numpy(batch.doc_upd.view(np.int64)).to(dev)
     torch.cuda.synchronize(dev)
@@ -196,7 +196,7 @@ def run_merge(a, rank, world, dev):
 
     e2e = None
     if not a.no_e2e:  # end-to-end: pinned host arena -> H2D -> pipeline -> pack -> D2H
-        h_b = torch.from_numpy(batch.data if batch.n_bytes else np.zeros(1, np.uint8)).pin_memory()
+        h_b = torch.from_numpy(ymerge.padded(batch.data)).pin_memory()
         h_u = torch.from_numpy(batch.upd_off.view(np.int64)).pin_memory()
         h_d = torch.from_numpy(batch.doc_upd.view(np.int64)).pin_memory()
         torch.cuda.synchronize(dev)
@@ -269,9 +269,9 @@ def run_diff(a, rank, world, dev):
     def sv_fn(dd, oo):
         return eng.state_vector_host(dd, oo)
     db = workloads.compacted_docs(data, offs, sv_fn=sv_fn)
-    t_b = torch.from_numpy(db.data).to(dev)
+    t_b = torch.from_numpy(ymerge.padded(db.data)).to(dev)
     t_u = torch.from_numpy(db.upd_off.view(np.int64)).to(dev)
-    t_s = torch.from_numpy(db.sv if len(db.sv) else np.zeros(1, np.uint8)).to(dev)
+    t_s = torch.from_numpy(ymerge.padded(db.sv)).to(dev)
     t_so = torch.from_numpy(db.sv_off.view(np.int64)).to(dev)
     torch.cuda.synchronize(dev)
 

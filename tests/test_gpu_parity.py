@@ -248,3 +248,27 @@ def test_large_block_sections(engine, oracle):
     check_batch(engine, oracle, batch_of(docs))
     st = engine.stats()
     assert st["docs_exact"] == 0
+
+
+def test_deleteset_union_shapes(engine, oracle):
+    """DeleteSet unions through both fast-path variants: the bitmap (non-empty ranges in
+    windows up to 32768 clocks) and the range sort (empty ranges [c, c), wide windows),
+    with touching / overlapping / nested / duplicate ranges and several clients."""
+    rng = np.random.default_rng(77)
+    docs = []
+    for case in range(60):
+        ups = []
+        span = [40, 300, 5000, 40000, 1 << 31][case % 5]
+        for _ in range(int(rng.integers(2, 60))):
+            ents = []
+            for c in rng.choice([3, 9, 27, 81, 1 << 30], size=int(rng.integers(1, 4)), replace=False):
+                rs = []
+                for _ in range(int(rng.integers(1, 4))):
+                    s = int(rng.integers(0, span))
+                    n = int(rng.integers(0 if case % 7 == 0 else 1, 40))
+                    rs.append((s, n))
+                ents.append((int(c), rs))
+            ups.append(_ds_update(ents))
+        ups.append(_root_text_update(5, 0, "x" * int(rng.integers(1, 30))))
+        docs.append([ups[i] for i in rng.permutation(len(ups))])
+    check_batch(engine, oracle, batch_of(docs))

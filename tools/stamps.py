@@ -29,8 +29,8 @@ def main():
     d = np.diff(st[ok][:, :12].astype(np.int64), axis=1)
     tot = d.sum(axis=1).mean()
     print(f"threads/WG {threads}: {ok.sum()} fast docs, mean {tot:.0f} cycles per doc")
-    print("  per doc: %.1f REC_SLOW records, %.1f REC_COMPLEX records" % (st[ok][:, 12].mean(), st[ok][:, 13].mean()))
-    print("  per doc: %.1f complex updates re-walked over HBM, %.1f overflow words gathered" % (st[ok][:, 14].mean(), st[ok][:, 15].mean()))
+    print("  per doc: %.1f updates walked over HBM (outside the stage), %.1f multi-record updates" % (st[ok][:, 12].mean(), st[ok][:, 13].mean()))
+    print("  per doc: %.1f multi-record updates re-walked over HBM" % st[ok][:, 14].mean())
     for i, nm in enumerate(NAMES):
         print(f"  {nm:10s} {d[:, i].mean():10.0f} cycles  {100 * d[:, i].mean() / tot:5.1f}%")
 

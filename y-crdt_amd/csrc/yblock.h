@@ -317,4 +317,23 @@ __device__ __forceinline__ uint32_t canon_size(const uint8_t *doc, uint32_t doc_
   return (uint32_t)cn.n;
 }
 
+// Cold paths out of line (they keep the merge kernels' register allocation small):
+// the exact walk of one update over HBM into a record / into its scanned positions.
+__device__ __noinline__ int walk_record_hbm(const uint8_t *p, uint32_t n, uint32_t *w) {
+  RegSink s;
+  s.nb = s.ne = s.nr = 0;
+  s.unsupported = s.big_ds = false;
+  s.ubase = 0;
+  WCur c;
+  wc_init(c, p, n);
+  const int e = smwalk_update(c, s);
+  rec_pack(s, e, w[0], w[1], w[2], w[3], w[4], w[5]);
+  return e;
+}
+__device__ __noinline__ void fill_hbm(const uint8_t *p, uint32_t n, FastFill *f) {
+  WCur c;
+  wc_init(c, p, n);
+  smwalk_update(c, *f);
+}
+
 } // namespace ym

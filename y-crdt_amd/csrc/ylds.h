@@ -120,9 +120,17 @@ template <class S> YM_INLINE int fast_walk(const uint32_t *w, uint32_t start, ui
           if (v == 1) {
             bi.len = 1;
           } else {
+            // any byte >= 0x80 in [s0, s0 + v)?  dword-wise: OR of the covering dwords,
+            // masked to the string's bytes in the first and last dword
             uint32_t hi = 0;
-            for (uint32_t q = 0; q < v; q++) hi |= lds_byte(w, s0 + q);
-            if (hi >= 0x80) return -1; // UTF-16 length of non-ASCII text: exact walk
+            const uint32_t e0 = s0 + v, q0 = s0 >> 2, q1 = (e0 - 1) >> 2;
+            for (uint32_t q = q0; q <= q1; q++) {
+              uint32_t x = w[q];
+              if (q == q0) x &= 0xFFFFFFFFu << (8 * (s0 & 3));
+              if (q == q1 && (e0 & 3)) x &= 0xFFFFFFFFu >> (8 * (4 - (e0 & 3)));
+              hi |= x;
+            }
+            if (hi & 0x80808080u) return -1; // UTF-16 length of non-ASCII text: exact walk
             bi.len = v;
           }
         } else {

@@ -288,14 +288,14 @@ __global__ void __launch_bounds__(NT) k_big_merge(BatchIn b, const uint32_t *cou
         w4 = x2.x;
         w5 = x2.y;
         if (w0 & REC_SLOW) {
-          RegSink s;
-          s.nb = s.ne = s.nr = 0;
-          s.unsupported = s.big_ds = false;
-          s.ubase = 0;
-          WCur c;
-          wc_init(c, in + ubase, ulen);
-          const int es = smwalk_update(c, s);
-          rec_pack(s, es, w0, w1, w2, w3, w4, w5);
+          uint32_t w[6];
+          walk_record_hbm(in + ubase, ulen, w);
+          w0 = w[0];
+          w1 = w[1];
+          w2 = w[2];
+          w3 = w[3];
+          w4 = w[4];
+          w5 = w[5];
         }
         shape = (w0 >> 10) & 3;
         if (shape == REC_BLOCK) snb = 1;
@@ -359,9 +359,7 @@ __global__ void __launch_bounds__(NT) k_big_merge(BatchIn b, const uint32_t *cou
         }
       } else if (shape == REC_COMPLEX) {
         FastFill f{m.bc, m.bk, m.bl, m.bp, m.bm, m.ec, m.et, m.rs, m.re, m.ri, i, ubase, pb, pe, pr, 0};
-        WCur c;
-        wc_init(c, in + ubase, ulen);
-        smwalk_update(c, f);
+        fill_hbm(in + ubase, ulen, &f);
       }
     }
   }

@@ -39,6 +39,7 @@ struct FastLayout {
   uint32_t misc, stage, total;
 };
 constexpr uint32_t FAST_BCAP = 1024;   // blocks per document on the fast path (caps.b_cap)
+constexpr uint32_t BMAP_WORDS = 1024;  // DeleteSet union bitmap (32768 clocks over all clients)
 constexpr uint32_t DCAP = 64;          // distinct DeleteSet clients per document on the fast path
 constexpr uint32_t DTAB_SLOTS = 256;   // LDS hash table for them
 constexpr uint32_t BTAB = 64; // client table of the counting sort (<= 8 distinct clients used)
@@ -102,7 +103,8 @@ __host__ __device__ inline FastLayout fast_layout(const FastCaps &c) {
 __global__ void __launch_bounds__(DEC_NT) k_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_upd,
                                                    uint32_t *rec, uint32_t *ovf) {
   __shared__ __align__(16) uint32_t stage[DEC_STAGE / 4 + 4];
-  __shared__ uint32_t ovf_top;
+  __shared__ uint32_t ovf_top, n_cx;
+  __shared__ uint32_t cx_lane[DEC_NT], cx_at[DEC_NT], cx_nb[DEC_NT], cx_ne[DEC_NT];
   const uint64_t g0 = (uint64_t)blockIdx.x * DEC_NT;
   const uint32_t t = threadIdx.x;
   const uint64_t i = g0 + t;
@@ -113,35 +115,53 @@ __global__ void __launch_bounds__(DEC_NT) k_decode(const uint8_t *bytes, const u
   if (nd > DEC_STAGE / 4) nd = DEC_STAGE / 4;
   const uint32_t *src = (const uint32_t *)(bytes + sbase);
   for (uint32_t k = t; k < nd; k += DEC_NT) stage[k] = src[k];
-  if (t == 0) ovf_top = 0;
-  __syncthreads();
-  if (i >= n_upd) return;
-  const uint64_t a0 = upd_off[i], a1 = upd_off[i + 1];
-  const uint32_t ulen = (uint32_t)(a1 - a0);
-  RegSink s;
-  s.nb = s.ne = s.nr = 0;
-  s.unsupported = s.big_ds = false;
-  s.ubase = 0;
-  const int e = a1 - sbase <= 4 * nd ? fast_walk(stage, (uint32_t)(a0 - sbase), ulen, s) : -1;
-  uint32_t w0 = REC_SLOW, w1 = 0, w2 = 0, w3 = 0, w4 = 0, w5 = 0;
-  if (e >= 0) rec_pack(s, e, w0, w1, w2, w3, w4, w5);
-  if (e == 0 && ((w0 >> 10) & 3) == REC_COMPLEX && !s.big_ds) {
-    // multi-record update: its records go to this workgroup's overflow words (LDS bump
-    // allocation); if they do not fit, k_fast_merge walks the update again
-    const uint32_t need = 5 * s.nb + s.ne + 3 * s.nr;
-    const uint32_t off = need <= DEC_OVF ? atomicAdd(&ovf_top, need) : DEC_OVF;
-    if (off + need <= DEC_OVF) {
-      const uint32_t at = blockIdx.x * DEC_OVF + off;
-      OvfFill f{ovf + at, s.nb, s.ne, 0, 0, 0};
-      fast_walk(stage, (uint32_t)(a0 - sbase), ulen, f);
-      w0 |= REC_OVF;
-      w4 = at;
-    }
+  if (t == 0) {
+    ovf_top = 0;
+    n_cx = 0;
   }
-  uint2 *o = (uint2 *)(rec + i * REC_WORDS);
-  o[0] = make_uint2(w0, w1);
-  o[1] = make_uint2(w2, w3);
-  o[2] = make_uint2(w4, w5);
+  __syncthreads();
+  if (i < n_upd) {
+    const uint64_t a0 = upd_off[i], a1 = upd_off[i + 1];
+    const uint32_t ulen = (uint32_t)(a1 - a0);
+    RegSink s;
+    s.nb = s.ne = s.nr = 0;
+    s.unsupported = s.big_ds = false;
+    s.ubase = 0;
+    const int e = a1 - sbase <= 4 * nd ? fast_walk(stage, (uint32_t)(a0 - sbase), ulen, s) : -1;
+    uint32_t w0 = REC_SLOW, w1 = 0, w2 = 0, w3 = 0, w4 = 0, w5 = 0;
+    if (e >= 0) rec_pack(s, e, w0, w1, w2, w3, w4, w5);
+    if (e == 0 && ((w0 >> 10) & 3) == REC_COMPLEX && !s.big_ds) {
+      // multi-record update: its records go to this workgroup's overflow words (LDS bump
+      // allocation), written by the second walk below; if they do not fit, k_fast_merge
+      // walks the update again
+      const uint32_t need = 5 * s.nb + s.ne + 3 * s.nr;
+      const uint32_t off = need <= DEC_OVF ? atomicAdd(&ovf_top, need) : DEC_OVF;
+      if (off + need <= DEC_OVF) {
+        const uint32_t at = blockIdx.x * DEC_OVF + off;
+        w0 |= REC_OVF;
+        w4 = at;
+        const uint32_t q = atomicAdd(&n_cx, 1u);
+        cx_lane[q] = t;
+        cx_at[q] = at;
+        cx_nb[q] = s.nb;
+        cx_ne[q] = s.ne;
+      }
+    }
+    uint2 *o = (uint2 *)(rec + i * REC_WORDS);
+    o[0] = make_uint2(w0, w1);
+    o[1] = make_uint2(w2, w3);
+    o[2] = make_uint2(w4, w5);
+  }
+  __syncthreads();
+  // second walk of the multi-record updates, packed onto the first lanes: a wave runs it
+  // only when it holds one of them (a few percent of an editor's updates), instead of every
+  // wave whose lanes happen to include one
+  for (uint32_t q = t; q < n_cx; q += DEC_NT) {
+    const uint64_t j = g0 + cx_lane[q];
+    const uint64_t a0 = upd_off[j], a1 = upd_off[j + 1];
+    OvfFill f{ovf + cx_at[q], cx_nb[q], cx_ne[q], 0, 0, 0};
+    fast_walk(stage, (uint32_t)(a0 - sbase), (uint32_t)(a1 - a0), f);
+  }
 }
 
 void launch_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_updates, uint32_t *rec, uint32_t *ovf,
@@ -232,14 +252,14 @@ __global__ void __launch_bounds__(NT, 3) k_fast_merge(BatchIn b, FastCaps caps, 
       if (STAMPS && ((w0 >> 10) & 3) == REC_COMPLEX)
         atomicAdd((unsigned long long *)&o.stamps[(size_t)blockIdx.x * 16 + 13], 1ull);
       if (w0 & REC_SLOW) { // not a fast shape (or malformed): exact walk over HBM
-        RegSink s;
-        s.nb = s.ne = s.nr = 0;
-        s.unsupported = s.big_ds = false;
-        s.ubase = 0;
-        WCur c;
-        wc_init(c, in + ubase, ulen);
-        const int es = smwalk_update(c, s);
-        rec_pack(s, es, w0, w1, w2, w3, w4, w5);
+        uint32_t w[6];
+        walk_record_hbm(in + ubase, ulen, w);
+        w0 = w[0];
+        w1 = w[1];
+        w2 = w[2];
+        w3 = w[3];
+        w4 = w[4];
+        w5 = w[5];
       }
       w0f = w0;
       e = w0 & 0xFF;
@@ -326,9 +346,7 @@ __global__ void __launch_bounds__(NT, 3) k_fast_merge(BatchIn b, FastCaps caps, 
         // not a one-record shape: walk the update again over HBM at its scanned positions
         if (STAMPS) atomicAdd((unsigned long long *)&o.stamps[(size_t)blockIdx.x * 16 + 14], 1ull);
         FastFill f{bc, bk, bl, bp, bm, ec, et, rs, re, ri, i, ubase, pb, pe, pr, 0};
-        WCur c;
-        wc_init(c, in + ubase, ulen);
-        smwalk_update(c, f);
+        fill_hbm(in + ubase, ulen, &f);
       }
     }
   }
@@ -843,6 +861,188 @@ __global__ void __launch_bounds__(NT, 3) k_fast_merge(BatchIn b, FastCaps caps, 
     return;
   }
   YM_STAMP(8);
+  // 5c' DeleteSet union by bitmap.  When every live range is non-empty and the clients'
+  //     clock windows [min start, max end) fit BMAP_WORDS words, each range sets its bits
+  //     in its client's window and the union's components are the runs of set bits:
+  //     ranges join when they overlap or touch (IdRange::squash, id_set.rs:129-164), the
+  //     runs come out in start order, so no range sort is needed.  (An empty range [c, c)
+  //     is a component of its own in yrs when isolated: the sort path below keeps that.)
+  {
+    uint32_t *cmin = d_first;                      // first occurrences are no longer needed
+    uint32_t *cmax = misc + 128;                   // [DCAP] (misc words 128..191 are free here)
+    uint32_t *woff = (uint32_t *)(smem + L.dbeg);  // [D + 1] word offset of each client's window
+    uint32_t *bmp = (uint32_t *)(smem + L.dkey);   // [BMAP_WORDS]
+    uint32_t *cb = bmp + BMAP_WORDS;               // [BMAP_WORDS + 1] components before each word
+    uint32_t *cst = (uint32_t *)(smem + L.coff);   // [NR] component start
+    uint32_t *cen = (uint32_t *)(smem + L.chead);  // [NR] component end
+    uint32_t *cof = (uint32_t *)(smem + L.dtab);   // [NR + 1] component byte offsets
+    auto rank_of = [&](uint32_t c) -> uint32_t {
+      uint32_t lo = 0, hi = D;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (d_client[mid] < c) lo = mid + 1;
+        else hi = mid;
+      }
+      return lo;
+    };
+    for (uint32_t r = t; r < D; r += NT) {
+      cmin[r] = 0xFFFFFFFFu;
+      cmax[r] = 0;
+    }
+    __syncthreads();
+    uint32_t bad = 0;
+    for (uint32_t j = t; j < NR; j += NT) {
+      if (!(et[ri[j]] & 0x80000000u)) continue;
+      if (re[j] == rs[j]) {
+        bad = 1;
+        continue;
+      }
+      const uint32_t r = rank_of(ec[ri[j]]);
+      atomicMin(&cmin[r], rs[j]);
+      atomicMax(&cmax[r], re[j]);
+    }
+    bad = __syncthreads_or(bad);
+    if (!bad && t == 0) {
+      uint32_t w = 0;
+      for (uint32_t r = 0; r < D; r++) {
+        woff[r] = w;
+        if (cmax[r] > cmin[r]) {
+          const uint64_t span = ((uint64_t)cmax[r] - cmin[r] + 31) >> 5;
+          w = span > BMAP_WORDS ? BMAP_WORDS + 1 : w + (uint32_t)span;
+          if (w > BMAP_WORDS) w = BMAP_WORDS + 1;
+        }
+      }
+      woff[D] = w;
+      sc[3] = w;
+    }
+    __syncthreads();
+    const uint32_t W = bad ? BMAP_WORDS + 1 : sc[3];
+    if (W <= BMAP_WORDS) {
+      for (uint32_t k = t; k < W; k += NT) bmp[k] = 0;
+      __syncthreads();
+      for (uint32_t j = t; j < NR; j += NT) {
+        if (!(et[ri[j]] & 0x80000000u)) continue;
+        const uint32_t r = rank_of(ec[ri[j]]);
+        uint32_t a = rs[j] - cmin[r];
+        const uint32_t z = re[j] - cmin[r];
+        while (a < z) {
+          const uint32_t wi = a >> 5, bo = a & 31, nb = (z - a < 32 - bo) ? z - a : 32 - bo;
+          const uint32_t mask = (nb == 32 ? 0xFFFFFFFFu : ((1u << nb) - 1)) << bo;
+          atomicOr(&bmp[woff[r] + wi], mask);
+          a += nb;
+        }
+      }
+      __syncthreads();
+      YM_STAMP(9);
+      // runs: starts / ends per word, components before each word (block scan)
+      const uint32_t wpl = (W + NT - 1) / NT, k0 = t * wpl, k1 = k0 + wpl < W ? k0 + wpl : W;
+      uint32_t nst = 0;
+      for (uint32_t k = k0; k < k1; k++) {
+        const uint32_t r = [&]() {
+          uint32_t lo = 0, hi = D;
+          while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (woff[mid + 1] <= k) lo = mid + 1;
+            else hi = mid;
+          }
+          return lo;
+        }();
+        const uint32_t bits = bmp[k], prev = k > woff[r] ? bmp[k - 1] >> 31 : 0;
+        nst += __popc(bits & ~((bits << 1) | prev));
+      }
+      uint32_t NCD;
+      uint32_t pre = bscan_sum<NT>(nst, ws, NCD);
+      for (uint32_t k = k0; k < k1; k++) {
+        uint32_t lo = 0, hi = D;
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (woff[mid + 1] <= k) lo = mid + 1;
+          else hi = mid;
+        }
+        const uint32_t r = lo;
+        const uint32_t bits = bmp[k], prev = k > woff[r] ? bmp[k - 1] >> 31 : 0;
+        const uint32_t next = k + 1 < woff[r + 1] ? bmp[k + 1] & 1 : 0;
+        uint32_t st = bits & ~((bits << 1) | prev), en = bits & ~((bits >> 1) | (next << 31));
+        const uint32_t st0 = st, base = cmin[r] + 32 * (k - woff[r]);
+        cb[k] = pre;
+        while (st) {
+          const uint32_t q = __builtin_ctz(st);
+          cst[pre + __popc(st0 & ((1u << q) - 1))] = base + q;
+          st &= st - 1;
+        }
+        while (en) {
+          const uint32_t q = __builtin_ctz(en);
+          const uint32_t upto = q == 31 ? st0 : (st0 & ((2u << q) - 1));
+          cen[pre + __popc(upto) - 1] = base + q + 1;
+          en &= en - 1;
+        }
+        pre += __popc(st0);
+      }
+      if (t == 0) cb[W] = NCD;
+      __syncthreads();
+      // component byte sizes -> offsets
+      const uint32_t cpl = (NCD + NT - 1) / NT, c0 = t * cpl, c1 = c0 + cpl < NCD ? c0 + cpl : NCD;
+      uint32_t ls = 0;
+      for (uint32_t c = c0; c < c1; c++) ls += varlen(cst[c]) + varlen(cen[c] - cst[c]);
+      uint32_t TS;
+      uint32_t po = bscan_sum<NT>(ls, ws, TS);
+      for (uint32_t c = c0; c < c1; c++) {
+        cof[c] = po;
+        po += varlen(cst[c]) + varlen(cen[c] - cst[c]);
+      }
+      if (t == 0) cof[NCD] = TS;
+      __syncthreads();
+      YM_STAMP(10);
+      uint32_t *r_ncomp = (uint32_t *)(smem + L.dnc), *r_off = (uint32_t *)(smem + L.doff);
+      if (t == 0) { // client headers in yrs' iteration order (d_aux)
+        uint32_t pos = varlen(D);
+        for (uint32_t i = 0; i < D; i++) {
+          const uint32_t r = d_aux[i];
+          const uint32_t ca = cb[woff[r]], cz = cb[woff[r + 1]];
+          r_ncomp[r] = cz - ca;
+          r_off[r] = pos;
+          pos += varlen(d_client[r]) + varlen(cz - ca) + (cof[cz] - cof[ca]);
+        }
+        sc[2] = pos;
+      }
+      __syncthreads();
+      const uint64_t total = (uint64_t)blocks_size + sc[2];
+      if (total > cap) {
+        handover();
+        return;
+      }
+      uint8_t *dso = out + blocks_size;
+      if (t == 0) {
+        Writer w{dso, 0};
+        w_var(w, D);
+      }
+      for (uint32_t r = t; r < D; r += NT) {
+        Writer w{dso, r_off[r]};
+        w_var(w, d_client[r]);
+        w_var(w, r_ncomp[r]);
+      }
+      for (uint32_t c = t; c < NCD; c += NT) {
+        uint32_t lo = 0, hi = D; // client of component c: last r with cb[woff[r]] <= c
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (cb[woff[mid + 1]] <= c) lo = mid + 1;
+          else hi = mid;
+        }
+        const uint32_t r = lo;
+        Writer w{dso, r_off[r] + varlen(d_client[r]) + varlen(r_ncomp[r]) + (cof[c] - cof[cb[woff[r]]])};
+        w_var(w, cst[c]);
+        w_var(w, cen[c] - cst[c]);
+      }
+      if (t == 0) {
+        o.path[d] = 0;
+        o.status[d] = 0;
+        o.out_len[d] = total;
+        o.out_start[d] = slot;
+      }
+      YM_STAMP(11);
+      return;
+    }
+  }
   // 5c ranges of live entries sorted by (client, start, index): rank sort, every lane
   //    counts the smaller keys with LDS broadcast reads (no barrier stages)
   {

@@ -86,6 +86,12 @@ def lib():
     return L
 
 
+def padded(a):
+    """uint8 array + 16 zero bytes: the kernels read arenas in 16-byte words (include/ymerge.h)."""
+    a = np.ascontiguousarray(a, dtype=np.uint8)
+    return np.concatenate([a, np.zeros(16, np.uint8)])
+
+
 def _take(ptr, n):
     if not ptr:
         code = lib().ymerge_last_error()
@@ -223,7 +229,8 @@ class Engine:
     def _host_batch(self, args_dev, fn):
         import torch
         dev = torch.device("cuda", self.device)
-        ts = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in args_dev]
+        ts = [torch.from_numpy(padded(a) if a.dtype == np.uint8 else np.ascontiguousarray(a)).to(dev)
+              for a in args_dev]
         torch.cuda.synchronize(dev)
         r = fn(*[t.data_ptr() for t in ts])
         return r.to_host()
@@ -248,7 +255,7 @@ class Engine:
     def merge_host(self, data, upd_off, doc_upd):
         import torch
         dev = torch.device("cuda", self.device)
-        t_b = torch.from_numpy(np.ascontiguousarray(data, dtype=np.uint8)).to(dev)
+        t_b = torch.from_numpy(padded(data)).to(dev)
         t_u = torch.from_numpy(np.ascontiguousarray(upd_off, dtype=np.uint64).view(np.int64)).to(dev)
         t_d = torch.from_numpy(np.ascontiguousarray(doc_upd, dtype=np.uint64).view(np.int64)).to(dev)
         torch.cuda.synchronize(dev)
