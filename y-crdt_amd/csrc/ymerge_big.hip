@@ -84,7 +84,7 @@ __device__ inline BigMem big_carve(uint32_t *w, uint32_t NB, uint32_t NE, uint32
 template <int NT>
 __global__ void __launch_bounds__(NT) k_big_count(BatchIn b, uint8_t *path, uint8_t *status, uint64_t *out_start,
                                                   uint64_t *out_len, uint32_t *counts, uint64_t *need,
-                                                  uint32_t *n_big) {
+                                                  uint32_t *n_big, uint32_t *npath) {
   const uint32_t d = blockIdx.x;
   if (d >= b.n_docs) return;
   const uint32_t t = threadIdx.x;
@@ -157,6 +157,7 @@ __global__ void __launch_bounds__(NT) k_big_count(BatchIn b, uint8_t *path, uint
   if (s_flags || s_nb >= (1ull << 28) || s_ne >= (1ull << 28) || s_nr >= (1ull << 28) ||
       b.upd_off[u1] - B0 >= (1ull << 30)) {
     path[d] = 1;
+    atomicAdd(&npath[1], 1u);
     return;
   }
   counts[4 * d + 1] = (uint32_t)s_nb;
@@ -258,6 +259,7 @@ __global__ void __launch_bounds__(NT) k_big_merge(BatchIn b, const uint32_t *cou
   uint8_t *out = o.out + slot;
   auto finish = [&](uint8_t p, uint8_t st, uint64_t len) {
     if (t == 0) {
+      if (p == 1) atomicAdd(&o.npath[1], 1u);
       o.path[d] = p;
       o.status[d] = st;
       o.out_len[d] = len;
@@ -845,7 +847,7 @@ void launch_big_count(const BatchIn &b, const FastOut &o, uint32_t *counts, uint
                       hipStream_t s) {
   if (!b.n_docs) return;
   hipLaunchKernelGGL((k_big_count<256>), dim3(b.n_docs), dim3(256), 0, s, b, o.path, o.status, o.out_start,
-                     o.out_len, counts, need, n_big);
+                     o.out_len, counts, need, n_big, o.npath);
 }
 void launch_big_merge(const BatchIn &b, const uint32_t *counts, const uint64_t *scr_off, uint32_t *scratch,
                       const FastOut &o, hipStream_t s) {

@@ -39,7 +39,8 @@ struct FastLayout {
   uint32_t misc, stage, total;
 };
 constexpr uint32_t FAST_BCAP = 1024;   // blocks per document on the fast path (caps.b_cap)
-constexpr uint32_t BMAP_WORDS = 1024;  // DeleteSet union bitmap (32768 clocks over all clients)
+constexpr uint32_t BMAP_WORDS = 1024;
+constexpr uint32_t OVF_BATCH = 16;     // overflow words of a DeleteSet-only update loaded at once  // DeleteSet union bitmap (32768 clocks over all clients)
 constexpr uint32_t DCAP = 64;          // distinct DeleteSet clients per document on the fast path
 constexpr uint32_t DTAB_SLOTS = 256;   // LDS hash table for them
 constexpr uint32_t BTAB = 64; // client table of the counting sort (<= 8 distinct clients used)
@@ -206,6 +207,7 @@ __global__ void __launch_bounds__(NT, 3) k_fast_merge(BatchIn b, FastCaps caps, 
   // LDS capacities only -> the tiled HBM-scratch kernel (ymerge_big.hip)
   auto handover = [&](uint8_t p = 1) {
     if (t == 0) {
+      atomicAdd(&o.npath[p], 1u);
       o.path[d] = p;
       o.status[d] = 0;
       o.out_len[d] = 0;
@@ -323,25 +325,27 @@ __global__ void __launch_bounds__(NT, 3) k_fast_merge(BatchIn b, FastCaps caps, 
         if (STAMPS) atomicAdd((unsigned long long *)&o.stamps[(size_t)blockIdx.x * 16 + 15],
                               (unsigned long long)(5 * snb + sne + 3 * snr));
         const uint32_t *ov = b.ovf + w4;
-        for (uint32_t k = 0; k < snb; k++) {
-          bc[pb + k] = ov[5 * k];
-          bk[pb + k] = ov[5 * k + 1];
-          bl[pb + k] = ov[5 * k + 2];
-          bp[pb + k] = ubase + ov[5 * k + 3];
-          bm[pb + k] = ov[5 * k + 4];
-        }
-        ov += 5 * snb;
-        for (uint32_t k = 0; k < sne; k++) {
-          ec[pe + k] = ov[k];
-          et[pe + k] = 0x80000000u | (i << 8);
+        {
+          for (uint32_t k = 0; k < snb; k++) {
+            bc[pb + k] = ov[5 * k];
+            bk[pb + k] = ov[5 * k + 1];
+            bl[pb + k] = ov[5 * k + 2];
+            bp[pb + k] = ubase + ov[5 * k + 3];
+            bm[pb + k] = ov[5 * k + 4];
+          }
+          ov += 5 * snb;
+          for (uint32_t k = 0; k < sne; k++) {
+            ec[pe + k] = ov[k];
+            et[pe + k] = 0x80000000u | (i << 8);
+          }
+          ov += sne;
+          for (uint32_t k = 0; k < snr; k++) {
+            rs[pr + k] = ov[3 * k];
+            re[pr + k] = ov[3 * k + 1];
+            ri[pr + k] = pe + ov[3 * k + 2];
+          }
         }
         if (sne >= 2) ds_order_packed(ec + pe, sne, et + pe, i << 8);
-        ov += sne;
-        for (uint32_t k = 0; k < snr; k++) {
-          rs[pr + k] = ov[3 * k];
-          re[pr + k] = ov[3 * k + 1];
-          ri[pr + k] = pe + ov[3 * k + 2];
-        }
       } else if (shape == REC_COMPLEX && !(flags & 2)) {
         // not a one-record shape: walk the update again over HBM at its scanned positions
         if (STAMPS) atomicAdd((unsigned long long *)&o.stamps[(size_t)blockIdx.x * 16 + 14], 1ull);
@@ -703,7 +707,7 @@ __global__ void __launch_bounds__(NT, 3) k_fast_merge(BatchIn b, FastCaps caps, 
           Writer w2 = w; // only the out-of-line re-encode takes a Writer by reference
           emit_block(in, nbytes, rp[k], rc[k], rk[k], rl[k], 0, w2);
         } else {
-          copy_window(w.p + w.n, in + rp[k], rm[k] >> 8);
+          copy_bytes16(w.p + w.n, in + rp[k], rm[k] >> 8);
         }
       }
     }
@@ -1254,12 +1258,7 @@ __global__ void __launch_bounds__(NT, 3) k_fast_merge(BatchIn b, FastCaps caps, 
   const uint32_t ds_size = sc[2];
   const uint64_t total = (uint64_t)blocks_size + ds_size;
   if (total > cap) {
-    if (t == 0) {
-      o.path[d] = 1;
-      o.status[d] = 0;
-      o.out_len[d] = 0;
-      o.out_start[d] = slot;
-    }
+    handover();
     return;
   }
   uint8_t *dso = out + blocks_size;

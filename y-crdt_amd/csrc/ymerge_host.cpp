@@ -163,7 +163,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     stamps = c->stamps.as<uint64_t>();
     c->stamps_docs = n_docs;
   }
-  ym::FastOut fo{arena, ostart, olen, status, path, stamps};
+  ym::FastOut fo{arena, ostart, olen, status, path, stamps, c->counter.as<uint32_t>() + 4};
   if (c->fast_threads) {
     ym::launch_decode(d_bytes, d_upd_off, n_updates, c->rec.as<uint32_t>(), c->ovf.as<uint32_t>(), c->s);
     hipEventRecord(c->ev[5], c->s);
@@ -176,9 +176,19 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     hipEventRecord(c->ev[6], c->s);
     hipMemsetAsync(path, 1, n, c->s);
   }
+  // hand-over counts of the fast path (npath[1] exact engine, npath[2] tiled kernel): the
+  // later stages are skipped when no document needs them
+  uint32_t n_p1 = n, n_p2 = 0;
+  if (c->fast_threads) {
+    hipMemcpyAsync(c->h_pinned + 12, c->counter.as<uint32_t>() + 4, 16, hipMemcpyDeviceToHost, c->s);
+    if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
+    const uint32_t *np = (const uint32_t *)(c->h_pinned + 12);
+    n_p1 = np[1];
+    n_p2 = np[2];
+  }
   // documents over the LDS capacities (path == 2): count, scratch offsets, tiled kernel
   uint32_t n_big = 0;
-  if (c->fast_threads) {
+  if (c->fast_threads && n_p2) {
     ym::launch_big_count(b, fo, c->counts.as<uint32_t>(), c->need.as<uint64_t>(), c->counter.as<uint32_t>() + 2, c->s);
     ym::launch_scan_u64(c->need.as<uint64_t>(), c->scr_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
     hipMemcpyAsync(c->h_pinned + 10, c->scr_off.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, c->s);
@@ -194,14 +204,18 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   }
   hipEventRecord(c->ev[1], c->s);
   // exact engine for documents the fast or tiled path handed over (path == 1)
-  ym::launch_seq_count(b, path, status, c->counts.as<uint32_t>(), c->need.as<uint64_t>(), c->counter.as<uint32_t>(),
-                       c->s);
-  ym::launch_scan_u64(c->need.as<uint64_t>(), c->scr_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
-  hipMemcpyAsync(c->h_pinned + 8, c->scr_off.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, c->s);
-  hipMemcpyAsync(c->h_pinned + 9, c->counter.p, 4, hipMemcpyDeviceToHost, c->s);
-  if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
-  const uint64_t words = c->h_pinned[8];
-  const uint32_t n_exact = (uint32_t)(c->h_pinned[9] & 0xFFFFFFFFu);
+  uint64_t words = 0;
+  uint32_t n_exact = 0;
+  if (n_p1 || n_p2) {
+    ym::launch_seq_count(b, path, status, c->counts.as<uint32_t>(), c->need.as<uint64_t>(), c->counter.as<uint32_t>(),
+                         c->s);
+    ym::launch_scan_u64(c->need.as<uint64_t>(), c->scr_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
+    hipMemcpyAsync(c->h_pinned + 8, c->scr_off.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, c->s);
+    hipMemcpyAsync(c->h_pinned + 9, c->counter.p, 4, hipMemcpyDeviceToHost, c->s);
+    if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
+    words = c->h_pinned[8];
+    n_exact = (uint32_t)(c->h_pinned[9] & 0xFFFFFFFFu);
+  }
   if (n_exact) {
     if (!c->scratch.ensure((size_t)words * 4 + 64)) return YMERGE_ERR_DEVICE;
     ym::launch_seq_merge(false, b, path, status, c->counts.as<uint32_t>(), c->scr_off.as<uint64_t>(),

@@ -263,6 +263,19 @@ YM_INLINE void copy_window(uint8_t *dst, const uint8_t *src, uint32_t len) {
   wc_init(c, src, len);
   for (uint32_t q = 0; q < len; q++) dst[q] = (uint8_t)wc_byte(c, q);
 }
+// byte copy global -> (LDS stage or global) in groups of 16: the 16 byte loads of a group
+// are issued before any store (one memory latency per group), one instruction per byte
+// each way instead of the window's select tree per byte
+YM_INLINE void copy_bytes16(uint8_t *dst, const uint8_t *src, uint32_t len) {
+  for (uint32_t q0 = 0; q0 < len; q0 += 16) {
+    uint32_t x[16];
+#pragma unroll
+    for (uint32_t k = 0; k < 16; k++) x[k] = q0 + k < len ? src[q0 + k] : 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < 16; k++)
+      if (q0 + k < len) dst[q0 + k] = (uint8_t)x[k];
+  }
+}
 YM_INLINE bool equal_window(const uint8_t *a, const uint8_t *b, uint32_t len) {
   WCur x, y;
   wc_init(x, a, len);
