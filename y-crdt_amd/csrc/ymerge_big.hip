@@ -540,7 +540,7 @@ __global__ void __launch_bounds__(NT) k_big_merge(BatchIn b, const uint32_t *cou
             Writer w2 = w;
             emit_block(in, nbytes, p, c, k, l, 0, w2);
           } else {
-            copy_window(w.p + w.n, in + p, mt >> 8);
+            copy_bytes16(w.p + w.n, in + p, mt >> 8);
           }
         }
       }
