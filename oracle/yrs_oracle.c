@@ -20,8 +20,12 @@
  *    infallible with_capacity aborts (REFERENCE_PANIC) when it would need more
  *    than 2^36 bytes.
  *  - Item-vs-GC ties at one (client, clock) make yrs' comparator inconsistent
- *    (update.rs:580-582); we follow Rust's insertion sort (exact for <= 20 live
- *    decoders, unpinned above).
+ *    (update.rs:580-582).  With <= 20 live decoders Rust's stable sort_by IS
+ *    insertion_sort_shift_left in every std version, and we follow it literally
+ *    (pinned).  Above 20 the outcome depends on the std version's sort algorithm
+ *    (merge sort before Rust 1.81, driftsort after, which may even panic): unpinned,
+ *    and our policy is the stable sort under the consistent comparator that treats
+ *    the Item/GC tie as Equal (update.rs:580's same_type arm) — see merge_blocks.
  *  - Embed/Format JSON goes through the serde_json + ryu restatement below (JSON section);
  *    objects with >= 2 distinct keys are RandomState-ordered in yrs: written at each key's
  *    last occurrence (the same policy as Any maps above).
@@ -1842,6 +1846,12 @@ static bool dec_less(const dec_t *a, const dec_t *b) {
   if (l->clock == r->clock) return l->kind != r->kind; /* Equal if same type, else Less */
   return l->clock < r->clock;
 }
+/* the same with the Item-vs-GC tie read as Equal: a consistent order (policy above 20) */
+static bool key_less(const dec_t *a, const dec_t *b) {
+  const car_t *l = &a->cur, *r = &b->cur;
+  if (l->client != r->client) return l->client > r->client;
+  return l->clock < r->clock;
+}
 static bool heap_less(const dec_t *a, const dec_t *b) {
   const car_t *l = &a->cur, *r = &b->cur;
   if (l->client != r->client) return l->client > r->client;
@@ -1927,6 +1937,7 @@ static int cmpk(const void *a, const void *b) {
   return (int)x->kind - (int)y->kind;
 }
 
+#define SORT_SMALL 20 /* Rust's MAX_LEN_ALWAYS_INSERTION_SORT / MAX_INSERTION */
 static int merge_blocks(upd_t *ups, size_t n, int mode, emit_t *em) {
   dec_t *decs = calloc(n + 1, sizeof(dec_t));
   dec_t **arr = malloc((n + 1) * sizeof(dec_t *));
@@ -1936,8 +1947,17 @@ static int merge_blocks(upd_t *ups, size_t n, int mode, emit_t *em) {
     dec_init(&decs[i], &ups[i], i);
     arr[na++] = &decs[i];
   }
-  bool use_heap = false;
-  if (mode == 1) { /* heap is exact unless an Item/GC tie exists at one (client, clock) */
+  /* Sort policy per iteration (update.rs:570-590): more than SORT_SMALL live decoders ->
+   * stable sort under key_less; otherwise Rust's insertion_sort_shift_left with yrs'
+   * comparator.  Mode 1 runs the first regime as a binary heap keyed (client desc, clock
+   * asc, last re-insert desc, input index asc) — the order a stable sort of the deque
+   * keeps — and the second one as a heap too when no Item/GC tie exists (the comparator
+   * is then consistent and both regimes give the heap order).  With a tie it switches to
+   * the literal loop once <= SORT_SMALL decoders are live, rebuilding the deque as
+   * [decoder popped last] + the rest in heap order. */
+  bool use_heap = false, anomaly = false;
+  dec_t *last = NULL;
+  if (mode == 1) {
     size_t tot = 0;
     for (size_t i = 0; i < na; i++) tot += arr[i]->n + 1;
     tiekey_t *ks = malloc((tot + 1) * sizeof(tiekey_t));
@@ -1956,11 +1976,10 @@ static int merge_blocks(upd_t *ups, size_t n, int mode, emit_t *em) {
       }
     }
     qsort(ks, m, sizeof(tiekey_t), cmpk);
-    bool anomaly = false;
     for (size_t i = 1; i < m; i++)
       if (ks[i].c == ks[i - 1].c && ks[i].k == ks[i - 1].k && ks[i].kind != ks[i - 1].kind) anomaly = true;
     free(ks);
-    use_heap = !anomaly;
+    use_heap = !anomaly || na > SORT_SMALL;
   }
   dec_t **heap = NULL;
   size_t nh = 0;
@@ -1981,6 +2000,15 @@ static int merge_blocks(upd_t *ups, size_t n, int mode, emit_t *em) {
   const upd_t *cw_u = NULL;
   for (;; iter++) {
     dec_t *d;
+    if (use_heap && anomaly && nh <= SORT_SMALL) { /* hand over to the literal loop */
+      na = 0;
+      if (last && last->has) arr[na++] = last;
+      while (nh) {
+        dec_t *x = heap_pop(heap, &nh);
+        if (x != last) arr[na++] = x;
+      }
+      use_heap = false;
+    }
     if (use_heap) {
       if (nh == 0) break;
       d = heap_pop(heap, &nh);
@@ -1989,11 +2017,12 @@ static int merge_blocks(upd_t *ups, size_t n, int mode, emit_t *em) {
       for (size_t i = 0; i < na; i++)
         if (arr[i]->has) arr[k++] = arr[i];
       na = k;
-      /* stable insertion sort (Rust sort_by for len <= 20: insertion_sort_shift_left) */
+      /* Rust sort_by: insertion_sort_shift_left for len <= 20; above, the policy order */
+      bool small = na <= SORT_SMALL;
       for (size_t i = 1; i < na; i++) {
         dec_t *tmp = arr[i];
         size_t j = i;
-        while (j > 0 && dec_less(tmp, arr[j - 1])) {
+        while (j > 0 && (small ? dec_less(tmp, arr[j - 1]) : key_less(tmp, arr[j - 1]))) {
           arr[j] = arr[j - 1];
           j--;
         }
@@ -2002,6 +2031,7 @@ static int merge_blocks(upd_t *ups, size_t n, int mode, emit_t *em) {
       if (na == 0) break;
       d = arr[0];
     }
+    last = d;
     uint64_t first_client = d->cur.client;
     if (has_cw) {
       bool iterated = false;

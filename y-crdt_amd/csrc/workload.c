@@ -84,9 +84,10 @@ static void runs_split(doc_t *d, size_t i, uint32_t o) {
   runs_insert_at(d, i + 1, b);
 }
 
-/* Yjs-style insert of `k` chars (one String item) by client index `ci` at visible pos p */
-static void doc_insert(doc_t *d, bytes_t *out, uint32_t ci, uint64_t p, const uint8_t *text, uint32_t k,
-                       const char *root) {
+/* Yjs-style insert of one String item by client index `ci` at visible pos p: `nb` UTF-8 bytes
+ * of text that are `k` UTF-16 units long (the item's clock length, block.rs ItemContent::len) */
+static void doc_insert_u(doc_t *d, bytes_t *out, uint32_t ci, uint64_t p, const uint8_t *text, uint32_t k,
+                         uint32_t nb, const char *root) {
   int has_o = 0, has_r = 0;
   uint32_t oc = 0, ok = 0, rc = 0, rk = 0;
   size_t at = 0;
@@ -135,9 +136,13 @@ static void doc_insert(doc_t *d, bytes_t *out, uint32_t ci, uint64_t p, const ui
     putv(out, rl);
     putbytes(out, (const uint8_t *)root, rl);
   }
-  putv(out, k);
-  putbytes(out, text, k);
+  putv(out, nb);
+  putbytes(out, text, nb);
   putv(out, 0); /* empty DeleteSet */
+}
+static void doc_insert(doc_t *d, bytes_t *out, uint32_t ci, uint64_t p, const uint8_t *text, uint32_t k,
+                       const char *root) {
+  doc_insert_u(d, out, ci, p, text, k, k, root);
 }
 
 typedef struct {
@@ -583,11 +588,13 @@ int yw_generate_ids(int kind, uint64_t seed, size_t n_docs, const uint64_t *ids,
   return 0;
 }
 
-/* C1: replay an editing trace (ops = pos, del, ins_len, then ins bytes) as one doc,
- * client id `client`, one update per transaction (insert+delete in one txn give a
- * block update followed by... yrs/Yjs put both in one update: blocks then DS). */
-int yw_replay(const uint32_t *pos, const uint32_t *del, const uint32_t *ins_len, const uint8_t *ins_bytes,
-              size_t n_txn, uint32_t client, uint8_t **bytes, uint64_t *n_bytes, uint64_t **upd_off) {
+/* C1: replay an editing trace (ops = pos, del, ins_len bytes, ins_units UTF-16 units (NULL:
+ * ASCII, = ins_len), then ins bytes) as one doc, client id `client`, one update per patch
+ * (a patch that deletes and inserts gives one update: its block, then its DeleteSet).
+ * Positions and delete counts are UTF-16 units. */
+int yw_replay(const uint32_t *pos, const uint32_t *del, const uint32_t *ins_len, const uint32_t *ins_units,
+              const uint8_t *ins_bytes, size_t n_txn, uint32_t client, uint8_t **bytes, uint64_t *n_bytes,
+              uint64_t **upd_off) {
   doc_t d;
   memset(&d, 0, sizeof(d));
   d.n_clients = 1;
@@ -605,14 +612,14 @@ int yw_replay(const uint32_t *pos, const uint32_t *del, const uint32_t *ins_len,
       tmp.n = 0;
       doc_delete(&d, &tmp, pos[t], del[t], &scratch, &scap);
       bytes_t blk = {0};
-      doc_insert(&d, &blk, 0, pos[t], ins_bytes + ib, ins_len[t], "text");
+      doc_insert_u(&d, &blk, 0, pos[t], ins_bytes + ib, ins_units ? ins_units[t] : ins_len[t], ins_len[t], "text");
       putbytes(&out, blk.d, blk.n - 1); /* drop the empty DS byte */
       putbytes(&out, tmp.d + 1, tmp.n - 1); /* drop the "0 clients" byte */
       free(blk.d);
     } else if (del[t]) {
       doc_delete(&d, &out, pos[t], del[t], &scratch, &scap);
     } else {
-      doc_insert(&d, &out, 0, pos[t], ins_bytes + ib, ins_len[t], "text");
+      doc_insert_u(&d, &out, 0, pos[t], ins_bytes + ib, ins_units ? ins_units[t] : ins_len[t], ins_len[t], "text");
     }
     ib += ins_len[t];
   }

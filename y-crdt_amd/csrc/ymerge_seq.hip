@@ -284,13 +284,15 @@ __device__ __forceinline__ bool heap_less(const SeqCtx &x, uint32_t a, uint32_t 
   if (ta != tb) return ta > tb;
   return a < b;
 }
-// yrs comparator (update.rs:572-589) as is_less
-__device__ __forceinline__ bool dec_less(const SeqCtx &x, uint32_t a, uint32_t b) {
+// yrs comparator (update.rs:572-589) as is_less; `small` = Rust's insertion-sort regime
+// (<= SORT_SMALL live decoders).  Above it the Item/GC tie reads as Equal.
+constexpr uint32_t SORT_SMALL = 20;
+__device__ __forceinline__ bool dec_less(const SeqCtx &x, uint32_t a, uint32_t b, bool small) {
   uint32_t pa = x.m.dec_pos[a], pb = x.m.dec_pos[b];
   uint32_t ca = x.m.b_client[pa], cb = x.m.b_client[pb];
   if (ca != cb) return ca > cb;
   uint32_t ka = x.m.b_clock[pa], kb = x.m.b_clock[pb];
-  if (ka == kb) return x.m.b_kind[pa] != x.m.b_kind[pb];
+  if (ka == kb) return small && x.m.b_kind[pa] != x.m.b_kind[pb];
   return ka < kb;
 }
 __device__ void heap_push(SeqCtx &x, uint32_t &nh, uint32_t d) {
@@ -326,26 +328,34 @@ __device__ uint32_t heap_pop(SeqCtx &x, uint32_t &nh) {
 
 __device__ int seq_merge_blocks(SeqCtx &x) {
   SeqMem &m = x.m;
-  // literal mode iff an Item and a GC share one (client, clock)
+  // Sort policy (oracle merge_blocks): a heap in the regime the comparator is consistent
+  // (> SORT_SMALL live decoders, or no Item/GC tie at one (client, clock) anywhere); the
+  // literal insertion-sort loop once <= SORT_SMALL are live and such a tie exists.
   for (uint32_t i = 0; i < x.NB; i++) {
     m.k64[i] = ((uint64_t)m.b_client[i] << 32) | m.b_clock[i];
     m.v32[i] = m.b_kind[i];
   }
   seq_sort64(m.k64, m.v32, m.t64, m.tv32, x.NB);
-  bool literal = false;
+  bool anomaly = false;
   for (uint32_t i = 1; i < x.NB; i++)
-    if (m.k64[i] == m.k64[i - 1] && m.v32[i] != m.v32[i - 1]) literal = true;
+    if (m.k64[i] == m.k64[i - 1] && m.v32[i] != m.v32[i - 1]) anomaly = true;
 
   uint32_t na = 0, nh = 0;
   for (uint32_t u = 0; u < x.U; u++) {
     m.dec_pos[u] = m.upd_beg[u];
     m.dec_t[u] = -1;
+    if (has_cur(x, u)) na++;
+  }
+  bool literal = anomaly && na <= SORT_SMALL;
+  na = 0;
+  for (uint32_t u = 0; u < x.U; u++) {
     if (!has_cur(x, u)) continue;
     if (literal)
       m.heap[na++] = u; // heap[] doubles as the decoder array
     else
       heap_push(x, nh, u);
   }
+  uint32_t last = ~0u;
   x.nem = 0;
   auto emit = [&](const Car &c) {
     uint32_t k = x.nem++;
@@ -360,14 +370,26 @@ __device__ int seq_merge_blocks(SeqCtx &x) {
   bool has_cw = false;
   for (int32_t iter = 0;; iter++) {
     uint32_t d;
+    if (!literal && anomaly && nh <= SORT_SMALL) { // deque = [popped last] + heap order
+      uint32_t tmp[SORT_SMALL], nt = 0;
+      while (nh) {
+        uint32_t e = heap_pop(x, nh);
+        if (e != last) tmp[nt++] = e;
+      }
+      na = 0;
+      if (last != ~0u && has_cur(x, last)) m.heap[na++] = last;
+      for (uint32_t i = 0; i < nt; i++) m.heap[na++] = tmp[i];
+      literal = true;
+    }
     if (literal) {
       uint32_t k = 0;
       for (uint32_t i = 0; i < na; i++)
         if (has_cur(x, m.heap[i])) m.heap[k++] = m.heap[i];
       na = k;
+      bool small = na <= SORT_SMALL;
       for (uint32_t i = 1; i < na; i++) { // insertion_sort_shift_left
         uint32_t tmp = m.heap[i], j = i;
-        while (j > 0 && dec_less(x, tmp, m.heap[j - 1])) {
+        while (j > 0 && dec_less(x, tmp, m.heap[j - 1], small)) {
           m.heap[j] = m.heap[j - 1];
           j--;
         }
@@ -379,6 +401,7 @@ __device__ int seq_merge_blocks(SeqCtx &x) {
       if (nh == 0) break;
       d = heap_pop(x, nh);
     }
+    last = d;
     Car b;
     cur_of(x, d, b);
     uint32_t first_client = b.client;

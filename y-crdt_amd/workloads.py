@@ -27,7 +27,8 @@ def _L():
         L.yw_generate.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_uint32,
                                   ctypes.c_uint32, ctypes.c_double, ctypes.c_int, P(ctypes.c_void_p),
                                   P(ctypes.c_uint64), P(ctypes.c_void_p), P(ctypes.c_uint64), P(ctypes.c_void_p)]
-        L.yw_replay.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+        L.yw_replay.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                ctypes.c_size_t,
                                 ctypes.c_uint32, P(ctypes.c_void_p), P(ctypes.c_uint64), P(ctypes.c_void_p)]
         L.yw_generate_ids.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_double, ctypes.c_int,
@@ -148,27 +149,43 @@ def delete_heavy_docs(n_docs, ops_per_doc=5000, seed=0xDE1E7E, threads=None):
     return Batch(*_generate(4, seed, n_ops, 1, 4, 0.7, threads), name="C4")
 
 
+TRACES = ("automerge-paper", "friendsforever_flat", "rustcode", "seph-blog1", "sveltecomponent")
+
+
+def trace_path(name):
+    return os.path.join(os.path.dirname(_HERE), "tests", "golden", name + ".json.gz")
+
+
 def trace_updates(path=None, client=1):
-    """C1: one update per transaction of an editing trace (default automerge-paper)."""
+    """C1: one update per patch of an editing trace (default automerge-paper).
+
+    Trace positions/lengths count Unicode scalar values; every trace here is BMP-only
+    (checked below), so they equal the UTF-16 units yrs counts clocks in."""
     if path is None:
-        path = os.path.join(os.path.dirname(_HERE), "tests", "golden", "automerge-paper.json.gz")
+        path = trace_path("automerge-paper")
+    elif not os.path.sep in path:
+        path = trace_path(path)
     with gzip.open(path) as f:
         d = json.load(f)
-    pos, dele, ilen, ins = [], [], [], []
+    pos, dele, ilen, iun, ins = [], [], [], [], []
     for t in d["txns"]:
         for p in t["patches"]:
+            if any(ord(c) > 0xFFFF for c in p[2]):
+                raise ValueError("astral-plane text: trace positions would need UTF-16 remapping")
             s = p[2].encode("utf-8")
             pos.append(p[0])
             dele.append(p[1])
             ilen.append(len(s))
+            iun.append(len(p[2]))
             ins.append(s)
     pos = np.array(pos, np.uint32)
     dele = np.array(dele, np.uint32)
     ilen = np.array(ilen, np.uint32)
+    iun = np.array(iun, np.uint32)
     insb = np.frombuffer(b"".join(ins) or b"\0", dtype=np.uint8)
     b, nb, uo = ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_void_p()
-    _L().yw_replay(pos.ctypes.data, dele.ctypes.data, ilen.ctypes.data, insb.ctypes.data, len(pos), client,
-                   ctypes.byref(b), ctypes.byref(nb), ctypes.byref(uo))
+    _L().yw_replay(pos.ctypes.data, dele.ctypes.data, ilen.ctypes.data, iun.ctypes.data, insb.ctypes.data, len(pos),
+                   client, ctypes.byref(b), ctypes.byref(nb), ctypes.byref(uo))
     data = np.frombuffer(ctypes.string_at(b, nb.value), dtype=np.uint8).copy()
     upd_off = np.ctypeslib.as_array(ctypes.cast(uo, ctypes.POINTER(ctypes.c_uint64)), (len(pos) + 1,)).copy()
     _L().yw_free(b)
