@@ -74,7 +74,7 @@ typedef struct {
   float ms_total, ms_fast, ms_exact, ms_tail;
   float ms_decode; /* merge: k_decode (ms_fast = k_fast_merge only) */
   float ms_big;    /* merge: documents over the LDS capacities (k_big_count + k_big_merge) */
-  uint32_t reserved;
+  uint32_t docs_overlap; /* merge: of docs_big, documents with overlapping updates (run order, splices) */
   uint64_t docs_big; /* merge: documents written by the tiled kernel (docs_exact: exact engine) */
 } ymerge_stats;
 

@@ -22,6 +22,7 @@ def engine():
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_overlap_docs(engine, oracle, seed):
     check_batch(engine, oracle, batch_of(overlap_docs(seed)))
+    print(engine.stats())
 
 
 def test_c4_full_size_docs(engine, oracle):
@@ -29,3 +30,7 @@ def test_c4_full_size_docs(engine, oracle):
     duplicated updates)."""
     b = workloads.delete_heavy_docs(48, ops_per_doc=5000)
     check_batch(engine, oracle, b)
+    st = engine.stats()
+    print(st)
+    assert st["docs_overlap"] >= 40, st  # run order + splices on the tiled kernel
+    assert st["docs_exact"] <= 4, st     # only Item/GC ties in the insertion-sort tail

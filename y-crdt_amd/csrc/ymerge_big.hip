@@ -15,8 +15,10 @@
 //                tiles) -> DeleteSet: distinct clients + first occurrence (LDS hash),
 //                hashbrown iteration order, ranges sorted by (client, start), segmented
 //                union, write.
-// Same fast-path precondition as the LDS kernel: a partial overlap or a
-// same-clock mismatch hands the document to the exact engine (path = 1).
+// Overlapping documents (partial overlaps, same-clock blocks that differ — snapshot +
+// pending-log merges) switch to the run order of the yrs loop (big_run_order below) and
+// write the overlapping blocks spliced; the exact engine (path = 1) keeps only the
+// shapes that order does not cover (see big_run_order).
 // Reference semantics: yrs/src/update.rs:537-704 (merge), :490-535 (encode),
 // yrs/src/id_set.rs:129-164, 385-410 (DeleteSet union and order).
 #include "yblock.h"
@@ -37,15 +39,22 @@ struct BigMem {
   uint64_t *k0, *k1;                // [M] sort keys (ping-pong)
   uint32_t *v0, *v1;                // [M] sort values
   uint32_t *fE, *fF, *sseg;         // [NB] per sorted position: running end, flags; per client segment counts
+  uint32_t *fO;                     // [NB] per sorted position: splice offset (overlap mode)
   uint32_t *ec, *et;                // [NE] DeleteSet entries
   uint32_t *rs, *re, *ri;           // [NR] DeleteSet ranges
   uint32_t *chead, *cend, *coff, *cpre; // [NR + 1] union of sorted live ranges
+  // overlap mode: per block update / run, sorted position -> block; per run (<= NB runs):
+  // first block, blocks, client, start, update, first-block kind, previous run of its
+  // update, rank, rank -> run (two buffers), first sorted block position; per update: last rank
+  uint32_t *bu, *rr, *sord;
+  uint32_t *Rb, *Rn, *Rc, *Rs, *Ru, *Rk, *Rp, *Rpos, *Rord, *Rord2, *Roff;
+  uint32_t *lu;
 };
-__host__ __device__ inline uint64_t big_words(uint32_t NB, uint32_t NE, uint32_t NR) {
+__host__ __device__ inline uint64_t big_words(uint32_t NB, uint32_t NE, uint32_t NR, uint32_t U) {
   const uint64_t M = (uint64_t)(NB > NR ? NB : NR) + 2;
-  return 4 * M + 2 * M + 8ull * NB + 2ull * NE + 3ull * NR + 4ull * (NR + 2) + 64;
+  return 4 * M + 2 * M + 9ull * NB + 2ull * NE + 3ull * NR + 4ull * (NR + 2) + 14ull * (NB + 2) + U + 96;
 }
-__device__ inline BigMem big_carve(uint32_t *w, uint32_t NB, uint32_t NE, uint32_t NR) {
+__device__ inline BigMem big_carve(uint32_t *w, uint32_t NB, uint32_t NE, uint32_t NR, uint32_t U) {
   BigMem m;
   const uint64_t M = (uint64_t)(NB > NR ? NB : NR) + 2;
   uint64_t o = 0;
@@ -75,6 +84,13 @@ __device__ inline BigMem big_carve(uint32_t *w, uint32_t NB, uint32_t NE, uint32
   m.cend = take(NR + 2);
   m.coff = take(NR + 2);
   m.cpre = take(NR + 2);
+  m.fO = take(NB);
+  m.bu = take(NB);
+  m.rr = take(NB);
+  m.sord = take(NB);
+  uint32_t **ra[11] = {&m.Rb, &m.Rn, &m.Rc, &m.Rs, &m.Ru, &m.Rk, &m.Rp, &m.Rpos, &m.Rord, &m.Rord2, &m.Roff};
+  for (int i = 0; i < 11; i++) *ra[i] = take(NB + 1);
+  m.lu = take(U);
   return m;
 }
 
@@ -163,7 +179,7 @@ __global__ void __launch_bounds__(NT) k_big_count(BatchIn b, uint8_t *path, uint
   counts[4 * d + 1] = (uint32_t)s_nb;
   counts[4 * d + 2] = (uint32_t)s_ne;
   counts[4 * d + 3] = (uint32_t)s_nr;
-  need[d] = (big_words((uint32_t)s_nb, (uint32_t)s_ne, (uint32_t)s_nr) + 1) & ~1ull;
+  need[d] = (big_words((uint32_t)s_nb, (uint32_t)s_ne, (uint32_t)s_nr, U) + 1) & ~1ull;
   atomicAdd(n_big, 1u);
 }
 
@@ -230,6 +246,239 @@ __device__ int wg_sort(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1, u
   return which;
 }
 
+// ------------------------------------------------------------------ overlap mode
+// Can block (pos, clock length len) be written from offset `off` the way the exact engine
+// writes a BlockCarrier::splice (update.rs:795-816, block.rs:1837-1879): GC, Deleted, JSON,
+// Any, and Strings whose split keeps len - off UTF-16 units and re-encodes cleanly.  Other
+// contents make yrs panic (ItemContent::splice -> None); those documents go to the exact
+// engine, which reports it.
+__device__ __noinline__ bool big_splice_ok(const uint8_t *p, uint32_t n, uint32_t pos, uint32_t len, uint32_t off) {
+  Cur c{p, n, pos};
+  uint8_t info;
+  bool cn;
+  uint32_t v;
+  if (rd_u8(c, info)) return false;
+  if (info == 0) return true;
+  if (info & 0x80) {
+    rd_var_u32(c, v, cn);
+    rd_var_u32(c, v, cn);
+  }
+  if (info & 0x40) {
+    rd_var_u32(c, v, cn);
+    rd_var_u32(c, v, cn);
+  }
+  if ((info & 0xC0) == 0) {
+    uint32_t pi;
+    rd_var_u32(c, pi, cn);
+    if (pi == 1) {
+      rd_var_u32(c, v, cn);
+      c.i += v;
+    } else {
+      rd_var_u32(c, v, cn);
+      rd_var_u32(c, v, cn);
+    }
+    if (info & 0x20) {
+      rd_var_u32(c, v, cn);
+      c.i += v;
+    }
+  }
+  const uint8_t ref = info & 15;
+  if (ref == 1 || ref == 2 || ref == 8) return true;
+  if (ref != 4) return false;
+  if (rd_var_u32(c, v, cn) || c.i + v > n) return false;
+  const uint8_t *str = p + c.i;
+  uint32_t bo, bo2;
+  if (str_split16(str, v, off, bo) || bo >= v) return false;
+  if (str_len16(str + bo, v - bo) != len - off) return false;
+  return str_split16(str + bo, v - bo, len - off, bo2) == 0;
+}
+
+// Order in which yrs' loop (update.rs:565-697) consumes the blocks of an overlapping
+// document.  Each update's decoder yields its client sections in descending client order
+// (IntoBlocks, update.rs:1030-1045); a "run" is a maximal contiguous stretch of one
+// section.  Once a decoder is popped, the skip loop (:611-620) drops its covered blocks,
+// the straddling block is spliced (:656-679) and the inner loop (:686-696) writes the rest
+// of the run in the same iteration: runs are consumed whole, one per pop.  The live
+// decoders are (re)sorted by their current run's (client desc, start asc); equal keys keep
+// the deque order — the decoder popped most recently first, decoders never popped after
+// them by input index — which is the heap order of the oracle (yrs_oracle.c
+// merge_blocks).  So the runs are sorted by (client desc, start asc) and every tie group
+// by (rank of the run's predecessor in its update desc, no predecessor last, update asc),
+// refined until stable (the predecessor has a smaller key, so the refinement is a DAG
+// walk).  Returns false (-> exact engine) for: a client with two runs in one update (a
+// Skip inside a section, or a repeated section), a tie group above 256 runs or over 16
+// refinement rounds, and an Item-vs-GC tie among the runs consumed while <= 20 decoders
+// are live (Rust's insertion-sort regime).  On success m.sord[j] is the
+// block at sorted position j (runs in order, blocks in run order).
+template <int NT>
+__device__ __noinline__ bool big_run_order(const BatchIn &b, uint64_t u0, uint32_t U, uint64_t B0, uint32_t NB,
+                                           BigMem &m, uint32_t *ws, uint32_t *sc, uint8_t *lds) {
+  const uint32_t t = threadIdx.x;
+  constexpr uint32_t NONE = 0xFFFFFFFFu;
+  // 1 update of every block (the records keep the byte position), run heads and ids
+  const uint64_t *uo = b.upd_off + u0;
+  for (uint32_t j = t; j < NB; j += NT) {
+    const uint64_t x = B0 + m.bp[j];
+    uint32_t lo = 0, hi = U; // last update with uo[u] <= x
+    while (lo + 1 < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (uo[mid] <= x) lo = mid;
+      else hi = mid;
+    }
+    m.bu[j] = lo;
+  }
+  __syncthreads();
+  uint32_t NRun = 0;
+  for (uint32_t base = 0; base < NB; base += NT) {
+    const uint32_t j = base + t;
+    bool h = false;
+    if (j < NB)
+      h = j == 0 || m.bu[j] != m.bu[j - 1] || m.bc[j] != m.bc[j - 1] || m.bk[j] != m.bk[j - 1] + m.bl[j - 1];
+    uint32_t T;
+    const uint32_t pre = bscan_sum<NT>(h ? 1u : 0u, ws, T);
+    if (j < NB) {
+      const uint32_t r = NRun + pre + (h ? 1 : 0) - 1;
+      m.rr[j] = r;
+      if (h) {
+        m.Rb[r] = j;
+        m.Rc[r] = m.bc[j];
+        m.Rs[r] = m.bk[j];
+        m.Ru[r] = m.bu[j];
+        m.Rk[r] = m.bm[j] & 3;
+      }
+    }
+    NRun += T;
+  }
+  __syncthreads();
+  for (uint32_t r = t; r < NRun; r += NT) m.Rn[r] = (r + 1 < NRun ? m.Rb[r + 1] : NB) - m.Rb[r];
+  // 2 predecessor of every run in its update's stream (clients descending): sort by
+  //   (update, client desc); a repeated (update, client) -> exact engine
+  uint32_t bad = 0;
+  for (uint32_t r = t; r < NRun; r += NT) {
+    m.k0[r] = ((uint64_t)m.Ru[r] << 32) | (uint32_t)~m.Rc[r];
+    m.v0[r] = r;
+  }
+  __syncthreads();
+  const uint32_t *pv = m.v0;
+  {
+    uint32_t uns = 0;
+    for (uint32_t r = t; r + 1 < NRun; r += NT) uns |= m.k0[r] > m.k0[r + 1];
+    if (__syncthreads_or(uns) && wg_sort<NT>(m.k0, m.v0, m.k1, m.v1, NRun, lds)) pv = m.v1;
+  }
+  const uint64_t *pk = pv == m.v0 ? m.k0 : m.k1;
+  for (uint32_t j = t; j < NRun; j += NT) {
+    const uint32_t r = pv[j];
+    uint32_t pr = NONE;
+    if (j > 0 && (pk[j] >> 32) == (pk[j - 1] >> 32)) {
+      if (pk[j] == pk[j - 1]) bad = 1;
+      pr = pv[j - 1];
+    }
+    m.Rp[r] = pr;
+  }
+  if (__syncthreads_or(bad)) return false;
+  // 3 runs by (client desc, start asc, run id): run ids ascend with the update index
+  for (uint32_t r = t; r < NRun; r += NT) {
+    m.k0[r] = ((uint64_t)(uint32_t)~m.Rc[r] << 32) | m.Rs[r];
+    m.v0[r] = r;
+  }
+  __syncthreads();
+  const uint32_t *ov = m.v0;
+  {
+    uint32_t uns = 0;
+    for (uint32_t r = t; r + 1 < NRun; r += NT) uns |= m.k0[r] > m.k0[r + 1];
+    if (__syncthreads_or(uns) && wg_sort<NT>(m.k0, m.v0, m.k1, m.v1, NRun, lds)) ov = m.v1;
+  }
+  for (uint32_t j = t; j < NRun; j += NT) {
+    const uint32_t r = ov[j];
+    m.Rord[j] = r;
+    m.Rord2[j] = r;
+    m.Rpos[r] = j;
+  }
+  __syncthreads();
+  auto key = [&](uint32_t r) -> uint64_t { return ((uint64_t)m.Rc[r] << 32) | m.Rs[r]; };
+  // 4 tie groups: one lane per group re-sorts it by the predecessors' current ranks
+  for (uint32_t round = 0;; round++) {
+    uint32_t flags = 0; // 1 changed, 2 too big
+    for (uint32_t j = t; j < NRun; j += NT) {
+      const uint64_t kj = key(m.Rord[j]);
+      if (j > 0 && key(m.Rord[j - 1]) == kj) continue;
+      uint32_t g1 = j + 1;
+      while (g1 < NRun && key(m.Rord[g1]) == kj) g1++;
+      if (g1 - j == 1) continue;
+      if (g1 - j > 256) {
+        flags |= 2;
+        continue;
+      }
+      for (uint32_t q = j; q < g1; q++) {
+        const uint32_t x = m.Rord[q], px = m.Rp[x];
+        uint32_t z = q;
+        while (z > j) {
+          const uint32_t y = m.Rord2[z - 1], py = m.Rp[y];
+          const bool before = px != NONE ? (py == NONE || m.Rpos[px] > m.Rpos[py]) : (py == NONE && m.Ru[x] < m.Ru[y]);
+          if (!before) break;
+          m.Rord2[z] = y;
+          z--;
+        }
+        m.Rord2[z] = x;
+      }
+      for (uint32_t q = j; q < g1; q++) flags |= m.Rord2[q] != m.Rord[q];
+    }
+    const uint32_t f = __syncthreads_or(flags & 1) | (__syncthreads_or(flags & 2) << 1);
+    if (f & 2) return false;
+    if (!(f & 1)) break;
+    if (round >= 16) return false;
+    for (uint32_t j = t; j < NRun; j += NT) {
+      const uint32_t r = m.Rord2[j];
+      m.Rord[j] = r;
+      m.Rpos[r] = j;
+    }
+    __syncthreads();
+  }
+  // 5 Item-vs-GC ties consumed while <= 20 decoders are live: last rank (+1) per update,
+  //   V = the smallest v with #{u : lu[u] >= v} <= 20, tail = ranks >= V - 1
+  for (uint32_t u = t; u < U; u += NT) m.lu[u] = 0;
+  __syncthreads();
+  for (uint32_t j = t; j < NRun; j += NT) atomicMax(&m.lu[m.Ru[m.Rord[j]]], j + 1);
+  __syncthreads();
+  uint32_t lo = 1, hi = NRun + 1;
+  while (lo < hi) { // uniform
+    const uint32_t mid = (lo + hi) >> 1;
+    uint32_t c = 0, T;
+    for (uint32_t u = t; u < U; u += NT) c += m.lu[u] >= mid;
+    bscan_sum<NT>(c, ws, T);
+    if (T <= 20) hi = mid;
+    else lo = mid + 1;
+  }
+  const uint32_t V = lo;
+  for (uint32_t j = t; j < NRun; j += NT) {
+    const uint32_t r = m.Rord[j];
+    const uint64_t kj = key(r);
+    if (j > 0 && key(m.Rord[j - 1]) == kj) continue;
+    uint32_t g1 = j + 1, kinds = 1u << m.Rk[r];
+    while (g1 < NRun && key(m.Rord[g1]) == kj) kinds |= 1u << m.Rk[m.Rord[g1++]];
+    if ((kinds & 3) == 3 && g1 >= V) bad = 1; // last rank g1 - 1 >= V - 1
+  }
+  if (__syncthreads_or(bad)) return false;
+  // 6 sorted block positions: runs in rank order, blocks in run order
+  uint32_t acc = 0;
+  for (uint32_t base = 0; base < NRun; base += NT) {
+    const uint32_t j = base + t;
+    const uint32_t n = j < NRun ? m.Rn[m.Rord[j]] : 0;
+    uint32_t T;
+    const uint32_t pre = bscan_sum<NT>(n, ws, T);
+    if (j < NRun) m.Roff[j] = acc + pre;
+    acc += T;
+  }
+  __syncthreads();
+  for (uint32_t j = t; j < NB; j += NT) {
+    const uint32_t r = m.rr[j];
+    m.sord[m.Roff[m.Rpos[r]] + (j - m.Rb[r])] = j;
+  }
+  __syncthreads();
+  (void)sc;
+  return true;
+}
+
 // ------------------------------------------------------------------ k_big_merge
 template <int NT> struct BigShared {
   uint32_t ws[2 * (NT / 64) + 8];
@@ -248,18 +497,24 @@ __global__ void __launch_bounds__(NT) k_big_merge(BatchIn b, const uint32_t *cou
   const uint32_t t = threadIdx.x;
   uint32_t *ws = S.ws, *sc = S.sc;
   const uint32_t NB = counts[4 * d + 1], NE = counts[4 * d + 2], NR = counts[4 * d + 3];
-  BigMem m = big_carve(scratch + scr_off[d], NB, NE, NR);
   const uint64_t u0 = b.doc_upd[d], u1 = b.doc_upd[d + 1];
   const uint32_t U = (uint32_t)(u1 - u0);
+  BigMem m = big_carve(scratch + scr_off[d], NB, NE, NR, U);
   const uint64_t B0 = b.upd_off[u0];
   const uint32_t nbytes = (uint32_t)(b.upd_off[u1] - B0);
   const uint8_t *in = b.bytes + B0;
   const uint64_t slot = 2 * B0 + 64ull * d;
   const uint64_t cap = 2ull * nbytes + 64;
   uint8_t *out = o.out + slot;
+  bool om = false; // overlap mode: m.sord holds the run order of big_run_order
   auto finish = [&](uint8_t p, uint8_t st, uint64_t len) {
     if (t == 0) {
-      if (p == 1) atomicAdd(&o.npath[1], 1u);
+      if (p == 1) {
+        atomicAdd(&o.npath[1], 1u);
+        atomicAdd(&o.npath[4], 1u); // tiled -> exact engine
+      } else if (om) {
+        atomicAdd(&o.npath[3], 1u); // written in overlap mode
+      }
       o.path[d] = p;
       o.status[d] = st;
       o.out_len[d] = len;
@@ -386,15 +641,17 @@ __global__ void __launch_bounds__(NT) k_big_merge(BatchIn b, const uint32_t *cou
       if (wg_sort<NT>(m.k0, m.v0, m.k1, m.v1, NB, S.un)) sval = m.v1;
     }
   }
-  auto srt = [&](uint32_t j) -> uint32_t { return ident ? j : sval[j]; };
+  auto srt = [&](uint32_t j) -> uint32_t { return om ? m.sord[j] : (ident ? j : sval[j]); };
 
   // ---- 3 classify (tiles of NT sorted positions, carries between tiles):
-  //      running end E (segmented max), keep / Skip / violation, duplicate check against
-  //      the last kept block, emitted blocks per client segment
+  //      running end E (segmented max), keep / Skip / drop; first pass: a partial overlap
+  //      or a same-clock block that is not a duplicate of the kept one -> overlap mode,
+  //      which classifies again in run order and keeps the straddling block spliced at E
+  //      (flag 4, offset E - clock); emitted blocks per client segment
   uint32_t NC = 0; // client segments
-  {
+  for (int pass = 0; pass < 2; pass++) {
     uint32_t cE = 0, cK = 0, cS = 0, cH = 0; // carries: running end, last kept (j+1), emitted count, heads
-    uint32_t viol = 0, pan = 0;
+    uint32_t viol = 0, pan = 0, zl = 0, bsp = 0;
     for (uint32_t base = 0; base < NB; base += NT) {
       const uint32_t j = base + t;
       const bool valid = j < NB;
@@ -414,19 +671,25 @@ __global__ void __launch_bounds__(NT) k_big_merge(BatchIn b, const uint32_t *cou
       const uint32_t E = hd ? 0 : (pf ? pv : (cE > pv ? cE : pv));
       uint32_t flag = 0;
       if (valid) {
-        if (l == 0) viol = 1; // zero-length GC: exact engine
+        if (l == 0) zl = 1; // zero-length GC: exact engine
         if (hd || k >= E) {
           flag = 1;
           if (!hd && k > E) flag |= 2;
         } else if (e > E) {
-          viol = 1; // partial overlap
+          if (!om) {
+            viol = 1; // partial overlap
+          } else {
+            flag = 1 | 4;
+            m.fO[j] = E - k;
+            if (!big_splice_ok(in, nbytes, m.bp[r], l, E - k)) bsp = 1;
+          }
         }
       }
       // last kept position (j + 1) before j within the segment
       uint32_t qf, qv;
       bscan_seg<NT, OpMax>(valid && hd, (flag & 1) ? j + 1 : 0, ws, qf, qv);
       const uint32_t last = hd ? 0 : (qf ? qv : (cK > qv ? cK : qv));
-      if (valid && !(flag & 1) && last) {
+      if (!om && valid && !(flag & 1) && last) {
         const uint32_t kr = srt(last - 1);
         if (m.bk[kr] == k) { // same start: must be an exact duplicate (kind, length, bytes)
           const uint32_t la = m.bm[kr] >> 8, lb = mt >> 8;
@@ -435,7 +698,7 @@ __global__ void __launch_bounds__(NT) k_big_merge(BatchIn b, const uint32_t *cou
           if (!same) viol = 1;
         }
       }
-      if (valid && (flag & 1) && (mt & 8)) pan = 1; // yrs panics encoding a kept String off a char boundary
+      if (valid && (flag & 5) == 1 && (mt & 8)) pan = 1; // yrs panics encoding a kept String off a char boundary
       // emitted blocks per client segment (kept + Skips) and the segment rank
       const uint32_t cnt = (flag & 1) + ((flag >> 1) & 1);
       uint32_t sf, sv2;
@@ -465,15 +728,26 @@ __global__ void __launch_bounds__(NT) k_big_merge(BatchIn b, const uint32_t *cou
       __syncthreads();
     }
     NC = cH;
-    const uint32_t vp = __syncthreads_or(viol | (pan << 1));
-    if (vp & 1) { // partial overlap / same-clock mismatch: exact engine
+    // (__syncthreads_or returns 0/1: one barrier per flag)
+    const uint32_t vp = (__syncthreads_or(viol) ? 1u : 0u) | (__syncthreads_or(pan) ? 2u : 0u) |
+                        (__syncthreads_or(zl | bsp) ? 4u : 0u);
+    if (vp & 4) { // zero-length GC, splice the device does not restate: exact engine
       finish(1, 0, 0);
       return;
+    }
+    if (vp & 1) { // partial overlap / same-clock mismatch: the run order of the yrs loop
+      if (!big_run_order<NT>(b, u0, U, B0, NB, m, ws, sc, S.un)) {
+        finish(1, 0, 0);
+        return;
+      }
+      om = true;
+      continue;
     }
     if (vp & 2) {
       finish(0, E_PANIC, 0);
       return;
     }
+    break;
   }
 
   // ---- 4 sizes, offsets, write (LDS-staged per tile when the tile's bytes fit)
@@ -509,7 +783,13 @@ __global__ void __launch_bounds__(NT) k_big_merge(BatchIn b, const uint32_t *cou
           s += varlen(cnt) + varlen(c) + varlen(k);
         }
         if (flag & 2) s += 1 + varlen(k - E);
-        if (flag & 1) s += canon_size(in, nbytes, p, c, k, l, mt);
+        if (flag & 4) {
+          Counter cn;
+          emit_block(in, nbytes, p, c, k, l, m.fO[j], cn);
+          s += (uint32_t)cn.n;
+        } else if (flag & 1) {
+          s += canon_size(in, nbytes, p, c, k, l, mt);
+        }
       }
       cH += HT;
       uint64_t TT;
@@ -536,7 +816,10 @@ __global__ void __launch_bounds__(NT) k_big_merge(BatchIn b, const uint32_t *cou
           w_var(w, k - E);
         }
         if (flag & 1) {
-          if ((mt & 4) && !(mt & 8)) {
+          if (flag & 4) {
+            Writer w2 = w;
+            emit_block(in, nbytes, p, c, k, l, m.fO[j], w2);
+          } else if ((mt & 4) && !(mt & 8)) {
             Writer w2 = w;
             emit_block(in, nbytes, p, c, k, l, 0, w2);
           } else {

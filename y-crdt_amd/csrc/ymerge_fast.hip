@@ -543,19 +543,20 @@ __global__ void __launch_bounds__(NT, 3) k_fast_merge(BatchIn b, FastCaps caps, 
       const uint32_t e = rk[k] + rl[k];
       const uint32_t E = hd[k] ? 0 : run;
       uint32_t flag = 0;
-      if (rl[k] == 0) viol = 1; // zero-length GC: leave to the exact engine
+      if (rl[k] == 0) viol |= 2; // zero-length GC: leave to the exact engine
       if (hd[k] || rk[k] >= E) {
         flag = 1;                               // keep
         if (!hd[k] && rk[k] > E) flag |= 2;     // Skip of (k - E) before it
       } else if (e > E) {
-        viol = 1; // partial overlap
+        viol |= 1; // partial overlap: the tiled kernel's overlap mode
       }
       rE[k] = E;
       rF[k] = flag;
       run = hd[k] ? e : OpMax::f(run, e);
     }
-    if (__syncthreads_or(viol)) {
-      handover();
+    const uint32_t vz = __syncthreads_or(viol & 2);
+    if (vz || __syncthreads_or(viol & 1)) {
+      handover(vz ? 1 : 2);
       return;
     }
   }
@@ -591,9 +592,9 @@ __global__ void __launch_bounds__(NT, 3) k_fast_merge(BatchIn b, FastCaps caps, 
         if (rm[k] & 8) pan = 1; // yrs panics encoding a kept String that is not valid UTF-8
       }
     }
-    const uint32_t vp = __syncthreads_or(viol | (pan << 1));
-    if (vp & 1) {
-      handover();
+    const uint32_t vp = (__syncthreads_or(viol) ? 1u : 0u) | (__syncthreads_or(pan) ? 2u : 0u); // (0/1 each)
+    if (vp & 1) { // same-clock blocks that differ: the tiled kernel's overlap mode
+      handover(2);
       return;
     }
     if (vp & 2) {

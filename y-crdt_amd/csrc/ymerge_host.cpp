@@ -205,16 +205,19 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   hipEventRecord(c->ev[1], c->s);
   // exact engine for documents the fast or tiled path handed over (path == 1)
   uint64_t words = 0;
-  uint32_t n_exact = 0;
+  uint32_t n_exact = 0, n_overlap = 0;
   if (n_p1 || n_p2) {
     ym::launch_seq_count(b, path, status, c->counts.as<uint32_t>(), c->need.as<uint64_t>(), c->counter.as<uint32_t>(),
                          c->s);
     ym::launch_scan_u64(c->need.as<uint64_t>(), c->scr_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
     hipMemcpyAsync(c->h_pinned + 8, c->scr_off.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, c->s);
     hipMemcpyAsync(c->h_pinned + 9, c->counter.p, 4, hipMemcpyDeviceToHost, c->s);
+    hipMemcpyAsync(c->h_pinned + 14, c->counter.as<uint32_t>() + 7, 8, hipMemcpyDeviceToHost, c->s);
     if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
     words = c->h_pinned[8];
     n_exact = (uint32_t)(c->h_pinned[9] & 0xFFFFFFFFu);
+    n_overlap = (uint32_t)(c->h_pinned[14] & 0xFFFFFFFFu);
+    n_big -= (uint32_t)(c->h_pinned[14] >> 32); // tiled-kernel documents handed to the exact engine
   }
   if (n_exact) {
     if (!c->scratch.ensure((size_t)words * 4 + 64)) return YMERGE_ERR_DEVICE;
@@ -251,6 +254,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   c->stats.bytes_out = total;
   c->stats.docs_exact = n_exact;
   c->stats.docs_big = n_big;
+  c->stats.docs_overlap = n_overlap;
   c->stats.docs_fast = n_docs - n_exact - n_big;
   c->stats.ms_big = t61;
   c->stats.ms_fast = t01;

@@ -6,6 +6,7 @@ C3  Zipf(1.5) op counts on [1, 1e4] (seed 0x5EED)
 C4  delete-heavy docs: GC'd snapshot + per-op log, 10% withheld, 5% duplicated (seed 0xDE1E7E)
 """
 import ctypes
+import functools
 import gzip
 import json
 import os
@@ -156,6 +157,7 @@ def trace_path(name):
     return os.path.join(os.path.dirname(_HERE), "tests", "golden", name + ".json.gz")
 
 
+@functools.lru_cache(maxsize=8)
 def trace_updates(path=None, client=1):
     """C1: one update per patch of an editing trace (default automerge-paper).
 

@@ -36,7 +36,7 @@ class _Stats(ctypes.Structure):
                 ("docs_fast", ctypes.c_uint64), ("docs_exact", ctypes.c_uint64), ("docs_error", ctypes.c_uint64),
                 ("ms_total", ctypes.c_float), ("ms_fast", ctypes.c_float), ("ms_exact", ctypes.c_float),
                 ("ms_tail", ctypes.c_float), ("ms_decode", ctypes.c_float), ("ms_big", ctypes.c_float),
-                ("reserved", ctypes.c_uint32), ("docs_big", ctypes.c_uint64)]
+                ("docs_overlap", ctypes.c_uint32), ("docs_big", ctypes.c_uint64)]
 
 
 class _DevRes(ctypes.Structure):
