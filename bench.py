@@ -56,7 +56,7 @@ def parse():
 
 def pmc_traffic(workload):
     """HBM bytes per launch of the pipeline from a committed rocprofv3 PMC pass, if any."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    p = os.path.join(ROOT, "profiles", f"pmc_traffic_{workload}.json")
     if os.path.exists(p):
         try:
             with open(p) as f:

@@ -3,7 +3,7 @@ evidence under profiles/:
 
   profiles/<TAG>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (rocpd2summary)
   profiles/<TAG>_pmc.json           per-kernel FETCH_SIZE / WRITE_SIZE (separate --pmc passes)
-  profiles/pmc_traffic.json         HBM bytes per launch of the dominant kernel, read by bench.py
+  profiles/pmc_traffic_<wl>.json    HBM bytes per launch of the dominant kernels, read by bench.py
 
 HBM traffic follows MI355X_MICROARCH.md (rocprofv3 section): FETCH_SIZE and WRITE_SIZE
 are in KiB; on gfx950 FETCH_SIZE reports half of the bytes of wide streaming reads,
@@ -66,7 +66,7 @@ def main():
         fs = sum(fetch[k] for k in fk)
         ws = sum(write[k] for k in wk)
         t = (2 * fs + ws) * 1024
-        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as f:
+        with open(os.path.join(ROOT, "profiles", f"pmc_traffic_{wl}.json"), "w") as f:
             json.dump({"tag": tag, "workload": wl, "kernel": " + ".join(fk), "fetch_kib": fs, "write_kib": ws,
                        "traffic_bytes_per_launch": t,
                        "formula": "(2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE half-count correction)"},
