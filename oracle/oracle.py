@@ -102,6 +102,69 @@ def encode_state_vector_from_update_v1(update):
     return _take(out, olen)
 
 
+def merge_updates_v2(updates, mode=1):
+    """lib0 v2 merge (yrs/src/alt.rs:35-48)."""
+    bufs = [_buf(u) for u in updates]
+    n = len(bufs)
+    ptrs = (ctypes.POINTER(ctypes.c_uint8) * max(1, n))(*[ctypes.cast(b[0], ctypes.POINTER(ctypes.c_uint8)) for b in bufs])
+    lens = (ctypes.c_size_t * max(1, n))(*[b[1] for b in bufs])
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    L = lib()
+    L.yo_merge_updates_v2.argtypes = L.yo_merge_updates_v1.argtypes
+    st = L.yo_merge_updates_v2(ptrs, lens, n, mode, ctypes.byref(out), ctypes.byref(olen))
+    if st:
+        raise OracleError(st)
+    return _take(out, olen)
+
+
+def diff_updates_v2(update, sv):
+    a, an = _buf(update)
+    b, bn = _buf(sv)
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    L = lib()
+    L.yo_diff_updates_v2.argtypes = L.yo_diff_updates_v1.argtypes
+    st = L.yo_diff_updates_v2(a, an, b, bn, ctypes.byref(out), ctypes.byref(olen))
+    if st:
+        raise OracleError(st)
+    return _take(out, olen)
+
+
+def encode_state_vector_from_update_v2(update):
+    a, an = _buf(update)
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    L = lib()
+    L.yo_encode_state_vector_from_update_v2.argtypes = L.yo_encode_state_vector_from_update_v1.argtypes
+    st = L.yo_encode_state_vector_from_update_v2(a, an, ctypes.byref(out), ctypes.byref(olen))
+    if st:
+        raise OracleError(st)
+    return _take(out, olen)
+
+
+def _convert(fn, update):
+    a, an = _buf(update)
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    f = getattr(lib(), fn)
+    f.argtypes = lib().yo_encode_state_vector_from_update_v1.argtypes
+    st = f(a, an, ctypes.byref(out), ctypes.byref(olen))
+    if st:
+        raise OracleError(st)
+    return _take(out, olen)
+
+
+def convert_update_v1_to_v2(update):
+    """Update::decode_v1(u).encode_v2() (test helper)."""
+    return _convert("yo_convert_update_v1_to_v2", update)
+
+
+def convert_update_v2_to_v1(update):
+    """Update::decode_v2(u).encode_v1() (test helper)."""
+    return _convert("yo_convert_update_v2_to_v1", update)
+
+
 def sync_step1_v1(update):
     a, an = _buf(update)
     L = lib()
@@ -137,8 +200,10 @@ def status_of(fn, *args, **kw):
         return e.code, None
 
 
-def merge_batch(data, upd_off, doc_upd, mode=0, threads=1):
-    """Arena batch; returns (list of bytes|None, status array)."""
+def merge_batch(data, upd_off, doc_upd, mode=0, threads=1, version=1):
+    """Arena batch; returns (arena, offsets, status array).  version 2 = lib0 v2."""
+    if version == 2:
+        mode |= 4
     data = np.ascontiguousarray(data, dtype=np.uint8)
     upd_off = np.ascontiguousarray(upd_off, dtype=np.uint64)
     doc_upd = np.ascontiguousarray(doc_upd, dtype=np.uint64)
@@ -154,7 +219,7 @@ def merge_batch(data, upd_off, doc_upd, mode=0, threads=1):
     return arena, out_off, status[:n_docs]
 
 
-def diff_batch(ubytes, u_off, svbytes, sv_off, threads=1):
+def diff_batch(ubytes, u_off, svbytes, sv_off, threads=1, version=1):
     ubytes = np.ascontiguousarray(ubytes, dtype=np.uint8)
     u_off = np.ascontiguousarray(u_off, dtype=np.uint64)
     svbytes = np.ascontiguousarray(svbytes, dtype=np.uint8)
@@ -163,15 +228,19 @@ def diff_batch(ubytes, u_off, svbytes, sv_off, threads=1):
     out = ctypes.POINTER(ctypes.c_uint8)()
     out_off = np.zeros(n_docs + 1, dtype=np.uint64)
     status = np.zeros(max(1, n_docs), dtype=np.uint8)
-    lib().yo_diff_batch(ubytes.ctypes.data, u_off.ctypes.data, svbytes.ctypes.data, sv_off.ctypes.data,
-                        n_docs, threads, ctypes.byref(out), out_off.ctypes.data, status.ctypes.data)
+    L = lib()
+    vp = ctypes.c_void_p
+    L.yo_diff_batch2.argtypes = [vp, vp, vp, vp, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                 ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)), vp, vp]
+    L.yo_diff_batch2(ubytes.ctypes.data, u_off.ctypes.data, svbytes.ctypes.data, sv_off.ctypes.data,
+                     n_docs, version, threads, ctypes.byref(out), out_off.ctypes.data, status.ctypes.data)
     total = int(out_off[-1])
     arena = ctypes.string_at(out, total) if total else b""
     lib().yo_free(out)
     return arena, out_off, status[:n_docs]
 
 
-def sv_batch(ubytes, u_off, threads=1):
+def sv_batch(ubytes, u_off, threads=1, version=1):
     """encode_state_vector_from_update_v1 per document (one update each)."""
     ubytes = np.ascontiguousarray(ubytes, dtype=np.uint8)
     u_off = np.ascontiguousarray(u_off, dtype=np.uint64)
@@ -179,8 +248,12 @@ def sv_batch(ubytes, u_off, threads=1):
     out = ctypes.POINTER(ctypes.c_uint8)()
     out_off = np.zeros(n_docs + 1, dtype=np.uint64)
     status = np.zeros(max(1, n_docs), dtype=np.uint8)
-    lib().yo_sv_batch(ubytes.ctypes.data, u_off.ctypes.data, n_docs, threads, ctypes.byref(out),
-                      out_off.ctypes.data, status.ctypes.data)
+    L = lib()
+    vp = ctypes.c_void_p
+    L.yo_sv_batch2.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                               ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)), vp, vp]
+    L.yo_sv_batch2(ubytes.ctypes.data, u_off.ctypes.data, n_docs, version, threads, ctypes.byref(out),
+                   out_off.ctypes.data, status.ctypes.data)
     total = int(out_off[-1])
     arena = ctypes.string_at(out, total) if total else b""
     lib().yo_free(out)

@@ -383,6 +383,7 @@ typedef struct {
 } span_t;
 typedef struct {
   uint8_t kind, ref, has_origin, has_ro, pkind, has_psub, tref, unsupported;
+  uint8_t json_any; /* lib0 v2: Embed/Format values are Any bytes (read_json = Any::decode) */
   uint64_t client, oc, rc, pc, sc, ec;
   uint32_t clock, len, ok, rk, pk, sk, ek;
   span_t pname, psub, cs, cs2;
@@ -1171,9 +1172,14 @@ int yo_f64_ryu(double x, char *buf, size_t cap) {
 }
 
 /* ------------------------------------------------------------------ content decode (block.rs:1786-1835) */
+static int doc_options_any(upd_t *u, rd_t *r, blk_t *b);
 static int doc_options_decode(upd_t *u, rd_t *r, blk_t *b) {
   /* Options::decode (doc.rs:840-872) */
   TRY(rd_buf(r, &b->cs.p, &b->cs.n)); /* guid */
+  return doc_options_any(u, r, b);
+}
+/* the options Any that follows the guid */
+static int doc_options_any(upd_t *u, rd_t *r, blk_t *b) {
   b->doc_skip_gc = 0;
   b->doc_auto_load = 0;
   b->doc_has_cid = 0;
@@ -2238,9 +2244,14 @@ int yo_merge_updates_v1(const uint8_t *const *updates, const size_t *lens, size_
 }
 
 /* StateVector::decode (state_vector.rs:107-120) */
+static int sv_decode_r(sv_t *sv, rd_t *rr);
 static int sv_decode(sv_t *sv, const uint8_t *p, size_t n) {
-  memset(sv, 0, sizeof(*sv));
   rd_t r = {p, n, 0};
+  return sv_decode_r(sv, &r);
+}
+static int sv_decode_r(sv_t *sv, rd_t *rp) {
+  memset(sv, 0, sizeof(*sv));
+  rd_t r = *rp;
   uint32_t len;
   TRY(rd_var_u32(&r, &len));
   if (len && cap_to_buckets(len) * 17ull > ALLOC_LIMIT) return YO_ERR_REFERENCE_PANIC;
@@ -2362,6 +2373,8 @@ int yo_encode_state_vector_from_update_v1(const uint8_t *update, size_t len, uin
 
 void yo_free(void *p) { free(p); }
 
+#include "yrs_oracle_v2.c"
+
 /* ------------------------------------------------------------------ y-sync framing
  * Message::encode / SyncMessage::encode (yrs/src/sync/protocol.rs:219-233, 245-258):
  * [MSG_SYNC = 0, step tag, varbuf(payload)]; Message::decode + SyncMessage::decode
@@ -2428,13 +2441,14 @@ static void *worker(void *arg) {
     if (d0 >= j->n_docs) break;
     for (size_t d = d0; d < d0 + 4 && d < j->n_docs; d++) {
       int st;
+      const bool v2 = j->mode & 4; /* lib0 v2 batch */
       if (j->is_diff == 2) {
-        st = yo_encode_state_vector_from_update_v1(j->bytes + j->upd_off[d], j->upd_off[d + 1] - j->upd_off[d],
-                                                   &j->outs[d], &j->lens[d]);
+        st = (v2 ? yo_encode_state_vector_from_update_v2 : yo_encode_state_vector_from_update_v1)(
+            j->bytes + j->upd_off[d], j->upd_off[d + 1] - j->upd_off[d], &j->outs[d], &j->lens[d]);
       } else if (j->is_diff) {
-        st = yo_diff_updates_v1(j->bytes + j->upd_off[d], j->upd_off[d + 1] - j->upd_off[d],
-                                j->svbytes + j->sv_off[d], j->sv_off[d + 1] - j->sv_off[d], &j->outs[d],
-                                &j->lens[d]);
+        st = (v2 ? yo_diff_updates_v2 : yo_diff_updates_v1)(j->bytes + j->upd_off[d], j->upd_off[d + 1] - j->upd_off[d],
+                                                            j->svbytes + j->sv_off[d], j->sv_off[d + 1] - j->sv_off[d],
+                                                            &j->outs[d], &j->lens[d]);
       } else {
         size_t u0 = j->doc_upd[d], u1 = j->doc_upd[d + 1];
         if (u1 - u0 > cap) {
@@ -2446,7 +2460,8 @@ static void *worker(void *arg) {
           ptrs[u - u0] = j->bytes + j->upd_off[u];
           lens[u - u0] = j->upd_off[u + 1] - j->upd_off[u];
         }
-        st = yo_merge_updates_v1(ptrs, lens, u1 - u0, j->mode, &j->outs[d], &j->lens[d]);
+        st = (v2 ? yo_merge_updates_v2 : yo_merge_updates_v1)(ptrs, lens, u1 - u0, j->mode & 3, &j->outs[d],
+                                                              &j->lens[d]);
       }
       j->status[d] = (uint8_t)st;
     }
@@ -2495,10 +2510,18 @@ int yo_merge_batch(const uint8_t *bytes, const uint64_t *upd_off, const uint64_t
   return run_batch(&j, threads, out, out_off);
 }
 
+int yo_diff_batch2(const uint8_t *ubytes, const uint64_t *u_off, const uint8_t *svbytes, const uint64_t *sv_off,
+                   size_t n_docs, int version, int threads, uint8_t **out, uint64_t *out_off, uint8_t *status);
 int yo_diff_batch(const uint8_t *ubytes, const uint64_t *u_off, const uint8_t *svbytes, const uint64_t *sv_off,
                   size_t n_docs, int threads, uint8_t **out, uint64_t *out_off, uint8_t *status) {
+  return yo_diff_batch2(ubytes, u_off, svbytes, sv_off, n_docs, 1, threads, out, out_off, status);
+}
+/* version 1 or 2 (lib0 v2: batch mode bit 4) */
+int yo_diff_batch2(const uint8_t *ubytes, const uint64_t *u_off, const uint8_t *svbytes, const uint64_t *sv_off,
+                   size_t n_docs, int version, int threads, uint8_t **out, uint64_t *out_off, uint8_t *status) {
   job_t j;
   memset(&j, 0, sizeof(j));
+  j.mode = version == 2 ? 4 : 0;
   j.bytes = ubytes;
   j.upd_off = u_off;
   j.svbytes = svbytes;
@@ -2509,10 +2532,17 @@ int yo_diff_batch(const uint8_t *ubytes, const uint64_t *u_off, const uint8_t *s
   return run_batch(&j, threads, out, out_off);
 }
 
+int yo_sv_batch2(const uint8_t *ubytes, const uint64_t *u_off, size_t n_docs, int version, int threads,
+                 uint8_t **out, uint64_t *out_off, uint8_t *status);
 int yo_sv_batch(const uint8_t *ubytes, const uint64_t *u_off, size_t n_docs, int threads, uint8_t **out,
                 uint64_t *out_off, uint8_t *status) {
+  return yo_sv_batch2(ubytes, u_off, n_docs, 1, threads, out, out_off, status);
+}
+int yo_sv_batch2(const uint8_t *ubytes, const uint64_t *u_off, size_t n_docs, int version, int threads,
+                 uint8_t **out, uint64_t *out_off, uint8_t *status) {
   job_t j;
   memset(&j, 0, sizeof(j));
+  j.mode = version == 2 ? 4 : 0;
   j.bytes = ubytes;
   j.upd_off = u_off;
   j.n_docs = n_docs;

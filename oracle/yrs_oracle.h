@@ -44,6 +44,14 @@ int yo_diff_updates_v1(const uint8_t *update, size_t update_len, const uint8_t *
 int yo_encode_state_vector_from_update_v1(const uint8_t *update, size_t len, uint8_t **out,
                                           size_t *out_len);
 void yo_free(void *p);
+/* lib0 v2 (yrs/src/alt.rs:35-48, 63-66, 88-97; codec yrs/src/updates/{decoder,encoder}.rs) */
+int yo_merge_updates_v2(const uint8_t *const *updates, const size_t *lens, size_t n, int mode, uint8_t **out,
+                        size_t *out_len);
+int yo_diff_updates_v2(const uint8_t *update, size_t update_len, const uint8_t *sv, size_t sv_len, uint8_t **out,
+                       size_t *out_len);
+int yo_encode_state_vector_from_update_v2(const uint8_t *update, size_t len, uint8_t **out, size_t *out_len);
+int yo_convert_update_v1_to_v2(const uint8_t *update, size_t len, uint8_t **out, size_t *out_len);
+int yo_convert_update_v2_to_v1(const uint8_t *update, size_t len, uint8_t **out, size_t *out_len);
 /* y-sync (yrs/src/sync/protocol.rs:62-69, 219-272): SyncStep1 message of an update's state
  * vector, and the SyncStep2 reply to a client's SyncStep1 message */
 int yo_sync_step1_v1(const uint8_t *update, size_t len, uint8_t **out, size_t *out_len);
