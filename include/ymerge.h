@@ -50,6 +50,13 @@ char *ymerge_updates_v1(const char *const *updates, const uint32_t *updates_len,
 char *ydiff_updates_v1(const char *update, uint32_t update_len, const char *state_vector, uint32_t sv_len,
                        uint32_t *out_len);
 char *yencode_state_vector_from_update_v1(const char *update, uint32_t update_len, uint32_t *out_len);
+/* lib0 v2 forms: yrs::merge_updates_v2 / diff_updates_v2 / encode_state_vector_from_update_v2
+ * (yrs/src/alt.rs:35-48, 88-97, 63-66) */
+char *ymerge_updates_v2(const char *const *updates, const uint32_t *updates_len, uint32_t updates_count,
+                        uint32_t *out_len);
+char *ydiff_updates_v2(const char *update, uint32_t update_len, const char *state_vector, uint32_t sv_len,
+                       uint32_t *out_len);
+char *yencode_state_vector_from_update_v2(const char *update, uint32_t update_len, uint32_t *out_len);
 /* frees a buffer returned by the three calls above */
 void ymerge_binary_destroy(char *ptr, uint32_t len);
 /* yffi's name, exported as a WEAK symbol: alone it frees this library's buffers; in a
@@ -121,6 +128,19 @@ int ysync_step1_v1_batch_device(ymerge_ctx *ctx, const uint8_t *d_bytes, const u
 int ysync_step2_v1_batch_device(ymerge_ctx *ctx, const uint8_t *d_bytes, const uint64_t *d_upd_off,
                                 const uint8_t *d_msg, const uint64_t *d_msg_off, uint64_t n_docs,
                                 ymerge_device_result *res);
+/* lib0 v2 (yrs/src/alt.rs:35-48, 63-66, 88-97): the same operations over v2-encoded updates
+ * and state vectors (yrs/src/updates/{decoder,encoder}.rs), outputs v2-encoded.  Device
+ * limits (status UNSUPPORTED): client ids >= 2^32; a key-table hit beyond the first 64 keys
+ * of one update. */
+int ymerge_updates_v2_batch_device(ymerge_ctx *ctx, const uint8_t *d_bytes, uint64_t n_bytes,
+                                   const uint64_t *d_upd_off, uint64_t n_updates, const uint64_t *d_doc_upd,
+                                   uint64_t n_docs, ymerge_device_result *res);
+int ydiff_updates_v2_batch_device(ymerge_ctx *ctx, const uint8_t *d_bytes, const uint64_t *d_upd_off,
+                                  const uint8_t *d_sv_bytes, const uint64_t *d_sv_off, uint64_t n_docs,
+                                  ymerge_device_result *res);
+int yencode_state_vector_from_update_v2_batch_device(ymerge_ctx *ctx, const uint8_t *d_bytes,
+                                                     const uint64_t *d_upd_off, uint64_t n_docs,
+                                                     ymerge_device_result *res);
 /* pack the last device result into host buffers: out (res->out_bytes), out_off (n_docs + 1,
  * document d at out[out_off[d] .. out_off[d+1])), status (n_docs) */
 int ymerge_result_to_host(ymerge_ctx *ctx, const ymerge_device_result *res, uint64_t n_docs, uint8_t *out,
@@ -149,6 +169,12 @@ int ysync_step1_v1_batch(ymerge_ctx *ctx, const uint8_t *bytes, const uint64_t *
                          ymerge_batch_result **res);
 int ysync_step2_v1_batch(ymerge_ctx *ctx, const uint8_t *bytes, const uint64_t *upd_off, const uint8_t *msg,
                          const uint64_t *msg_off, uint64_t n_docs, ymerge_batch_result **res);
+int ymerge_updates_v2_batch(ymerge_ctx *ctx, const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_updates,
+                            const uint64_t *doc_upd, uint64_t n_docs, ymerge_batch_result **res);
+int ydiff_updates_v2_batch(ymerge_ctx *ctx, const uint8_t *bytes, const uint64_t *upd_off, const uint8_t *sv,
+                           const uint64_t *sv_off, uint64_t n_docs, ymerge_batch_result **res);
+int yencode_state_vector_from_update_v2_batch(ymerge_ctx *ctx, const uint8_t *bytes, const uint64_t *upd_off,
+                                              uint64_t n_docs, ymerge_batch_result **res);
 void ymerge_batch_result_destroy(ymerge_batch_result *res);
 
 #ifdef __cplusplus

@@ -751,6 +751,17 @@ __device__ __noinline__ SlowRes parse_content_slow(const uint8_t *p, uint32_t n,
       bi.len = 1;
       return 0;
     }
+    case 12: case 13: { // internal (yv2.hip): lib0 v2 Embed / Format, value as Any bytes
+      if (ref == 13) {
+        YM_TRY(rd_var_u32(c, v, cn));
+        YM_TRY(rd_skip(c, v));
+      }
+      Counter cnt;
+      YM_TRY(any_walk(c, cnt, bi.reenc));
+      bi.reenc = true;
+      bi.len = 1;
+      return 0;
+    }
     default: return E_UNEXPECTED;
     }
   
@@ -1010,6 +1021,15 @@ __device__ __noinline__ int emit_block(const uint8_t *p, uint32_t n, uint32_t po
       }
     }
     return 0;
+  }
+  case 12: case 13: { // internal lib0 v2 Embed / Format (yv2.hip): key, canonical Any
+    if (ref == 13) {
+      rd_var_u32(c, v, cn);
+      w_str(w, p + c.i, v);
+      c.i += v;
+    }
+    bool r;
+    return any_walk(c, w, r);
   }
   case 8: {
     uint32_t cnt;

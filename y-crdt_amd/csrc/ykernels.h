@@ -82,6 +82,16 @@ struct DiffBatch {
 };
 // y-sync: parse one client message per document (must be Message::Sync(SyncStep1(sv)),
 // yrs/src/sync/protocol.rs:179-203, 245-272) -> SV slice [sv_off, sv_end) + status
+// lib0 v2 (yv2.hip): v2 -> v1x transcode per update, per-document status fixup, state
+// vector header parse, v1x -> v2 encode per document (mode 0 update, 1 state vector)
+void launch_v2_decode(bool write, const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_upd, uint64_t *sz_off,
+                      uint8_t *out, uint8_t *ust, hipStream_t s);
+void launch_v2_doc_status(const uint64_t *doc_upd, const uint8_t *ust, uint32_t n_docs, uint8_t *status,
+                          uint64_t *out_len, hipStream_t s);
+void launch_v2_sv_parse(const uint8_t *sv, const uint64_t *sv_off, const uint8_t *ust, uint32_t n, uint64_t *rest_off,
+                        uint64_t *rest_end, uint8_t *pre, hipStream_t s);
+void launch_v2_encode(bool write, const uint8_t *src, const uint64_t *src_start, const uint64_t *src_len,
+                      const uint8_t *status, uint32_t n_docs, uint64_t *sz_off, uint8_t *out, int mode, hipStream_t s);
 void launch_sync_parse(const uint8_t *msg, const uint64_t *msg_off, uint32_t n, uint64_t *sv_off, uint64_t *sv_end,
                        uint8_t *status, hipStream_t s);
 struct PlanCaps {

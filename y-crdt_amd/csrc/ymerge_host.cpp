@@ -54,6 +54,9 @@ struct ymerge_ctx {
   DevBuf in_bytes, in_upd_off, in_doc_upd, in_sv, in_sv_off, sync_off, sync_end, sync_st;
   DevBuf status, path, out_start, out_len, pack_off, counts, need, scr_off, scratch, sizes, spill_off, scan_tmp;
   DevBuf arena, packed, counter, stamps, plan_small, plan_big, rec, ovf, big_scratch;
+  // lib0 v2: v1x arena + offsets + per-update status, v2 output arena + sizes + offsets,
+  // state-vector rest offsets + pre-status
+  DevBuf v2x, v2x_sz, v2x_off, v2_ust, v2_out, v2_osz, v2_ooff, v2_svoff, v2_svend, v2_pre;
   bool want_stamps = false;
   uint64_t *h_pinned = nullptr;
   hipEvent_t ev[8];
@@ -104,7 +107,8 @@ extern "C" void ymerge_ctx_destroy(ymerge_ctx *c) {
                     &c->sync_end, &c->sync_st, &c->rec, &c->ovf, &c->status, &c->path,
                     &c->out_start, &c->out_len, &c->pack_off, &c->counts, &c->need, &c->scr_off, &c->scratch,
                     &c->sizes, &c->spill_off, &c->scan_tmp, &c->arena, &c->packed, &c->counter, &c->stamps,
-                    &c->plan_small, &c->plan_big, &c->big_scratch})
+                    &c->plan_small, &c->plan_big, &c->big_scratch, &c->v2x, &c->v2x_sz, &c->v2x_off, &c->v2_ust,
+                    &c->v2_out, &c->v2_osz, &c->v2_ooff, &c->v2_svoff, &c->v2_svend, &c->v2_pre})
     b->release();
   if (c->h_pinned) hipHostFree(c->h_pinned);
   for (auto &e : c->ev)
@@ -286,7 +290,7 @@ extern "C" int ymerge_updates_v1_batch_device(ymerge_ctx *c, const uint8_t *d_by
 // 2 y-sync SyncStep1 message (state vector)
 static int plan_exec(ymerge_ctx *c, bool diff, const uint8_t *d_bytes, const uint64_t *d_upd_off,
                      const uint8_t *d_sv, const uint64_t *d_sv_off, uint64_t n_docs, ymerge_device_result *res,
-                     uint32_t frame = 0) {
+                     uint32_t frame = 0, const uint64_t *sv_end = nullptr, const uint8_t *pre_status = nullptr) {
   if (hipSetDevice(c->device) != hipSuccess) return YMERGE_ERR_DEVICE;
   if (n_docs > 0xFFFFFFFFull) return YMERGE_ERR_OTHER;
   const uint32_t n = (uint32_t)n_docs;
@@ -300,6 +304,10 @@ static int plan_exec(ymerge_ctx *c, bool diff, const uint8_t *d_bytes, const uin
     b.sv_off = c->sync_off.as<uint64_t>();
     b.sv_end = c->sync_end.as<uint64_t>();
     b.pre_status = c->sync_st.as<uint8_t>();
+  }
+  if (pre_status) { // lib0 v2 front end: state-vector slices and decode statuses
+    b.sv_end = sv_end;
+    b.pre_status = pre_status;
   }
   const size_t nn = (size_t)n + 1;
   const uint64_t sw = ym::plan_small_words();
@@ -389,6 +397,108 @@ extern "C" int ydiff_updates_v1_batch_device(ymerge_ctx *c, const uint8_t *d_byt
   return plan_exec(c, true, d_bytes, d_upd_off, d_sv, d_sv_off, n_docs, res);
 }
 
+// ---------------------------------------------------------------- lib0 v2 (yv2.hip)
+// v2 updates -> v1x arena (c->v2x, offsets c->v2x_off[n_upd + 1], status c->v2_ust)
+static int v2_transcode(ymerge_ctx *c, const uint8_t *d_bytes, const uint64_t *d_upd_off, uint64_t n_upd,
+                        uint64_t *total) {
+  if (n_upd > 0xFFFFFFFFull) return YMERGE_ERR_OTHER;
+  const size_t nn = (size_t)n_upd + 1;
+  if (!c->v2x_sz.ensure(nn * 8) || !c->v2x_off.ensure(nn * 8) || !c->v2_ust.ensure(nn) ||
+      !c->scan_tmp.ensure(ym::scan_tmp_elems((uint32_t)n_upd) * 8 + 64))
+    return YMERGE_ERR_DEVICE;
+  ym::launch_v2_decode(false, d_bytes, d_upd_off, n_upd, c->v2x_sz.as<uint64_t>(), nullptr, c->v2_ust.as<uint8_t>(),
+                       c->s);
+  ym::launch_scan_u64(c->v2x_sz.as<uint64_t>(), c->v2x_off.as<uint64_t>(), (uint32_t)n_upd,
+                      c->scan_tmp.as<uint64_t>(), c->s);
+  if (!read_words(c, c->v2x_off.as<uint64_t>() + n_upd, 8, total)) return YMERGE_ERR_DEVICE;
+  if (!c->v2x.ensure(*total + 64)) return YMERGE_ERR_DEVICE;
+  ym::launch_v2_decode(true, d_bytes, d_upd_off, n_upd, c->v2x_off.as<uint64_t>(), c->v2x.as<uint8_t>(),
+                       c->v2_ust.as<uint8_t>(), c->s);
+  return hipGetLastError() == hipSuccess ? 0 : YMERGE_ERR_DEVICE;
+}
+// v1x result -> v2 (mode 0 update, 1 state vector) in c->v2_out; `res` then describes it
+static int v2_encode(ymerge_ctx *c, ymerge_device_result *res, uint32_t n, int mode) {
+  const size_t nn = (size_t)n + 1;
+  if (!c->v2_osz.ensure(nn * 8) || !c->v2_ooff.ensure(nn * 8) || !c->pack_off.ensure(nn * 8) ||
+      !c->scan_tmp.ensure(ym::scan_tmp_elems(n) * 8 + 64))
+    return YMERGE_ERR_DEVICE;
+  ym::launch_v2_encode(false, res->d_out, res->d_out_start, res->d_out_len, res->d_status, n,
+                       c->v2_osz.as<uint64_t>(), nullptr, mode, c->s);
+  ym::launch_scan_u64(c->v2_osz.as<uint64_t>(), c->v2_ooff.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
+  uint64_t total = 0;
+  if (!read_words(c, c->v2_ooff.as<uint64_t>() + n, 8, &total)) return YMERGE_ERR_DEVICE;
+  if (!c->v2_out.ensure(total + 64)) return YMERGE_ERR_DEVICE;
+  ym::launch_v2_encode(true, res->d_out, res->d_out_start, res->d_out_len, res->d_status, n,
+                       c->v2_ooff.as<uint64_t>(), c->v2_out.as<uint8_t>(), mode, c->s);
+  // packed offsets of the result (pack_to_host copies the arena in their order)
+  if (hipMemcpyAsync(c->pack_off.p, c->v2_ooff.p, nn * 8, hipMemcpyDeviceToDevice, c->s) != hipSuccess)
+    return YMERGE_ERR_DEVICE;
+  if (hipStreamSynchronize(c->s) != hipSuccess || hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
+  res->d_out = c->v2_out.as<uint8_t>();
+  res->d_out_start = c->v2_ooff.as<uint64_t>();
+  res->d_out_len = c->v2_osz.as<uint64_t>();
+  res->arena_bytes = c->v2_out.cap;
+  res->out_bytes = total;
+  return 0;
+}
+static int merge_v2_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes, const uint64_t *d_upd_off,
+                           uint64_t n_updates, const uint64_t *d_doc_upd, uint64_t n_docs, ymerge_device_result *res) {
+  if (hipSetDevice(c->device) != hipSuccess) return YMERGE_ERR_DEVICE;
+  if (n_docs > 0xFFFFFFFFull) return YMERGE_ERR_OTHER;
+  uint64_t xbytes = 0;
+  int st = v2_transcode(c, d_bytes, d_upd_off, n_updates, &xbytes);
+  if (st) return st;
+  st = merge_device(c, c->v2x.as<uint8_t>(), xbytes, c->v2x_off.as<uint64_t>(), n_updates, d_doc_upd, n_docs, res);
+  if (st) return st;
+  ym::launch_v2_doc_status(d_doc_upd, c->v2_ust.as<uint8_t>(), (uint32_t)n_docs, res->d_status,
+                           (uint64_t *)res->d_out_len, c->s);
+  st = v2_encode(c, res, (uint32_t)n_docs, 0);
+  c->stats.bytes_in = n_bytes;
+  c->stats.bytes_out = res->out_bytes;
+  return st;
+}
+// diff_updates_v2 (diff = true) / encode_state_vector_from_update_v2: one update per document
+static int plan_v2_device(ymerge_ctx *c, bool diff, const uint8_t *d_bytes, const uint64_t *d_upd_off,
+                          const uint8_t *d_sv, const uint64_t *d_sv_off, uint64_t n_docs, ymerge_device_result *res) {
+  if (hipSetDevice(c->device) != hipSuccess) return YMERGE_ERR_DEVICE;
+  if (n_docs > 0xFFFFFFFFull) return YMERGE_ERR_OTHER;
+  const uint32_t n = (uint32_t)n_docs;
+  uint64_t xbytes = 0;
+  int st = v2_transcode(c, d_bytes, d_upd_off, n_docs, &xbytes);
+  if (st) return st;
+  if (!c->v2_svoff.ensure((n + 1) * 8) || !c->v2_svend.ensure((n + 1) * 8) || !c->v2_pre.ensure(n + 1))
+    return YMERGE_ERR_DEVICE;
+  ym::launch_v2_sv_parse(diff ? d_sv : nullptr, d_sv_off, c->v2_ust.as<uint8_t>(), n, c->v2_svoff.as<uint64_t>(),
+                         c->v2_svend.as<uint64_t>(), c->v2_pre.as<uint8_t>(), c->s);
+  st = plan_exec(c, diff, c->v2x.as<uint8_t>(), c->v2x_off.as<uint64_t>(), d_sv,
+                 diff ? c->v2_svoff.as<uint64_t>() : nullptr, n_docs, res, 0,
+                 diff ? c->v2_svend.as<uint64_t>() : nullptr, c->v2_pre.as<uint8_t>());
+  if (st) return st;
+  return v2_encode(c, res, n, diff ? 0 : 1);
+}
+
+extern "C" int ymerge_updates_v2_batch_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
+                                              const uint64_t *d_upd_off, uint64_t n_updates, const uint64_t *d_doc_upd,
+                                              uint64_t n_docs, ymerge_device_result *res) {
+  if (!c || !res) return YMERGE_ERR_OTHER;
+  std::lock_guard<std::mutex> g(c->mu);
+  return merge_v2_device(c, d_bytes, n_bytes, d_upd_off, n_updates, d_doc_upd, n_docs, res);
+}
+extern "C" int ydiff_updates_v2_batch_device(ymerge_ctx *c, const uint8_t *d_bytes, const uint64_t *d_upd_off,
+                                             const uint8_t *d_sv, const uint64_t *d_sv_off, uint64_t n_docs,
+                                             ymerge_device_result *res) {
+  if (!c || !res) return YMERGE_ERR_OTHER;
+  std::lock_guard<std::mutex> g(c->mu);
+  return plan_v2_device(c, true, d_bytes, d_upd_off, d_sv, d_sv_off, n_docs, res);
+}
+extern "C" int yencode_state_vector_from_update_v2_batch_device(ymerge_ctx *c, const uint8_t *d_bytes,
+                                                                const uint64_t *d_upd_off, uint64_t n_docs,
+                                                                ymerge_device_result *res) {
+  if (!c || !res) return YMERGE_ERR_OTHER;
+  std::lock_guard<std::mutex> g(c->mu);
+  return plan_v2_device(c, false, d_bytes, d_upd_off, nullptr, nullptr, n_docs, res);
+}
+
 static int pack_to_host(ymerge_ctx *c, const ymerge_device_result *res, uint64_t n_docs, uint8_t *out,
                         uint64_t *out_off, uint8_t *status) {
   const uint32_t n = (uint32_t)n_docs;
@@ -431,9 +541,20 @@ extern "C" void ymerge_last_stats(ymerge_ctx *c, ymerge_stats *st) {
   *st = c->stats;
 }
 
+static int host_merge(ymerge_ctx *c, int version, const uint8_t *bytes, const uint64_t *upd_off,
+                      uint64_t n_updates, const uint64_t *doc_upd, uint64_t n_docs, ymerge_batch_result **out);
 extern "C" int ymerge_updates_v1_batch(ymerge_ctx *c, const uint8_t *bytes, const uint64_t *upd_off,
                                        uint64_t n_updates, const uint64_t *doc_upd, uint64_t n_docs,
                                        ymerge_batch_result **out) {
+  return host_merge(c, 1, bytes, upd_off, n_updates, doc_upd, n_docs, out);
+}
+extern "C" int ymerge_updates_v2_batch(ymerge_ctx *c, const uint8_t *bytes, const uint64_t *upd_off,
+                                       uint64_t n_updates, const uint64_t *doc_upd, uint64_t n_docs,
+                                       ymerge_batch_result **out) {
+  return host_merge(c, 2, bytes, upd_off, n_updates, doc_upd, n_docs, out);
+}
+static int host_merge(ymerge_ctx *c, int version, const uint8_t *bytes, const uint64_t *upd_off,
+                      uint64_t n_updates, const uint64_t *doc_upd, uint64_t n_docs, ymerge_batch_result **out) {
   if (!c || !out) return YMERGE_ERR_OTHER;
   std::lock_guard<std::mutex> g(c->mu);
   hipSetDevice(c->device);
@@ -447,8 +568,9 @@ extern "C" int ymerge_updates_v1_batch(ymerge_ctx *c, const uint8_t *bytes, cons
       hipMemcpyAsync(c->in_doc_upd.p, doc_upd, (n_docs + 1) * 8, hipMemcpyHostToDevice, c->s) != hipSuccess)
     return YMERGE_ERR_DEVICE;
   ymerge_device_result dr{};
-  int st = merge_device(c, c->in_bytes.as<uint8_t>(), nbytes, c->in_upd_off.as<uint64_t>(), n_updates,
-                        c->in_doc_upd.as<uint64_t>(), n_docs, &dr);
+  int st = (version == 2 ? merge_v2_device : merge_device)(c, c->in_bytes.as<uint8_t>(), nbytes,
+                                                           c->in_upd_off.as<uint64_t>(), n_updates,
+                                                           c->in_doc_upd.as<uint64_t>(), n_docs, &dr);
   if (st) return st;
   ymerge_batch_result *r = alloc_result(n_docs, dr.out_bytes);
   if (!r) return YMERGE_ERR_NOT_ENOUGH_MEMORY;
@@ -560,7 +682,7 @@ extern "C" char *ymerge_updates_v1(const char *const *updates, const uint32_t *u
 // host buffers of one (or more) documents -> device -> plan/exec -> host
 static int host_plan_exec(ymerge_ctx *c, bool diff, const uint8_t *bytes, const uint64_t *upd_off,
                           const uint8_t *sv, const uint64_t *sv_off, uint64_t n_docs, ymerge_batch_result **out,
-                          uint32_t frame = 0) {
+                          uint32_t frame = 0, int version = 1) {
   std::lock_guard<std::mutex> g(c->mu);
   hipSetDevice(c->device);
   const uint64_t nbytes = upd_off[n_docs], nsv = diff ? sv_off[n_docs] : 0;
@@ -577,9 +699,13 @@ static int host_plan_exec(ymerge_ctx *c, bool diff, const uint8_t *bytes, const 
       return YMERGE_ERR_DEVICE;
   }
   ymerge_device_result dr{};
-  int st = plan_exec(c, diff, c->in_bytes.as<uint8_t>(), c->in_upd_off.as<uint64_t>(),
-                     diff ? c->in_sv.as<uint8_t>() : nullptr, diff ? c->in_sv_off.as<uint64_t>() : nullptr, n_docs,
-                     &dr, frame);
+  int st = version == 2
+               ? plan_v2_device(c, diff, c->in_bytes.as<uint8_t>(), c->in_upd_off.as<uint64_t>(),
+                                diff ? c->in_sv.as<uint8_t>() : nullptr, diff ? c->in_sv_off.as<uint64_t>() : nullptr,
+                                n_docs, &dr)
+               : plan_exec(c, diff, c->in_bytes.as<uint8_t>(), c->in_upd_off.as<uint64_t>(),
+                           diff ? c->in_sv.as<uint8_t>() : nullptr, diff ? c->in_sv_off.as<uint64_t>() : nullptr,
+                           n_docs, &dr, frame);
   if (st) return st;
   ymerge_batch_result *r = alloc_result(n_docs, dr.out_bytes);
   if (!r) return YMERGE_ERR_NOT_ENOUGH_MEMORY;
@@ -597,6 +723,18 @@ extern "C" int ydiff_updates_v1_batch(ymerge_ctx *c, const uint8_t *bytes, const
                                       ymerge_batch_result **res) {
   if (!c || !res) return YMERGE_ERR_OTHER;
   return host_plan_exec(c, true, bytes, upd_off, sv, sv_off, n_docs, res);
+}
+extern "C" int ydiff_updates_v2_batch(ymerge_ctx *c, const uint8_t *bytes, const uint64_t *upd_off,
+                                      const uint8_t *sv, const uint64_t *sv_off, uint64_t n_docs,
+                                      ymerge_batch_result **res) {
+  if (!c || !res) return YMERGE_ERR_OTHER;
+  return host_plan_exec(c, true, bytes, upd_off, sv, sv_off, n_docs, res, 0, 2);
+}
+extern "C" int yencode_state_vector_from_update_v2_batch(ymerge_ctx *c, const uint8_t *bytes,
+                                                         const uint64_t *upd_off, uint64_t n_docs,
+                                                         ymerge_batch_result **res) {
+  if (!c || !res) return YMERGE_ERR_OTHER;
+  return host_plan_exec(c, false, bytes, upd_off, nullptr, nullptr, n_docs, res, 0, 2);
 }
 extern "C" int ysync_step1_v1_batch(ymerge_ctx *c, const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_docs,
                                     ymerge_batch_result **res) {
@@ -661,6 +799,68 @@ extern "C" char *yencode_state_vector_from_update_v1(const char *update, uint32_
   const uint64_t uo[2] = {0, update_len};
   ymerge_batch_result *r = nullptr;
   int st = yencode_state_vector_from_update_v1_batch(c, (const uint8_t *)update, uo, 1, &r);
+  if (st) {
+    g_last_error = (uint8_t)st;
+    return nullptr;
+  }
+  return single_result(r, out_len);
+}
+
+// ---------------------------------------------------------------- single document, lib0 v2
+extern "C" char *ymerge_updates_v2(const char *const *updates, const uint32_t *updates_len, uint32_t updates_count,
+                                   uint32_t *out_len) {
+  g_last_error = 0;
+  ymerge_ctx *c = default_ctx();
+  if (!c) {
+    g_last_error = YMERGE_ERR_DEVICE;
+    return nullptr;
+  }
+  std::vector<uint64_t> off(updates_count + 1);
+  uint64_t tot = 0;
+  for (uint32_t i = 0; i < updates_count; i++) {
+    off[i] = tot;
+    tot += updates_len[i];
+  }
+  off[updates_count] = tot;
+  std::vector<uint8_t> arena(tot + 1);
+  for (uint32_t i = 0; i < updates_count; i++)
+    if (updates_len[i]) memcpy(arena.data() + off[i], updates[i], updates_len[i]);
+  const uint64_t doc_upd[2] = {0, updates_count};
+  ymerge_batch_result *r = nullptr;
+  const int st = ymerge_updates_v2_batch(c, arena.data(), off.data(), updates_count, doc_upd, 1, &r);
+  if (st) {
+    g_last_error = (uint8_t)st;
+    return nullptr;
+  }
+  return single_result(r, out_len);
+}
+extern "C" char *ydiff_updates_v2(const char *update, uint32_t update_len, const char *state_vector,
+                                  uint32_t sv_len, uint32_t *out_len) {
+  g_last_error = 0;
+  ymerge_ctx *c = default_ctx();
+  if (!c) {
+    g_last_error = YMERGE_ERR_DEVICE;
+    return nullptr;
+  }
+  const uint64_t uo[2] = {0, update_len}, so[2] = {0, sv_len};
+  ymerge_batch_result *r = nullptr;
+  const int st = ydiff_updates_v2_batch(c, (const uint8_t *)update, uo, (const uint8_t *)state_vector, so, 1, &r);
+  if (st) {
+    g_last_error = (uint8_t)st;
+    return nullptr;
+  }
+  return single_result(r, out_len);
+}
+extern "C" char *yencode_state_vector_from_update_v2(const char *update, uint32_t update_len, uint32_t *out_len) {
+  g_last_error = 0;
+  ymerge_ctx *c = default_ctx();
+  if (!c) {
+    g_last_error = YMERGE_ERR_DEVICE;
+    return nullptr;
+  }
+  const uint64_t uo[2] = {0, update_len};
+  ymerge_batch_result *r = nullptr;
+  const int st = yencode_state_vector_from_update_v2_batch(c, (const uint8_t *)update, uo, 1, &r);
   if (st) {
     g_last_error = (uint8_t)st;
     return nullptr;

@@ -4,6 +4,8 @@ Same names, argument meaning and error behaviour as yrs/src/alt.rs:
     merge_updates_v1(updates)                 -> bytes   (alt.rs:15-28)
     diff_updates_v1(update, state_vector)     -> bytes   (alt.rs:73-81)
     encode_state_vector_from_update_v1(update)-> bytes   (alt.rs:54-57)
+and their lib0 v2 forms merge_updates_v2 / diff_updates_v2 /
+encode_state_vector_from_update_v2 (alt.rs:35-48, 88-97, 63-66).
 A decode failure raises YrsError carrying yffi's error code (yffi/src/lib.rs:1137-1174).
 
 `Engine` is the batched, multi-tenant entry point (one HIP stream per device).
@@ -76,6 +78,16 @@ def lib():
     L.ydiff_updates_v1.argtypes = [c.c_char_p, u32, c.c_char_p, u32, c.POINTER(u32)]
     L.yencode_state_vector_from_update_v1.restype = vp
     L.yencode_state_vector_from_update_v1.argtypes = [c.c_char_p, u32, c.POINTER(u32)]
+    for v in ("v1", "v2"):
+        getattr(L, f"ymerge_updates_{v}").restype = vp
+        getattr(L, f"ymerge_updates_{v}").argtypes = [c.POINTER(c.c_char_p), c.POINTER(u32), u32, c.POINTER(u32)]
+        getattr(L, f"ydiff_updates_{v}").restype = vp
+        getattr(L, f"ydiff_updates_{v}").argtypes = [c.c_char_p, u32, c.c_char_p, u32, c.POINTER(u32)]
+        getattr(L, f"yencode_state_vector_from_update_{v}").restype = vp
+        getattr(L, f"yencode_state_vector_from_update_{v}").argtypes = [c.c_char_p, u32, c.POINTER(u32)]
+    L.ymerge_updates_v2_batch_device.argtypes = [vp, vp, u64, vp, u64, vp, u64, c.POINTER(_DevRes)]
+    L.ydiff_updates_v2_batch_device.argtypes = [vp, vp, vp, vp, vp, u64, c.POINTER(_DevRes)]
+    L.yencode_state_vector_from_update_v2_batch_device.argtypes = [vp, vp, vp, u64, c.POINTER(_DevRes)]
     L.ymerge_binary_destroy.argtypes = [vp, u32]
     L.ymerge_set_default_device.argtypes = [c.c_int]
     L.ymerge_last_error.restype = c.c_uint8
@@ -126,6 +138,29 @@ def encode_state_vector_from_update_v1(update):
     return _take(lib().yencode_state_vector_from_update_v1(u, len(u), ctypes.byref(n)), n)
 
 
+def merge_updates_v2(updates):
+    """yrs::merge_updates_v2 (alt.rs:35)."""
+    ups = [bytes(u) for u in updates]
+    arr = (ctypes.c_char_p * max(1, len(ups)))(*ups)
+    lens = (ctypes.c_uint32 * max(1, len(ups)))(*[len(u) for u in ups])
+    n = ctypes.c_uint32()
+    return _take(lib().ymerge_updates_v2(arr, lens, len(ups), ctypes.byref(n)), n)
+
+
+def diff_updates_v2(update, state_vector):
+    """yrs::diff_updates_v2 (alt.rs:88)."""
+    n = ctypes.c_uint32()
+    u, s = bytes(update), bytes(state_vector)
+    return _take(lib().ydiff_updates_v2(u, len(u), s, len(s), ctypes.byref(n)), n)
+
+
+def encode_state_vector_from_update_v2(update):
+    """yrs::encode_state_vector_from_update_v2 (alt.rs:63)."""
+    n = ctypes.c_uint32()
+    u = bytes(update)
+    return _take(lib().yencode_state_vector_from_update_v2(u, len(u), ctypes.byref(n)), n)
+
+
 class DeviceResult:
     def __init__(self, engine, res, n_docs):
         self.engine, self.res, self.n_docs = engine, res, n_docs
@@ -166,19 +201,19 @@ class Engine:
         except Exception:
             pass
 
-    def merge_device(self, d_bytes, n_bytes, d_upd_off, n_updates, d_doc_upd, n_docs):
-        """Inputs are device pointers (ints) into HBM; returns a DeviceResult."""
+    def merge_device(self, d_bytes, n_bytes, d_upd_off, n_updates, d_doc_upd, n_docs, version=1):
+        """Inputs are device pointers (ints) into HBM; returns a DeviceResult.  version 2 = lib0 v2."""
         res = _DevRes()
-        rc = lib().ymerge_updates_v1_batch_device(self._ctx, d_bytes, n_bytes, d_upd_off, n_updates, d_doc_upd,
-                                                  n_docs, ctypes.byref(res))
+        fn = lib().ymerge_updates_v2_batch_device if version == 2 else lib().ymerge_updates_v1_batch_device
+        rc = fn(self._ctx, d_bytes, n_bytes, d_upd_off, n_updates, d_doc_upd, n_docs, ctypes.byref(res))
         if rc:
             raise DeviceError(f"merge batch failed ({rc})")
         return DeviceResult(self, res, n_docs)
 
-    def diff_device(self, d_bytes, d_upd_off, d_sv, d_sv_off, n_docs):
+    def diff_device(self, d_bytes, d_upd_off, d_sv, d_sv_off, n_docs, version=1):
         res = _DevRes()
-        rc = lib().ydiff_updates_v1_batch_device(self._ctx, d_bytes, d_upd_off, d_sv, d_sv_off, n_docs,
-                                                 ctypes.byref(res))
+        fn = lib().ydiff_updates_v2_batch_device if version == 2 else lib().ydiff_updates_v1_batch_device
+        rc = fn(self._ctx, d_bytes, d_upd_off, d_sv, d_sv_off, n_docs, ctypes.byref(res))
         if rc:
             raise DeviceError(f"diff batch failed ({rc})")
         return DeviceResult(self, res, n_docs)
@@ -213,10 +248,11 @@ class Engine:
         args = [ub if len(ub) else np.zeros(1, np.uint8), np.asarray(u_off, np.uint64).view(np.int64)]
         return self._host_batch(args, lambda a, b: self.sync_step1_device(a, b, n))
 
-    def state_vector_device(self, d_bytes, d_upd_off, n_docs):
+    def state_vector_device(self, d_bytes, d_upd_off, n_docs, version=1):
         res = _DevRes()
-        rc = lib().yencode_state_vector_from_update_v1_batch_device(self._ctx, d_bytes, d_upd_off, n_docs,
-                                                                    ctypes.byref(res))
+        fn = (lib().yencode_state_vector_from_update_v2_batch_device if version == 2
+              else lib().yencode_state_vector_from_update_v1_batch_device)
+        rc = fn(self._ctx, d_bytes, d_upd_off, n_docs, ctypes.byref(res))
         if rc:
             raise DeviceError(f"state-vector batch failed ({rc})")
         return DeviceResult(self, res, n_docs)
@@ -235,24 +271,24 @@ class Engine:
         r = fn(*[t.data_ptr() for t in ts])
         return r.to_host()
 
-    def diff_host(self, ubytes, u_off, svbytes, sv_off):
-        """Batched diff_updates_v1: document d = (update d, remote state vector d)."""
+    def diff_host(self, ubytes, u_off, svbytes, sv_off, version=1):
+        """Batched diff_updates_v1 (v2): document d = (update d, remote state vector d)."""
         n = len(u_off) - 1
         ub = np.ascontiguousarray(ubytes, dtype=np.uint8)
         sb = np.ascontiguousarray(svbytes, dtype=np.uint8)
         args = [ub if len(ub) else np.zeros(1, np.uint8), np.asarray(u_off, np.uint64).view(np.int64),
                 sb if len(sb) else np.zeros(1, np.uint8), np.asarray(sv_off, np.uint64).view(np.int64)]
-        return self._host_batch(args, lambda a, b, c, d: self.diff_device(a, b, c, d, n))
+        return self._host_batch(args, lambda a, b, c, d: self.diff_device(a, b, c, d, n, version))
 
-    def state_vector_host(self, ubytes, u_off):
-        """Batched encode_state_vector_from_update_v1 (one update per document)."""
+    def state_vector_host(self, ubytes, u_off, version=1):
+        """Batched encode_state_vector_from_update_v1 (v2) (one update per document)."""
         n = len(u_off) - 1
         ub = np.ascontiguousarray(ubytes, dtype=np.uint8)
         args = [ub if len(ub) else np.zeros(1, np.uint8), np.asarray(u_off, np.uint64).view(np.int64)]
-        return self._host_batch(args, lambda a, b: self.state_vector_device(a, b, n))
+        return self._host_batch(args, lambda a, b: self.state_vector_device(a, b, n, version))
 
     # convenience: host arrays in, host arrays out (uses torch for HBM residency)
-    def merge_host(self, data, upd_off, doc_upd):
+    def merge_host(self, data, upd_off, doc_upd, version=1):
         import torch
         dev = torch.device("cuda", self.device)
         t_b = torch.from_numpy(padded(data)).to(dev)
@@ -260,5 +296,5 @@ class Engine:
         t_d = torch.from_numpy(np.ascontiguousarray(doc_upd, dtype=np.uint64).view(np.int64)).to(dev)
         torch.cuda.synchronize(dev)
         r = self.merge_device(t_b.data_ptr(), int(upd_off[-1]), t_u.data_ptr(), len(upd_off) - 1, t_d.data_ptr(),
-                              len(doc_upd) - 1)
+                              len(doc_upd) - 1, version)
         return r.to_host()
