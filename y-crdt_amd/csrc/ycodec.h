@@ -633,6 +633,16 @@ struct SlowRes {
   uint32_t pos, len;
   bool reenc, unsupported;
 };
+// Content refs 12 / 13 exist only in the engine's internal v1x grammar (yv2.hip: lib0 v2
+// Embed / Format with Any values); in lib0 v1 input they are ItemContent::decode's
+// UnexpectedValue (yrs/src/block.rs:1786-1835).  Every kernel that parses content states its
+// batch's grammar first with ym_set_grammar (from every lane, before any parse: no barrier
+// needed); a kernel that never set it reads garbage, which is not the magic: v1 behaviour.
+static __shared__ uint32_t s_grammar_v1x;
+constexpr uint32_t GRAMMAR_V1X_MAGIC = 0x76317821u;
+YM_INLINE void ym_set_grammar(uint32_t v1x) { s_grammar_v1x = v1x ? GRAMMAR_V1X_MAGIC : 0u; }
+YM_INLINE bool ym_grammar_v1x() { return s_grammar_v1x == GRAMMAR_V1X_MAGIC; }
+
 __device__ __noinline__ SlowRes parse_content_slow(const uint8_t *p, uint32_t n, uint32_t pos, uint8_t ref,
                                                    bool reenc_in) {
   Cur c{p, n, pos};
@@ -752,6 +762,7 @@ __device__ __noinline__ SlowRes parse_content_slow(const uint8_t *p, uint32_t n,
       return 0;
     }
     case 12: case 13: { // internal (yv2.hip): lib0 v2 Embed / Format, value as Any bytes
+      if (!ym_grammar_v1x()) return E_UNEXPECTED;
       if (ref == 13) {
         YM_TRY(rd_var_u32(c, v, cn));
         YM_TRY(rd_skip(c, v));

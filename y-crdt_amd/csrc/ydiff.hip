@@ -146,6 +146,103 @@ __device__ __forceinline__ uint32_t vars_size(uint32_t k, uint32_t a, uint32_t b
   return s;
 }
 
+// The output plan of a fully walked document (shared by plan_doc and the ring planner):
+// ops for encode_diff (clients descending, DeleteSet in table order) or the state vector.
+template <bool DIFF>
+__device__ __noinline__ uint32_t plan_finish(uint32_t *scr, const PlanLayout &L, const PlanCaps &cap, GHB &ct,
+                                             uint32_t nsec, GHB &dt, bool unsupported, uint32_t pending,
+                                             uint64_t &out_size) {
+  const uint32_t *cl = scr + L.cl, *sec = scr + L.sec, *de = scr + L.de;
+  OpW ow{scr + L.ops, 0, cap.O};
+  uint64_t total = 0;
+  if (DIFF) {
+    if (unsupported) return E_UNSUPPORTED;
+    if (pending) return pending;
+    // clients with content, descending (encode_diff sorts by client id)
+    uint32_t *ord = scr + L.ct_tmp;
+    uint32_t nf = 0;
+    for (uint32_t e = 0; e < ct.items; e++)
+      if (cl[CLW * e + 5]) {
+        const uint32_t k = ct.keys[e];
+        uint32_t j = nf++;
+        while (j > 0 && ct.keys[ord[j - 1]] < k) {
+          ord[j] = ord[j - 1];
+          j--;
+        }
+        ord[j] = e;
+      }
+    if (!ow.put(OP_VARS, varlen(nf), 1, nf)) return PLAN_OVF;
+    total += varlen(nf);
+    for (uint32_t q = 0; q < nf; q++) {
+      const uint32_t e = ord[q];
+      const uint32_t *st = cl + CLW * e;
+      const uint32_t client = ct.keys[e];
+      const uint32_t hclock = st[7] + st[9];
+      uint32_t hs = vars_size(3, st[10], client, hclock);
+      if (!ow.put(OP_VARS, hs, 3, st[10], client, hclock)) return PLAN_OVF;
+      if (!ow.put(OP_EMIT, st[11], st[6], st[7], st[8], st[9], client)) return PLAN_OVF;
+      total += hs + st[11];
+      for (uint32_t s = 0; s < nsec; s++) {
+        const uint32_t *sr = sec + SECW * s;
+        if (sr[0] != e || sr[1] >= sr[2]) continue;
+        bool ok = sr[3] ? ow.put(OP_COPY, sr[2] - sr[1], sr[1]) : ow.put(OP_WALK, sr[4], sr[1], sr[2], 0, 0, client);
+        if (!ok) return PLAN_OVF;
+        total += sr[3] ? sr[2] - sr[1] : sr[4];
+      }
+    }
+    // DeleteSet in table order
+    if (!ow.put(OP_VARS, varlen(dt.items), 1, dt.items)) return PLAN_OVF;
+    total += varlen(dt.items);
+    for (uint32_t s = 0; s < dt.buckets; s++) {
+      if (!dt.slot[s]) continue;
+      const uint32_t *r = de + DEW * (dt.slot[s] - 1);
+      const uint32_t vs = varlen(r[0]);
+      bool ok = ow.put(OP_VARS, vs, 1, r[0]);
+      if (r[4] & 1) {
+        ok = ok && ((r[4] & 2) ? ow.put(OP_COPY, r[2] - r[1], r[1]) : ow.put(OP_DSS, r[7] - vs, r[1], r[3]));
+      } else {
+        ok = ok && ow.put(OP_DSQ, r[7] - vs, r[5], r[6]);
+      }
+      if (!ok) return PLAN_OVF;
+      total += r[7];
+    }
+  } else {
+    // Update::state_vector: iterate the decoded client table, set_max into a fresh table
+    GHB s2{scr + L.s2_slot, scr + L.s2_keys, L.BC, 0, 0, 0};
+    uint32_t *val = scr + L.s2_val;
+    for (uint32_t s = 0; s < ct.buckets; s++) {
+      if (!ct.slot[s]) continue;
+      const uint32_t e = ct.slot[s] - 1;
+      const uint32_t *st = cl + CLW * e;
+      if (st[0] == 0) return E_PANIC; // blocks[blocks.len() - 1] on an empty deque
+      // last_id().clock + 1: Item -> clock + len; GC / Skip -> clock + len + 1 (block.rs:1150-1152)
+      const uint32_t v = st[2] + st[3] + ((st[1] & 0xFF) != BK_ITEM ? 1u : 0u);
+      const uint32_t key = ct.keys[e];
+      int f = s2.find(key);
+      if (f < 0) {
+        f = (int)s2.items;
+        if (!s2.reserve(1, scr + L.s2_tmp)) return PLAN_OVF;
+        s2.place(key, (uint32_t)f);
+        val[f] = 0;
+      }
+      if (v > val[f]) val[f] = v;
+    }
+    if (!ow.put(OP_VARS, varlen(s2.items), 1, s2.items)) return PLAN_OVF;
+    total += varlen(s2.items);
+    for (uint32_t s = 0; s < s2.buckets; s++) {
+      if (!s2.slot[s]) continue;
+      const uint32_t e = s2.slot[s] - 1;
+      const uint32_t k = s2.keys[e], v = val[e];
+      const uint32_t sz = varlen(k) + varlen(v);
+      if (!ow.put(OP_VARS, sz, 2, k, v)) return PLAN_OVF;
+      total += sz;
+    }
+  }
+  scr[0] = ow.n;
+  out_size = total;
+  return 0;
+}
+
 // Plans one document.  Returns PLAN_OVF when the scratch capacities are exceeded (the
 // document is re-planned with big capacities), otherwise the yrs status (0 = ok).
 template <bool DIFF>
@@ -277,6 +374,7 @@ __device__ uint32_t plan_doc(const uint8_t *up, uint32_t un, const uint8_t *svp,
     uint32_t prev_e = 0, sz = varlen(n);
     for (uint32_t k = 0; k < n; k++) {
       uint32_t s0, ln;
+      wc_ensure(c, 20);
       YM_TRY(wc_var_u32(c, s0, cn));
       canon &= cn;
       YM_TRY(wc_var_u32(c, ln, cn));
@@ -346,95 +444,7 @@ __device__ uint32_t plan_doc(const uint8_t *up, uint32_t un, const uint8_t *svp,
     }
     r[7] = varlen(client) + sz;
   }
-  // ---- output plan
-  OpW ow{scr + L.ops, 0, cap.O};
-  uint64_t total = 0;
-  if (DIFF) {
-    if (unsupported) return E_UNSUPPORTED;
-    if (pending) return pending;
-    // clients with content, descending (encode_diff sorts by client id)
-    uint32_t *ord = scr + L.ct_tmp;
-    uint32_t nf = 0;
-    for (uint32_t e = 0; e < ct.items; e++)
-      if (cl[CLW * e + 5]) {
-        const uint32_t k = ct.keys[e];
-        uint32_t j = nf++;
-        while (j > 0 && ct.keys[ord[j - 1]] < k) {
-          ord[j] = ord[j - 1];
-          j--;
-        }
-        ord[j] = e;
-      }
-    if (!ow.put(OP_VARS, varlen(nf), 1, nf)) return PLAN_OVF;
-    total += varlen(nf);
-    for (uint32_t q = 0; q < nf; q++) {
-      const uint32_t e = ord[q];
-      const uint32_t *st = cl + CLW * e;
-      const uint32_t client = ct.keys[e];
-      const uint32_t hclock = st[7] + st[9];
-      uint32_t hs = vars_size(3, st[10], client, hclock);
-      if (!ow.put(OP_VARS, hs, 3, st[10], client, hclock)) return PLAN_OVF;
-      if (!ow.put(OP_EMIT, st[11], st[6], st[7], st[8], st[9], client)) return PLAN_OVF;
-      total += hs + st[11];
-      for (uint32_t s = 0; s < nsec; s++) {
-        const uint32_t *sr = sec + SECW * s;
-        if (sr[0] != e || sr[1] >= sr[2]) continue;
-        bool ok = sr[3] ? ow.put(OP_COPY, sr[2] - sr[1], sr[1]) : ow.put(OP_WALK, sr[4], sr[1], sr[2], 0, 0, client);
-        if (!ok) return PLAN_OVF;
-        total += sr[3] ? sr[2] - sr[1] : sr[4];
-      }
-    }
-    // DeleteSet in table order
-    if (!ow.put(OP_VARS, varlen(dt.items), 1, dt.items)) return PLAN_OVF;
-    total += varlen(dt.items);
-    for (uint32_t s = 0; s < dt.buckets; s++) {
-      if (!dt.slot[s]) continue;
-      const uint32_t *r = de + DEW * (dt.slot[s] - 1);
-      const uint32_t vs = varlen(r[0]);
-      bool ok = ow.put(OP_VARS, vs, 1, r[0]);
-      if (r[4] & 1) {
-        ok = ok && ((r[4] & 2) ? ow.put(OP_COPY, r[2] - r[1], r[1]) : ow.put(OP_DSS, r[7] - vs, r[1], r[3]));
-      } else {
-        ok = ok && ow.put(OP_DSQ, r[7] - vs, r[5], r[6]);
-      }
-      if (!ok) return PLAN_OVF;
-      total += r[7];
-    }
-  } else {
-    // Update::state_vector: iterate the decoded client table, set_max into a fresh table
-    GHB s2{scr + L.s2_slot, scr + L.s2_keys, L.BC, 0, 0, 0};
-    uint32_t *val = scr + L.s2_val;
-    for (uint32_t s = 0; s < ct.buckets; s++) {
-      if (!ct.slot[s]) continue;
-      const uint32_t e = ct.slot[s] - 1;
-      const uint32_t *st = cl + CLW * e;
-      if (st[0] == 0) return E_PANIC; // blocks[blocks.len() - 1] on an empty deque
-      // last_id().clock + 1: Item -> clock + len; GC / Skip -> clock + len + 1 (block.rs:1150-1152)
-      const uint32_t v = st[2] + st[3] + ((st[1] & 0xFF) != BK_ITEM ? 1u : 0u);
-      const uint32_t key = ct.keys[e];
-      int f = s2.find(key);
-      if (f < 0) {
-        f = (int)s2.items;
-        if (!s2.reserve(1, scr + L.s2_tmp)) return PLAN_OVF;
-        s2.place(key, (uint32_t)f);
-        val[f] = 0;
-      }
-      if (v > val[f]) val[f] = v;
-    }
-    if (!ow.put(OP_VARS, varlen(s2.items), 1, s2.items)) return PLAN_OVF;
-    total += varlen(s2.items);
-    for (uint32_t s = 0; s < s2.buckets; s++) {
-      if (!s2.slot[s]) continue;
-      const uint32_t e = s2.slot[s] - 1;
-      const uint32_t k = s2.keys[e], v = val[e];
-      const uint32_t sz = varlen(k) + varlen(v);
-      if (!ow.put(OP_VARS, sz, 2, k, v)) return PLAN_OVF;
-      total += sz;
-    }
-  }
-  scr[0] = ow.n;
-  out_size = total;
-  return 0;
+  return plan_finish<DIFF>(scr, L, cap, ct, nsec, dt, unsupported, pending, out_size);
 }
 
 // Validation only (first error in stream order), for documents whose section count
@@ -467,11 +477,484 @@ __device__ __noinline__ uint32_t validate_doc(const uint8_t *up, uint32_t un, co
   return e ? (uint32_t)e : (uint32_t)E_OTHER;
 }
 
+// ------------------------------------------------------------------ ring planner
+// k_plan_ring: the common-shape planner.  Lane per document (a C5 batch has ~100k documents:
+// one lane each is the instruction-cheapest walk), but each lane reads its update from a
+// private 256-byte LDS ring instead of HBM: the ring is refilled with sixteen 16-byte loads at
+// one program point of the step loop, so a wave waits for memory once per refill round instead
+// of once per block.  One step consumes one whole item — a block, a section header, a
+// DeleteSet entry header or range — with branch-free LEB128 decodes of 8-byte LDS reads, so
+// lanes of a wave stay converged on the item kind that dominates (string blocks).  Shapes it
+// does not plan — a decode error, cold content kinds, non-ASCII strings, non-canonical blocks,
+// unsquashed DeleteSet ranges, more than 8 clients / DeleteSet entries, a varint longer than 5
+// bytes, a block header longer than the ring — leave the document to the general planner
+// (k_plan pass 0), marked ps.big[d] = PLAN_REDO; everything it plans is byte-identical to it.
+constexpr uint32_t RING = 256;          // ring bytes per lane
+constexpr uint32_t RING_STRIDE = 272;   // LDS bytes per lane (16-byte aligned rows)
+constexpr uint32_t RING_NT = 256;       // lanes (documents) per workgroup
+constexpr uint32_t RING_STEPS = 10;     // item steps between refill points
+constexpr uint8_t PLAN_REDO = 3;
+
+enum : uint32_t { R_NCL, R_SEC, R_BLOCK, R_NDS, R_DENT, R_DRANGE, R_DONE };
+
+// 8 stream bytes at ring byte offset o (o + 8 <= RING_STRIDE): three dword reads + alignbyte
+__device__ __forceinline__ uint64_t ring_read8(const uint32_t *row, uint32_t o) {
+  const uint32_t w = o >> 2, sh = o & 3;
+  const uint32_t d0 = row[w], d1 = row[w + 1], d2 = row[w + 2];
+  const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sh), hi = __builtin_amdgcn_alignbyte(d2, d1, sh);
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
+// Per-lane reader over the ring.  Every read checks that its 8 bytes are in the ring (else
+// `fail` = F_SHORT: the step is retried after a refill) and that the value ends inside the
+// stream (else F_BAIL, like any decode error or a varint longer than 5 bytes).
+enum : uint32_t { F_OK = 0, F_SHORT = 1, F_BAIL = 2 };
+struct RingRd {
+  const uint32_t *row;
+  uint64_t sbase, rb, rend, send;
+  uint32_t un, fail;
+  __device__ __forceinline__ uint64_t at(uint32_t q) {
+    const uint64_t a = sbase + q;
+    if (fail) return 0;
+    if (q >= un) {
+      fail = F_BAIL;
+      return 0;
+    }
+    if (a + 8 > rend && rend != send) {
+      fail = F_SHORT;
+      return 0;
+    }
+    return ring_read8(row, (uint32_t)(a - rb));
+  }
+  // read_var_u32 (varint.rs:244-260, wrapping_shl) at q: bytes consumed
+  __device__ __forceinline__ uint32_t var(uint32_t q, uint32_t &v, bool &canon) {
+    const uint64_t x = at(q);
+    const uint64_t m = ~x & 0x0000008080808080ull;
+    uint32_t nb = ((uint32_t)__builtin_ctzll(m | (1ull << 63)) >> 3) + 1;
+    if (!fail && (nb > 5 || nb > un - q)) fail = F_BAIL;
+    if (fail) nb = 1;
+    const uint64_t xm = x & (nb >= 8 ? ~0ull : ((1ull << (8 * nb)) - 1));
+    v = (uint32_t)((xm & 0x7F) | ((xm >> 1) & 0x3F80) | ((xm >> 2) & 0x1FC000) | ((xm >> 3) & 0xFE00000) |
+                   ((xm >> 4) & 0x7F0000000ull));
+    canon = nb == varlen(v) && (nb != 5 || ((xm >> 32) & 0xFF) < 16);
+    return nb;
+  }
+};
+
+template <bool DIFF>
+__global__ void __launch_bounds__(RING_NT) k_plan_ring(DiffBatch b, PlanScratch ps) {
+  ym_set_grammar(b.v1x);
+  __shared__ __align__(16) uint32_t ring_lds[RING_NT * RING_STRIDE / 4];
+  const uint32_t t = threadIdx.x;
+  const uint32_t d = blockIdx.x * RING_NT + t;
+  uint32_t *row = ring_lds + t * (RING_STRIDE / 4);
+  bool active = d < b.n_docs;
+  if (active && b.pre_status && b.pre_status[d]) { // e.g. a y-sync message that is not SyncStep1
+    ps.big[d] = 0;
+    ps.status[d] = b.pre_status[d];
+    ps.size[d] = 0;
+    active = false;
+  }
+  const uint8_t *up = nullptr, *svp = nullptr;
+  uint32_t un = 0, svn = 0, nsv = 0;
+  uint32_t *scr = nullptr;
+  const PlanCaps cap = small_caps();
+  const PlanLayout L = plan_layout(cap);
+  bool bail = false;
+  if (active) {
+    const uint64_t o0 = b.upd_off[d], o1 = b.upd_off[d + 1];
+    up = b.bytes + o0;
+    un = (uint32_t)(o1 - o0);
+    if (o1 - o0 >= (1ull << 31)) bail = true;
+    scr = ps.small + (size_t)d * ps.small_words;
+    if (DIFF && !bail) { // remote state vector, decoded before the update (alt.rs:77-78)
+      svp = b.sv + b.sv_off[d];
+      svn = (uint32_t)((b.sv_end ? b.sv_end[d] : b.sv_off[d + 1]) - b.sv_off[d]);
+      // entries with a u32 client id go to a small table (the sq region: unsquashed ranges
+      // are the general planner's); a client listed twice keeps its last clock (HashMap::insert)
+      Cur s{svp, svn, 0};
+      bool cn;
+      uint32_t len = 0, clk;
+      uint64_t c;
+      if (rd_var_u32(s, len, cn) || (len && (uint64_t)buckets_for(len) * 17ull > ALLOC_LIMIT)) bail = true;
+      uint32_t *svt = scr + L.sq;
+      for (uint32_t i = 0; i < len && !bail; i++) {
+        if (rd_var_u64(s, c, cn) || rd_var_u32(s, clk, cn)) {
+          bail = true;
+          break;
+        }
+        if (c >> 32) continue;
+        uint32_t k = 0;
+        while (k < nsv && svt[2 * k] != (uint32_t)c) k++;
+        if (k == nsv) {
+          if (nsv == cap.R / 2) {
+            bail = true;
+            break;
+          }
+          nsv++;
+        }
+        svt[2 * k] = (uint32_t)c;
+        svt[2 * k + 1] = clk;
+      }
+    }
+    if (bail) active = false;
+  }
+  GHB ct{scr + L.ct_slot, scr + L.ct_keys, L.BC, 0, 0, 0};
+  GHB dt{scr + L.dt_slot, scr + L.dt_keys, L.BE, 0, 0, 0};
+  uint32_t *cl = scr + L.cl, *sec = scr + L.sec, *de = scr + L.de;
+  uint32_t st = R_NCL, pos = 0, ncl = 0, isec = 0, nb = 0, j = 0, client = 0, clock = 0, nclients = 0;
+  // current section (plan_doc's per-client record, kept in registers while the section runs)
+  uint32_t e = 0, nstored = 0, lkind = 0, lclock = 0, llen = 0, remote = 0, found = 0, count = 0, kb = 0, pure = 1,
+           ssize = 0, nsec = 0;
+  // DeleteSet
+  uint32_t nds = 0, ids = 0, dclient = 0, cpos = 0, nr = 0, kr = 0, prev_e = 0, dsz = 0;
+  bool dcanon = true, dsq = true;
+  RingRd R{row, (uint64_t)up, 0, 0, (uint64_t)up + un, un, F_OK};
+  bool have = false, wait = false;
+
+  for (;;) {
+    if (!__any(active)) break;
+    // ---- refill point: lanes that ran short, or are within 64 bytes of their ring's end
+    const uint64_t a0 = R.sbase + pos;
+    if (active && (!have || wait || (a0 + 64 > R.rb + RING && R.rb + RING < R.send))) {
+      if (have && wait && R.rb == (a0 & ~15ull)) { // an item longer than a fresh ring
+        bail = true;
+        active = false;
+      } else {
+        R.rb = a0 & ~15ull;
+        const uint4 *q = (const uint4 *)R.rb;
+        uint4 *dst = (uint4 *)row;
+#pragma unroll
+        for (uint32_t g = 0; g < RING / 16; g += 8) { // two groups of eight 16-byte loads
+          uint4 x[8];
+#pragma unroll
+          for (uint32_t k = 0; k < 8; k++) x[k] = R.rb + 16 * (g + k) < R.send ? q[g + k] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+          for (uint32_t k = 0; k < 8; k++) dst[g + k] = x[k];
+        }
+        R.rend = R.rb + RING < R.send ? R.rb + RING : R.send;
+        have = true;
+        wait = false;
+      }
+    }
+    for (uint32_t step = 0; step < RING_STEPS; step++) {
+      const bool can = active && !wait;
+      if (!__any(can)) break;
+      if (!can) continue;
+      R.fail = F_OK;
+      bool cn, sec_end = false, entry_end = false;
+      uint32_t q = pos, v;
+      if (st == R_BLOCK) {
+        // ---- one block (Update::decode_block, update.rs:433-488 + ItemContent::decode)
+        const uint32_t info = (uint32_t)(R.at(q) & 0xFF);
+        q++;
+        bool reenc = false;
+        uint32_t kind = BK_ITEM, len = 0, rbytes = 0;
+        if (info == 10 || info == 0) {
+          kind = info == 10 ? BK_SKIP : BK_GC;
+          q += R.var(q, len, cn);
+          reenc = !cn;
+        } else {
+          uint32_t want = info & 0xCF; // 0x10 never re-emitted; 0x20 only when parent_sub decoded
+          if (info & 0x80) {
+            q += R.var(q, v, cn);
+            reenc |= !cn;
+            q += R.var(q, v, cn);
+            reenc |= !cn;
+          }
+          if (info & 0x40) {
+            uint32_t n1 = R.var(q, v, cn);
+            reenc |= !cn;
+            q += n1;
+            uint32_t n2 = R.var(q, v, cn);
+            reenc |= !cn;
+            q += n2;
+            rbytes = n1 + n2;
+          }
+          if ((info & 0xC0) == 0) {
+            uint32_t pi;
+            q += R.var(q, pi, cn);
+            reenc |= !cn || pi > 1;
+            if (pi == 1) {
+              q += R.var(q, v, cn);
+              reenc |= !cn;
+              if (!R.fail && v > un - q) R.fail = F_BAIL;
+              q += v;
+            } else {
+              q += R.var(q, v, cn);
+              reenc |= !cn;
+              q += R.var(q, v, cn);
+              reenc |= !cn;
+            }
+            if (info & 0x20) {
+              want |= 0x20;
+              q += R.var(q, v, cn);
+              reenc |= !cn;
+              if (!R.fail && v > un - q) R.fail = F_BAIL;
+              q += v;
+            }
+          }
+          if (want != info) reenc = true;
+          const uint32_t ref = info & 15;
+          if (ref == 1) {
+            q += R.var(q, len, cn);
+            reenc |= !cn;
+          } else if (ref == 4) {
+            uint32_t slen;
+            q += R.var(q, slen, cn);
+            reenc |= !cn;
+            if (!R.fail && slen > un - q) R.fail = F_BAIL;
+            if (!R.fail && slen > 1) { // v == 1: one UTF-16 unit whatever the byte (wparse_block)
+              uint64_t hib = 0;
+              const uint64_t a = R.sbase + q;
+              if (a + slen + 8 <= R.rend || (R.rend == R.send && a + slen <= R.rend)) {
+                for (uint32_t k = 0; k < slen; k += 8) {
+                  const uint32_t n8 = slen - k < 8 ? slen - k : 8;
+                  hib |= ring_read8(row, (uint32_t)(a + k - R.rb)) & (n8 == 8 ? ~0ull : ((1ull << (8 * n8)) - 1));
+                }
+              } else { // payload past the ring: read it from HBM (the lane refills after it)
+                for (uint32_t k = 0; k < slen; k++) hib |= up[q + k];
+                wait = true;
+              }
+              if (hib & 0x8080808080808080ull) R.fail = F_BAIL; // non-ASCII: UTF-16 length / split checks
+            }
+            len = slen;
+            q += slen;
+          } else {
+            R.fail = F_BAIL; // cold content kinds
+          }
+        }
+        if (!R.fail && reenc) R.fail = F_BAIL; // re-encoded sizes: general planner
+        if (!R.fail) {
+          const uint32_t bpos = pos, blen = q - pos;
+          pos = q;
+          if (kind == BK_ITEM && len == 0) { // Item::new -> None: dropped
+            if (kb != 0xFFFFFFFFu) pure = 0;
+          } else if ((uint64_t)clock + len > 0xFFFFFFFFull) {
+            R.fail = F_BAIL;
+          } else {
+            nstored++;
+            lkind = kind;
+            lclock = clock;
+            llen = len;
+            if (DIFF) {
+              if (!found) {
+                if (kind != BK_SKIP && clock + len > remote) {
+                  found = 1;
+                  const uint32_t off = remote > clock ? remote - clock : 0;
+                  uint32_t sz;
+                  if (off == 0) {
+                    sz = blen;
+                  } else if (kind != BK_ITEM) {
+                    sz = 1 + varlen(len - off);
+                  } else {
+                    // ItemSlice::encode with an offset (emit_block): origin (client, clock + off - 1)
+                    // synthesised, right origin copied (canonical here), no parent info, content
+                    // sliced (ASCII string: byte offset = UTF-16 offset)
+                    const uint32_t rest = len - off;
+                    sz = 1 + varlen(client) + varlen(clock + off - 1) + rbytes + varlen(rest) +
+                         ((info & 15) == 4 ? rest : 0u);
+                  }
+                  uint32_t *sr = cl + CLW * e;
+                  sr[6] = bpos;
+                  sr[7] = clock;
+                  sr[8] = len;
+                  sr[9] = off;
+                  sr[11] = sz;
+                  count = 1;
+                  kb = pos;
+                }
+              } else {
+                if (kb == 0xFFFFFFFFu) kb = bpos;
+                count++;
+                ssize += blen;
+              }
+            }
+            clock += len;
+          }
+          if (!R.fail && ++j == nb) sec_end = true;
+        }
+      } else if (st == R_SEC) {
+        // ---- section header: blocks count, client, first clock
+        q += R.var(q, nb, cn);
+        q += R.var(q, client, cn);
+        q += R.var(q, clock, cn);
+        if (!R.fail) {
+          pos = q;
+          uint32_t f = 0;
+          while (f < nclients && ct.keys[f] != client) f++;
+          if (f == nclients) { // entry(..).or_default (the table itself is built after the walk)
+            nclients++;
+            ct.keys[f] = client;
+            uint32_t *sr = cl + CLW * f;
+            for (uint32_t k = 0; k < CLW; k++) sr[k] = 0;
+            if (DIFF) {
+              const uint32_t *svt = scr + L.sq;
+              uint32_t rc = 0;
+              for (uint32_t k = 0; k < nsv; k++)
+                if (svt[2 * k] == client) rc = svt[2 * k + 1];
+              sr[4] = rc;
+            }
+          }
+          e = f;
+          const uint32_t *sr = cl + CLW * e;
+          nstored = sr[0];
+          lkind = sr[1];
+          lclock = sr[2];
+          llen = sr[3];
+          remote = sr[4];
+          found = sr[5];
+          count = sr[10];
+          if (((uint64_t)nstored + nb) * 32ull > ALLOC_LIMIT || nsec >= cap.C) R.fail = F_BAIL;
+          kb = 0xFFFFFFFFu;
+          pure = 1;
+          ssize = 0;
+          j = 0;
+          if (nb) st = R_BLOCK;
+          else sec_end = true;
+        }
+      } else if (st == R_DRANGE) {
+        // ---- one DeleteSet range (start, len)
+        uint32_t rs, rl;
+        bool c1, c2;
+        q += R.var(q, rs, c1);
+        q += R.var(q, rl, c2);
+        if (!R.fail && (uint64_t)rs + rl > 0xFFFFFFFFull) R.fail = F_BAIL;
+        if (!R.fail) {
+          pos = q;
+          dcanon &= c1 && c2;
+          if (kr > 0 && rs < prev_e) dsq = false;
+          prev_e = rs + rl;
+          dsz += varlen(rs) + varlen(rl);
+          if (++kr == nr) entry_end = true;
+        }
+      } else if (st == R_DENT) {
+        // ---- DeleteSet entry header: client, range count
+        q += R.var(q, dclient, cn);
+        const uint32_t cp = q;
+        q += R.var(q, nr, cn);
+        if (!R.fail) {
+          pos = q;
+          cpos = cp;
+          dcanon = cn;
+          dsq = true;
+          prev_e = 0;
+          dsz = varlen(nr);
+          kr = 0;
+          if (nr) st = R_DRANGE;
+          else entry_end = true;
+        }
+      } else if (st == R_NCL) {
+        q += R.var(q, ncl, cn);
+        if (!R.fail && ncl > cap.C) R.fail = F_BAIL;
+        if (!R.fail) {
+          pos = q;
+          st = ncl ? R_SEC : R_NDS;
+        }
+      } else { // R_NDS
+        q += R.var(q, nds, cn);
+        if (!R.fail && DIFF && nds > cap.E) R.fail = F_BAIL;
+        if (!R.fail) {
+          pos = q;
+          ids = 0;
+          st = nds ? R_DENT : R_DONE;
+        }
+      }
+      if (R.fail == F_SHORT) { // nothing consumed: the item is read again after the refill
+        wait = true;
+        continue;
+      }
+      if (R.fail) {
+        bail = true;
+        active = false;
+        continue;
+      }
+      if (sec_end) {
+        if (kb == 0xFFFFFFFFu) kb = pos;
+        uint32_t *sr = sec + SECW * nsec++;
+        sr[0] = e;
+        sr[1] = kb;
+        sr[2] = pos;
+        sr[3] = pure;
+        sr[4] = ssize;
+        uint32_t *cr = cl + CLW * e;
+        cr[0] = nstored;
+        cr[1] = lkind | 0x100;
+        cr[2] = lclock;
+        cr[3] = llen;
+        cr[5] = found;
+        cr[10] = count;
+        st = ++isec < ncl ? R_SEC : R_NDS;
+      }
+      if (entry_end) {
+        if (DIFF) {
+          if (!dsq) { // squash of a clone: general planner
+            bail = true;
+            active = false;
+            continue;
+          }
+          uint32_t *r = de + DEW * ids;
+          r[0] = dclient;
+          r[1] = cpos;
+          r[2] = pos;
+          r[3] = nr;
+          r[4] = 1u | (dcanon ? 2u : 0u);
+          r[7] = varlen(dclient) + dsz;
+        }
+        st = ++ids < nds ? R_DENT : R_DONE;
+      }
+      if (st == R_DONE) active = false;
+    }
+  }
+  // ---- after the walk (out of the step loop: the calls below do not hold its registers):
+  // hash tables replayed in yrs' insertion order, re-encoded slice sizes, the output plan
+  if (d >= b.n_docs) return;
+  if (!bail && st == R_DONE) {
+    if (ncl && !ct.reserve(ncl, scr + L.ct_tmp)) bail = true;
+    for (uint32_t f = 0; f < nclients && !bail; f++) {
+      if (!ct.reserve(1, scr + L.ct_tmp)) bail = true;
+      else ct.place(ct.keys[f], f);
+    }
+    if (DIFF) {
+      for (uint32_t i = 0; i < nds && !bail; i++) {
+        const uint32_t dc = de[DEW * i];
+        if (!dt.reserve(1, scr + L.dt_tmp)) {
+          bail = true;
+          break;
+        }
+        const int f = dt.find(dc);
+        if (f >= 0) { // replaced in place: the slot now names entry i
+          for (uint32_t s = 0; s < dt.buckets; s++)
+            if (dt.slot[s] == (uint32_t)f + 1) dt.slot[s] = i + 1;
+          dt.keys[i] = dc;
+        } else {
+          dt.place(dc, i);
+        }
+      }
+    }
+    if (!bail) {
+      uint64_t sz = 0;
+      const uint32_t stt = plan_finish<DIFF>(scr, L, cap, ct, nsec, dt, false, 0u, sz);
+      if (stt == PLAN_OVF) {
+        bail = true;
+      } else {
+        if (b.frame && !stt) sz += 2 + varlen(sz); // y-sync message framing
+        ps.big[d] = 0;
+        ps.status[d] = (uint8_t)stt;
+        ps.size[d] = stt ? 0 : sz;
+      }
+    }
+  }
+  if (bail) ps.big[d] = PLAN_REDO;
+}
+
 template <bool DIFF>
 __global__ void __launch_bounds__(64) k_plan(DiffBatch b, PlanScratch ps, int pass) {
+  ym_set_grammar(b.v1x);
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= b.n_docs) return;
   if (pass == 1 && !ps.big[d]) return;
+  if (pass == 0 && ps.big[d] != PLAN_REDO) return; // planned by k_plan_ring
   if (b.pre_status && b.pre_status[d]) { // e.g. a y-sync message that is not SyncStep1
     ps.big[d] = 0;
     ps.status[d] = b.pre_status[d];
@@ -566,7 +1049,36 @@ template <class W> __device__ __forceinline__ void walk_emit(const uint8_t *up, 
   }
 }
 
+// One wavefront copies len bytes (any alignments): byte stores up to the first 16-byte
+// aligned destination address, then per lane 16-byte aligned stores assembled from the
+// source dwords with v_alignbyte (every dword read holds at least one source byte, so no
+// read leaves the source's pages), then the byte tail.
+__device__ __forceinline__ void wave_copy(uint8_t *dst, const uint8_t *src, uint32_t len, uint32_t lane) {
+  uint32_t h = (uint32_t)(-(uintptr_t)dst) & 15u;
+  if (len < 64) h = len;
+  if (lane < h) dst[lane] = src[lane];
+  if (h == len) return;
+  const uint32_t n16 = (len - h) >> 4;
+  const uint8_t *s = src + h;
+  uint4 *d = (uint4 *)(dst + h);
+  const uint32_t sh = (uint32_t)(uintptr_t)s & 3u;
+  const uint32_t *sa = (const uint32_t *)((uintptr_t)s & ~(uintptr_t)3);
+  for (uint32_t k = lane; k < n16; k += 64) {
+    const uint32_t *x = sa + 4 * k;
+    const uint32_t x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3], x4 = sh ? x[4] : 0u;
+    uint4 v;
+    v.x = __builtin_amdgcn_alignbyte(x1, x0, sh);
+    v.y = __builtin_amdgcn_alignbyte(x2, x1, sh);
+    v.z = __builtin_amdgcn_alignbyte(x3, x2, sh);
+    v.w = __builtin_amdgcn_alignbyte(x4, x3, sh);
+    d[k] = v;
+  }
+  const uint32_t done = h + 16 * n16;
+  if (lane < len - done) dst[done + lane] = src[done + lane];
+}
+
 __global__ void __launch_bounds__(256) k_exec(DiffBatch b, PlanScratch ps, const uint64_t *out_off, uint8_t *out) {
+  ym_set_grammar(b.v1x);
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t d = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   if (d >= b.n_docs) return;
@@ -651,19 +1163,23 @@ __global__ void __launch_bounds__(256) k_exec(DiffBatch b, PlanScratch ps, const
     default: break;
     }
   }
-  // verbatim ranges: all lanes, coalesced
+  // verbatim ranges: all lanes, 16-byte aligned stores
   for (uint32_t k = 0; k < nops; k++) {
     const uint32_t *o = ops + OPW * k;
     if (o[0] != OP_COPY) continue;
-    const uint8_t *src = up + o[2];
-    uint8_t *q = dst + o[7];
-    const uint32_t len = o[1];
-    for (uint32_t j = lane; j < len; j += 64) q[j] = src[j];
+    wave_copy(dst + o[7], up + o[2], o[1], lane);
   }
 }
 
 void launch_plan(bool diff, int pass, const DiffBatch &b, const PlanScratch &ps, hipStream_t s) {
   if (!b.n_docs) return;
+  if (pass == 0) { // common shapes: ring planner; the rest (ps.big = PLAN_REDO) in k_plan pass 0
+    dim3 gr((b.n_docs + RING_NT - 1) / RING_NT), tr(RING_NT);
+    if (diff)
+      hipLaunchKernelGGL(k_plan_ring<true>, gr, tr, 0, s, b, ps);
+    else
+      hipLaunchKernelGGL(k_plan_ring<false>, gr, tr, 0, s, b, ps);
+  }
   dim3 g((b.n_docs + 63) / 64), t(64);
   if (diff)
     hipLaunchKernelGGL(k_plan<true>, g, t, 0, s, b, ps, pass);

@@ -14,6 +14,7 @@ struct BatchIn {
   uint32_t n_docs;
   const uint32_t *rec; // per-update decode records (k_decode), REC_WORDS u32 each; fast path only
   const uint32_t *ovf; // their overflow words (DEC_OVF per decode workgroup)
+  uint32_t v1x = 0;    // bytes are the internal v1x grammar (lib0 v2 path), not lib0 v1
 };
 
 // Per-update decode record written by k_decode (one lane per update over the whole
@@ -79,6 +80,7 @@ struct DiffBatch {
   const uint64_t *sv_end = nullptr;       // optional: doc d's SV is [sv_off[d], sv_end[d])
   const uint8_t *pre_status = nullptr;    // optional: nonzero = the document failed before planning
   uint32_t frame = 0;                     // y-sync framing: 0 none, 1 SyncStep2, 2 SyncStep1
+  uint32_t v1x = 0;                       // bytes are the internal v1x grammar (lib0 v2 path)
 };
 // y-sync: parse one client message per document (must be Message::Sync(SyncStep1(sv)),
 // yrs/src/sync/protocol.rs:179-203, 245-272) -> SV slice [sv_off, sv_end) + status

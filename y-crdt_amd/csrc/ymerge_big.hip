@@ -101,6 +101,7 @@ template <int NT>
 __global__ void __launch_bounds__(NT) k_big_count(BatchIn b, uint8_t *path, uint8_t *status, uint64_t *out_start,
                                                   uint64_t *out_len, uint32_t *counts, uint64_t *need,
                                                   uint32_t *n_big, uint32_t *npath) {
+  ym_set_grammar(b.v1x);
   const uint32_t d = blockIdx.x;
   if (d >= b.n_docs) return;
   const uint32_t t = threadIdx.x;
@@ -491,6 +492,7 @@ template <int NT> struct BigShared {
 template <int NT>
 __global__ void __launch_bounds__(NT) k_big_merge(BatchIn b, const uint32_t *counts, const uint64_t *scr_off,
                                                   uint32_t *scratch, FastOut o) {
+  ym_set_grammar(b.v1x);
   const uint32_t d = blockIdx.x;
   if (d >= b.n_docs || o.path[d] != 2) return;
   __shared__ BigShared<NT> S;

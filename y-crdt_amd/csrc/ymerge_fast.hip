@@ -185,6 +185,7 @@ void launch_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_upd
 
 template <int NT, bool STAMPS>
 __global__ void __launch_bounds__(NT, 3) k_fast_merge(BatchIn b, FastCaps caps, FastOut o) {
+  ym_set_grammar(b.v1x);
   constexpr int PER = (int)(FAST_BCAP / NT); // sorted positions per lane (b_cap == FAST_BCAP)
   extern __shared__ __align__(16) uint8_t smem[];
   const FastLayout L = fast_layout(caps);

@@ -143,6 +143,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   if (n_docs > 0xFFFFFFFFull) return YMERGE_ERR_OTHER;
   const uint32_t n = (uint32_t)n_docs;
   ym::BatchIn b{d_bytes, d_upd_off, d_doc_upd, n, nullptr, nullptr};
+  b.v1x = d_bytes == c->v2x.as<uint8_t>(); // the lib0 v2 path's transcoded arena
   const size_t nn = (size_t)n + 1;
   const uint64_t slots = 2 * n_bytes + 64 * (uint64_t)n_docs;
   if (!c->status.ensure(nn) || !c->path.ensure(nn) || !c->out_start.ensure(nn * 8) || !c->out_len.ensure(nn * 8) ||
@@ -295,6 +296,7 @@ static int plan_exec(ymerge_ctx *c, bool diff, const uint8_t *d_bytes, const uin
   if (n_docs > 0xFFFFFFFFull) return YMERGE_ERR_OTHER;
   const uint32_t n = (uint32_t)n_docs;
   ym::DiffBatch b{d_bytes, d_upd_off, d_sv, d_sv_off, n};
+  b.v1x = d_bytes == c->v2x.as<uint8_t>(); // the lib0 v2 path's transcoded arena
   b.frame = frame;
   if (frame == 1) {
     if (!c->sync_off.ensure((n + 1) * 8) || !c->sync_end.ensure((n + 1) * 8) || !c->sync_st.ensure(n + 1))

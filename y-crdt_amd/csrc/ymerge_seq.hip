@@ -34,6 +34,7 @@ struct CountSink {
 
 __global__ void k_seq_count(BatchIn b, const uint8_t *path, uint8_t *status, uint32_t *counts,
                             uint64_t *need_words, uint32_t *n_exact) {
+  ym_set_grammar(b.v1x);
   uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= b.n_docs) return;
   if (path && path[d] != 1) {
@@ -620,6 +621,7 @@ __global__ void k_seq_merge(BatchIn b, const uint8_t *path, const uint8_t *statu
                             const uint64_t *scr_off, uint32_t *scratch, uint64_t *sizes, const uint64_t *out_off,
                             uint8_t *out, uint64_t out_base, uint64_t *out_start, uint64_t *out_len,
                             uint8_t *status_out) {
+  ym_set_grammar(b.v1x);
   uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= b.n_docs) return;
   if (path && path[d] != 1) {

@@ -62,7 +62,12 @@ template <class S> YM_INLINE int smwalk_update(WCur &c, S &s) {
     bool canon = true;
     {
       const bool raw = st == W_INFO;
-      if (raw) bpos = c.i;
+      if (raw) {
+        bpos = c.i;
+        wc_ensure(c, 48); // the whole block in the window: one wait per block
+      } else if (st == W_DST) {
+        wc_ensure(c, 20);
+      }
       uint32_t sh = 0, nbytes = 0, b = 0;
       for (;;) {
         if (c.i >= c.n) return E_EOS;

@@ -99,6 +99,18 @@ YM_INLINE uint32_t wc_byte(WCur &c, uint32_t pos) {
   return __builtin_amdgcn_perm(r1, r0, s4);
 }
 
+// Make the window hold [i, i + need) (clamped to the stream end) before a burst of reads.
+// Called at the top of a block / range: a wave whose lanes need reloads then waits for
+// memory once per block instead of once at every byte-read site some lane misses at
+// (each inlined wc_byte reload is its own divergent branch + wait).  need <= 48 is
+// always satisfiable (the window starts at most 15 bytes before i).
+YM_INLINE void wc_ensure(WCur &c, uint32_t need) {
+  const uint64_t a = (uint64_t)(c.p + c.i), lim = (uint64_t)(c.p + c.n);
+  if (a >= lim) return;
+  const uint64_t want = a + need < lim ? a + need : lim;
+  if (a < c.wa || want > c.wa + 64) wc_load(c, a & ~15ull);
+}
+
 YM_INLINE int wc_u8(WCur &c, uint8_t &v) {
   if (c.i >= c.n) return E_EOS;
   v = (uint8_t)wc_byte(c, c.i++);
@@ -146,6 +158,7 @@ YM_INLINE int wc_var_u64(WCur &c, uint64_t &v, bool &canon) {
 YM_INLINE int wparse_block(WCur &c, BlockInfo &bi) {
   uint8_t info;
   bool cn;
+  wc_ensure(c, 48);
   YM_TRY(wc_u8(c, info));
   bi.info = info;
   bi.reenc = false;
@@ -298,6 +311,7 @@ template <class S> YM_INLINE int wwalk_update(WCur &c, S &s) {
     YM_TRY(s.on_ds_entry(client, nr));
     for (uint32_t k = 0; k < nr; k++) {
       uint32_t st, ln;
+      wc_ensure(c, 20);
       YM_TRY(wc_var_u32(c, st, cn));
       YM_TRY(wc_var_u32(c, ln, cn));
       if ((uint64_t)st + ln > 0xFFFFFFFFull) return E_PANIC;
