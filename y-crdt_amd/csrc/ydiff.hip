@@ -29,9 +29,9 @@
 
 namespace ym {
 
-enum : uint32_t { OP_VARS = 1, OP_COPY = 2, OP_EMIT = 3, OP_WALK = 4, OP_DSQ = 5, OP_DSS = 6 };
+enum : uint32_t { OP_VARS = 1, OP_COPY = 2, OP_EMIT = 3, OP_WALK = 4, OP_DSQ = 5, OP_DSS = 6, OP_SLICE = 7 };
 constexpr uint32_t OPW = 8;  // words per op: kind, size, p0..p4, out offset
-constexpr uint32_t CLW = 12; // words per client entry
+constexpr uint32_t CLW = 16; // words per client entry ([12..14]: first-block op hint, k_plan_ring)
 constexpr uint32_t SECW = 5; // words per section record
 constexpr uint32_t DEW = 8;  // words per DeleteSet entry
 constexpr uint32_t PLAN_OVF = 0xFFFF;
@@ -180,7 +180,12 @@ __device__ __noinline__ uint32_t plan_finish(uint32_t *scr, const PlanLayout &L,
       const uint32_t hclock = st[7] + st[9];
       uint32_t hs = vars_size(3, st[10], client, hclock);
       if (!ow.put(OP_VARS, hs, 3, st[10], client, hclock)) return PLAN_OVF;
-      if (!ow.put(OP_EMIT, st[11], st[6], st[7], st[8], st[9], client)) return PLAN_OVF;
+      // first block past the remote clock: verbatim (canonical, offset 0), an ASCII / Deleted
+      // slice written by the hot executor (ring planner), or emit_block (cold executor)
+      const bool okf = st[14] == 1   ? ow.put(OP_COPY, st[11], st[6])
+                       : st[14] == 2 ? ow.put(OP_SLICE, st[11], client, st[7] + st[9] - 1, st[12], st[13], st[8] - st[9])
+                                     : ow.put(OP_EMIT, st[11], st[6], st[7], st[8], st[9], client);
+      if (!okf) return PLAN_OVF;
       total += hs + st[11];
       for (uint32_t s = 0; s < nsec; s++) {
         const uint32_t *sr = sec + SECW * s;
@@ -326,6 +331,7 @@ __device__ uint32_t plan_doc(const uint8_t *up, uint32_t un, const uint8_t *svp,
             st[8] = bi.len;
             st[9] = off;
             st[11] = sz;
+            if (off == 0 && !bi.reenc && !bi.enc_panic && !bi.unsupported) st[14] = 1; // bytes as they are
             count = 1;
             kb = c.i;
           }
@@ -649,7 +655,7 @@ __global__ void __launch_bounds__(RING_NT) k_plan_ring(DiffBatch b, PlanScratch 
         const uint32_t info = (uint32_t)(R.at(q) & 0xFF);
         q++;
         bool reenc = false;
-        uint32_t kind = BK_ITEM, len = 0, rbytes = 0;
+        uint32_t kind = BK_ITEM, len = 0, rbytes = 0, ropos = 0;
         if (info == 10 || info == 0) {
           kind = info == 10 ? BK_SKIP : BK_GC;
           q += R.var(q, len, cn);
@@ -662,6 +668,7 @@ __global__ void __launch_bounds__(RING_NT) k_plan_ring(DiffBatch b, PlanScratch 
             q += R.var(q, v, cn);
             reenc |= !cn;
           }
+          ropos = q;
           if (info & 0x40) {
             uint32_t n1 = R.var(q, v, cn);
             reenc |= !cn;
@@ -761,6 +768,14 @@ __global__ void __launch_bounds__(RING_NT) k_plan_ring(DiffBatch b, PlanScratch 
                   sr[8] = len;
                   sr[9] = off;
                   sr[11] = sz;
+                  if (off == 0) {
+                    sr[14] = 1;
+                  } else if (kind == BK_ITEM) { // OP_SLICE: right origin bytes, ref, parent_sub flag
+                    const uint32_t has_ps = (info & 0xE0) == 0x20 ? 1u : 0u;
+                    sr[12] = ropos;
+                    sr[13] = rbytes | ((info & 15) << 8) | (has_ps << 12) | ((pos - ropos) << 16);
+                    sr[14] = 2;
+                  }
                   count = 1;
                   kb = pos;
                 }
@@ -1077,8 +1092,25 @@ __device__ __forceinline__ void wave_copy(uint8_t *dst, const uint8_t *src, uint
   if (lane < len - done) dst[done + lane] = src[done + lane];
 }
 
+// The op list of document d (small or length-sized plan scratch)
+__device__ __forceinline__ const uint32_t *plan_ops(const DiffBatch &b, const PlanScratch &ps, uint32_t d, uint32_t un,
+                                                    const uint32_t *&scr, PlanLayout &L) {
+  if (ps.big[d]) {
+    L = plan_layout(big_caps(un));
+    scr = ps.bigscr + ps.big_off[d];
+  } else {
+    L = plan_layout(small_caps());
+    scr = ps.small + (size_t)d * ps.small_words;
+  }
+  return scr + L.ops;
+}
+
+// Hot executor: one wavefront per document.  Wave scan of the op sizes (offsets stored in
+// op word 7), the y-sync header, header varints and ASCII / Deleted slices one lane per op,
+// verbatim ranges (most of the output) by the whole wave with 16-byte stores.  The re-encode
+// ops (OP_EMIT / OP_WALK / OP_DSQ / OP_DSS: general-planner shapes) are k_exec_cold's, so
+// this kernel keeps a small register footprint (no emit_block call).
 __global__ void __launch_bounds__(256) k_exec(DiffBatch b, PlanScratch ps, const uint64_t *out_off, uint8_t *out) {
-  ym_set_grammar(b.v1x);
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t d = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   if (d >= b.n_docs) return;
@@ -1087,16 +1119,8 @@ __global__ void __launch_bounds__(256) k_exec(DiffBatch b, PlanScratch ps, const
   const uint8_t *up = b.bytes + o0;
   const uint32_t un = (uint32_t)(o1 - o0);
   const uint32_t *scr;
-  PlanCaps cap;
-  if (ps.big[d]) {
-    cap = big_caps(un);
-    scr = ps.bigscr + ps.big_off[d];
-  } else {
-    cap = small_caps();
-    scr = ps.small + (size_t)d * ps.small_words;
-  }
-  const PlanLayout L = plan_layout(cap);
-  uint32_t *ops = (uint32_t *)scr + L.ops;
+  PlanLayout L;
+  uint32_t *ops = (uint32_t *)plan_ops(b, ps, d, un, scr, L);
   const uint32_t nops = scr[0];
   uint8_t *dst = out + out_off[d];
   // op offsets: wave-wide exclusive scan of the sizes (acc = the unframed payload size)
@@ -1123,16 +1147,64 @@ __global__ void __launch_bounds__(256) k_exec(DiffBatch b, PlanScratch ps, const
     }
     dst += hl;
   }
-  // header / re-encode ops: one lane each
   for (uint32_t k = lane; k < nops; k += 64) {
     const uint32_t *o = ops + OPW * k;
     Writer w{dst + o[7], 0};
-    switch (o[0]) {
-    case OP_VARS:
+    if (o[0] == OP_VARS) {
       w_var(w, o[3]);
       if (o[2] > 1) w_var(w, o[4]);
       if (o[2] > 2) w_var(w, o[5]);
-      break;
+    } else if (o[0] == OP_SLICE) {
+      // ItemSlice::encode with an offset (slice.rs:199-251 as emit_block does it): origin
+      // (client, clock + off - 1), the right origin's bytes, no parent info; content: the
+      // remaining length, and for a String the payload's last `rest` bytes (ASCII)
+      const uint32_t ro = o[4], pk = o[5], rest = o[6];
+      const uint32_t rbytes = pk & 0xFF, ref = (pk >> 8) & 15, ps_flag = (pk >> 12) & 1, bend = ro + (pk >> 16);
+      w.u8((uint8_t)(0x80 | (rbytes ? 0x40 : 0) | (ps_flag ? 0x20 : 0) | ref));
+      w_var(w, o[2]);
+      w_var(w, o[3]);
+      for (uint32_t q = 0; q < rbytes; q++) w.u8(up[ro + q]);
+      w_var(w, rest);
+      if (ref == 4)
+        for (uint32_t q = 0; q < rest; q++) w.u8(up[bend - rest + q]);
+    }
+  }
+  // verbatim ranges: all lanes, 16-byte aligned stores
+  for (uint32_t k = 0; k < nops; k++) {
+    const uint32_t *o = ops + OPW * k;
+    if (o[0] != OP_COPY) continue;
+    wave_copy(dst + o[7], up + o[2], o[1], lane);
+  }
+}
+
+// Cold executor (after k_exec, whose scan stored the op offsets): one lane per document
+// writes the re-encode ops — emit_block with an offset, a section walked block by block,
+// squashed or re-encoded DeleteSet ranges.
+__global__ void __launch_bounds__(64) k_exec_cold(DiffBatch b, PlanScratch ps, const uint64_t *out_off, uint8_t *out) {
+  ym_set_grammar(b.v1x);
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= b.n_docs) return;
+  if (ps.status[d] || ps.size[d] == 0) return;
+  const uint64_t o0 = b.upd_off[d], o1 = b.upd_off[d + 1];
+  const uint8_t *up = b.bytes + o0;
+  const uint32_t un = (uint32_t)(o1 - o0);
+  const uint32_t *scr;
+  PlanLayout L;
+  const uint32_t *ops = plan_ops(b, ps, d, un, scr, L);
+  const uint32_t nops = scr[0];
+  bool any = false;
+  uint32_t acc = 0;
+  for (uint32_t k = 0; k < nops; k++) {
+    const uint32_t kind = ops[OPW * k];
+    any |= kind == OP_EMIT || kind == OP_WALK || kind == OP_DSQ || kind == OP_DSS;
+    acc += ops[OPW * k + 1];
+  }
+  if (!any) return;
+  uint8_t *dst = out + out_off[d] + (b.frame ? 2 + varlen(acc) : 0);
+  for (uint32_t k = 0; k < nops; k++) {
+    const uint32_t *o = ops + OPW * k;
+    Writer w{dst + o[7], 0};
+    switch (o[0]) {
     case OP_EMIT: emit_block(up, un, o[2], o[6], o[3], o[4], o[5], w); break;
     case OP_WALK: walk_emit(up, un, o[2], o[3], o[6], w); break;
     case OP_DSQ: {
@@ -1163,12 +1235,6 @@ __global__ void __launch_bounds__(256) k_exec(DiffBatch b, PlanScratch ps, const
     default: break;
     }
   }
-  // verbatim ranges: all lanes, 16-byte aligned stores
-  for (uint32_t k = 0; k < nops; k++) {
-    const uint32_t *o = ops + OPW * k;
-    if (o[0] != OP_COPY) continue;
-    wave_copy(dst + o[7], up + o[2], o[1], lane);
-  }
 }
 
 void launch_plan(bool diff, int pass, const DiffBatch &b, const PlanScratch &ps, hipStream_t s) {
@@ -1193,6 +1259,7 @@ void launch_big_need(const uint64_t *upd_off, const uint8_t *big, uint32_t n, ui
 void launch_exec(const DiffBatch &b, const PlanScratch &ps, const uint64_t *out_off, uint8_t *out, hipStream_t s) {
   if (!b.n_docs) return;
   hipLaunchKernelGGL(k_exec, dim3((b.n_docs + 3) / 4), dim3(256), 0, s, b, ps, out_off, out);
+  hipLaunchKernelGGL(k_exec_cold, dim3((b.n_docs + 63) / 64), dim3(64), 0, s, b, ps, out_off, out);
 }
 
 } // namespace ym
