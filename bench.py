@@ -193,6 +193,7 @@ def run_merge(a, rank, world, dev):
     ms_decode, ms_fast, ms_big, ms_exact = mean("ms_decode"), mean("ms_fast"), mean("ms_big"), mean("ms_exact")
     ms_pipe = ms_decode + ms_fast + ms_big + ms_exact
     docs_exact, docs_big = int(kstats[-1]["docs_exact"]), int(kstats[-1]["docs_big"])
+    docs_tiny = int(kstats[-1]["docs_tiny"])
 
     e2e = None
     if not a.no_e2e:  # end-to-end: pinned host arena -> H2D -> pipeline -> pack -> D2H
@@ -238,6 +239,7 @@ def run_merge(a, rank, world, dev):
                      "kernel": "k_decode+k_fast_merge(+k_big_merge, exact engine)", "kernel_ms": ms_pipe,
                      "k_decode_ms": ms_decode, "k_fast_merge_ms": ms_fast, "big_path_ms": ms_big,
                      "exact_path_ms": ms_exact, "docs_big_path": docs_big, "docs_exact_path": docs_exact,
+                     "docs_tiny_path": docs_tiny,
                      "alg_bytes_per_launch": alg_bytes},
         "end_to_end": None if e2e is None else {
             "value": float(allst[:, 1].sum()) / float(allst[:, 6].max()) / 1e9, "unit": "GB/s",

@@ -83,6 +83,9 @@ typedef struct {
   float ms_big;    /* merge: documents over the LDS capacities (k_big_count + k_big_merge) */
   uint32_t docs_overlap; /* merge: of docs_big, documents with overlapping updates (run order, splices) */
   uint64_t docs_big; /* merge: documents written by the tiled kernel (docs_exact: exact engine) */
+  uint64_t docs_tiny; /* merge: documents of <= 4 updates (<= 4 KB) written one lane each by the
+                         lane-per-document engine (not counted in docs_exact) */
+  float ms_tiny;      /* merge: exact-engine stage time when it ran tiny documents only */
 } ymerge_stats;
 
 /* Device-resident result, owned by the context, valid until the next batch.

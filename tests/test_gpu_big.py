@@ -28,6 +28,25 @@ def test_c3_zipf_tail_on_tiled_kernel(engine, oracle):
     st = engine.stats()
     assert st["docs_exact"] == 0, st
     assert st["docs_big"] >= big, st
+    assert st["docs_tiny"] > 0, st  # documents of <= 4 updates: lane per document
+
+
+def test_tiny_docs_on_fast_path(oracle):
+    """The same Zipf documents with the tiny-document route off (YMERGE_TINY=0): the
+    workgroup fast path must keep handling documents of 1-4 updates."""
+    import os
+    import ymerge
+    os.environ["YMERGE_TINY"] = "0"
+    try:
+        e = ymerge.Engine(0)
+    finally:
+        del os.environ["YMERGE_TINY"]
+    try:
+        check_batch(e, oracle, workloads.zipf_docs(3000, seed=0x5EED + 1))
+        st = e.stats()
+        assert st["docs_tiny"] == 0 and st["docs_exact"] == 0, st
+    finally:
+        e.close()
 
 
 def test_c1_trace_on_tiled_kernel(engine, oracle):

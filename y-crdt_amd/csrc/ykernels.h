@@ -44,7 +44,8 @@ struct FastOut {
   uint8_t *status, *path;
   uint64_t *stamps; // diagnostic build only: s_memtime per phase (16 per document)
   uint32_t *npath;  // npath[p]: documents handed to path p (1 exact engine, 2 tiled kernel); [3] tiled
-                    // kernel in overlap mode, [4] tiled kernel -> exact engine
+                    // kernel in overlap mode, [4] tiled kernel -> exact engine, [5] of [1]:
+                    // tiny documents (FastCaps.in_cap / u_cap)
 };
 size_t fast_lds_bytes(const FastCaps &c);
 void launch_fast_merge(const BatchIn &b, const FastCaps &caps, const FastOut &o, int nt, hipStream_t s);

@@ -221,6 +221,14 @@ __global__ void __launch_bounds__(NT, 3) k_fast_merge(BatchIn b, FastCaps caps, 
     handover();
     return;
   }
+  // Tiny documents (<= in_cap updates, <= u_cap bytes): one lane each in the lane-per-document
+  // engine is cheaper than this workgroup's fixed phase sequence (C3: 2/3 of the documents;
+  // measured 13.5 ms here vs 4.5 ms there for the 645k documents of <= 4 updates).
+  if (U > 0 && U <= caps.in_cap && B1 - B0 <= caps.u_cap) {
+    if (t == 0) atomicAdd(&o.npath[5], 1u);
+    handover();
+    return;
+  }
   if (t == 0) {
     misc[0] = 0xFFFFFFFFu;
     misc[1] = 0;

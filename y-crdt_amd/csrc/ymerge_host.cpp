@@ -62,7 +62,8 @@ struct ymerge_ctx {
   hipEvent_t ev[8];
   ymerge_stats stats{};
   uint64_t stamps_docs = 0; // documents covered by `stamps` (last merge batch)
-  ym::FastCaps caps{0, 0, 1024, 512, 512}; // b_cap must equal FAST_BCAP (ymerge_fast.hip) // (unused), (unused), blocks, DS entries, DS ranges
+  // tiny-document updates / bytes, blocks (must equal FAST_BCAP, ymerge_fast.hip), DS entries, DS ranges
+  ym::FastCaps caps{4, 4096, 1024, 512, 512};
   int fast_threads = 256;
   std::mutex mu;
 };
@@ -80,6 +81,7 @@ static bool ctx_init(ymerge_ctx *c, int device) {
   // document through the exact engine (used by the parity tests to cover both engines)
   if (const char *v = getenv("YMERGE_FAST_THREADS")) c->fast_threads = atoi(v);
   if (const char *v = getenv("YMERGE_STAMPS")) c->want_stamps = atoi(v) != 0;
+  if (const char *v = getenv("YMERGE_TINY")) c->caps.in_cap = (uint32_t)atoi(v); // 0: no tiny path
   // the fast kernel's LDS layout must fit one workgroup (160 KB on gfx950)
   int lds_max = 0;
   if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess) return false;
@@ -210,19 +212,20 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   hipEventRecord(c->ev[1], c->s);
   // exact engine for documents the fast or tiled path handed over (path == 1)
   uint64_t words = 0;
-  uint32_t n_exact = 0, n_overlap = 0;
+  uint32_t n_exact = 0, n_overlap = 0, n_tiny = 0;
   if (n_p1 || n_p2) {
     ym::launch_seq_count(b, path, status, c->counts.as<uint32_t>(), c->need.as<uint64_t>(), c->counter.as<uint32_t>(),
                          c->s);
     ym::launch_scan_u64(c->need.as<uint64_t>(), c->scr_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
     hipMemcpyAsync(c->h_pinned + 8, c->scr_off.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, c->s);
     hipMemcpyAsync(c->h_pinned + 9, c->counter.p, 4, hipMemcpyDeviceToHost, c->s);
-    hipMemcpyAsync(c->h_pinned + 14, c->counter.as<uint32_t>() + 7, 8, hipMemcpyDeviceToHost, c->s);
+    hipMemcpyAsync(c->h_pinned + 14, c->counter.as<uint32_t>() + 7, 12, hipMemcpyDeviceToHost, c->s);
     if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
     words = c->h_pinned[8];
     n_exact = (uint32_t)(c->h_pinned[9] & 0xFFFFFFFFu);
     n_overlap = (uint32_t)(c->h_pinned[14] & 0xFFFFFFFFu);
     n_big -= (uint32_t)(c->h_pinned[14] >> 32); // tiled-kernel documents handed to the exact engine
+    n_tiny = (uint32_t)(c->h_pinned[15] & 0xFFFFFFFFu);
   }
   if (n_exact) {
     if (!c->scratch.ensure((size_t)words * 4 + 64)) return YMERGE_ERR_DEVICE;
@@ -257,7 +260,9 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   c->stats.n_docs = n_docs;
   c->stats.bytes_in = n_bytes;
   c->stats.bytes_out = total;
-  c->stats.docs_exact = n_exact;
+  c->stats.docs_exact = n_exact - n_tiny;
+  c->stats.docs_tiny = n_tiny;
+  c->stats.ms_tiny = n_exact == n_tiny ? t12 : 0.0f;
   c->stats.docs_big = n_big;
   c->stats.docs_overlap = n_overlap;
   c->stats.docs_fast = n_docs - n_exact - n_big;
