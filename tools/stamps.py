@@ -15,7 +15,60 @@ NAMES = ["decode", "-", "sort", "classify", "sizes", "write", "ds_clients", "ds_
          "ds_write"]
 
 
+BIG_NAMES = ["gather", "sort", "classify", "write", "deleteset"]
+
+
+def main_big(n):
+    """Tiled-kernel documents (k_big_merge, marker 0xB16 in slot 7) of a C3-style batch."""
+    b = workloads.zipf_docs(n, seed=0x5EED)
+    e = ymerge.Engine(0)
+    e.merge_host(b.data, b.upd_off, b.doc_upd)
+    L = ymerge.lib()
+    L.ymerge_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+    st = np.zeros((n, 16), np.uint64)
+    assert L.ymerge_debug_stamps(e._ctx, n, st.ctypes.data) == 0
+    ok = (st[:, 7] == 0xB16) & (st[:, 5] > 0)
+    U = np.diff(b.doc_upd.astype(np.int64))[ok]
+    d = np.diff(st[ok][:, :6].astype(np.int64), axis=1)
+    tot = d.sum(axis=1)
+    print(f"tiled docs: {ok.sum()}, updates/doc mean {U.mean():.0f}, cycles/doc mean {tot.mean():.0f}, "
+          f"cycles/update {(tot / U).mean():.0f}")
+    for i, nm in enumerate(BIG_NAMES):
+        print(f"  {nm:10s} {d[:, i].mean():10.0f} cycles  {100 * d[:, i].mean() / tot.mean():5.1f}%")
+    for lo, hi in ((0, 2000), (2000, 4000), (4000, 10001)):
+        sel = (U > lo) & (U <= hi)
+        if sel.any():
+            print(f"  U in ({lo},{hi}]: {sel.sum()} docs, cycles/doc {tot[sel].mean():.0f}, "
+                  + ", ".join(f"{nm} {d[sel, i].mean():.0f}" for i, nm in enumerate(BIG_NAMES)))
+
+
+def main_zipf(n):
+    """Fast-path documents of a C3-style batch, phase cycles by update count."""
+    b = workloads.zipf_docs(n, seed=0x5EED)
+    e = ymerge.Engine(0)
+    e.merge_host(b.data, b.upd_off, b.doc_upd)
+    L = ymerge.lib()
+    L.ymerge_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+    st = np.zeros((n, 16), np.uint64)
+    assert L.ymerge_debug_stamps(e._ctx, n, st.ctypes.data) == 0
+    ok = (st[:, 11] > 0) & (st[:, 7] != 0xB16)
+    U = np.diff(b.doc_upd.astype(np.int64))[ok]
+    d = np.diff(st[ok][:, :12].astype(np.int64), axis=1)
+    tot = d.sum(axis=1)
+    print(f"fast docs {ok.sum()}: cycles/doc mean {tot.mean():.0f}")
+    for lo, hi in ((0, 4), (4, 16), (16, 64), (64, 256), (256, 1300)):
+        sel = (U > lo) & (U <= hi)
+        if sel.any():
+            print(f"  U in ({lo},{hi}]: {sel.sum()} docs, cycles/doc {tot[sel].mean():.0f}: "
+                  + ", ".join(f"{nm} {d[sel, i].mean():.0f}" for i, nm in enumerate(NAMES) if nm != "-"))
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "zipf":
+        os.environ["YMERGE_TINY"] = "0"
+        return main_zipf(int(sys.argv[2]) if len(sys.argv) > 2 else 20000)
+    if len(sys.argv) > 1 and sys.argv[1] == "big":
+        return main_big(int(sys.argv[2]) if len(sys.argv) > 2 else 20000)
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
     threads = os.environ.get("YMERGE_FAST_THREADS", "256")
     b = workloads.text_docs(n, 1000)

@@ -134,6 +134,22 @@ __device__ __forceinline__ void bscan_seg(uint32_t f, uint32_t v, uint32_t *ws, 
 }
 
 // bitonic sort of (key64, val32) pairs, n a power of two, composite order (key, val)
+// Ascending bitonic sort of one u64 per lane across a wavefront (registers and lane
+// shuffles, no LDS, no barrier); pad unused lanes with ~0.
+YM_INLINE uint64_t wave_bitonic64(uint64_t x, uint32_t lane) {
+#pragma unroll
+  for (uint32_t size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+      const uint32_t lo = __shfl_xor((uint32_t)x, stride, 64), hi = __shfl_xor((uint32_t)(x >> 32), stride, 64);
+      const uint64_t y = ((uint64_t)hi << 32) | lo;
+      const bool take_min = ((lane & stride) == 0) == ((lane & size) == 0);
+      x = take_min ? (x < y ? x : y) : (x < y ? y : x);
+    }
+  }
+  return x;
+}
+
 template <int NT> YM_INLINE void bitonic(uint64_t *k, uint32_t *v, uint32_t n) {
   for (uint32_t size = 2; size <= n; size <<= 1) {
     for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {

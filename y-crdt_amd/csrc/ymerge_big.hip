@@ -195,15 +195,16 @@ template <int NT>
 __device__ int wg_sort(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1, uint32_t n, uint8_t *lds) {
   uint64_t *ck = (uint64_t *)lds;
   uint32_t *cv = (uint32_t *)(lds + 8 * BIG_CHUNK);
-  for (uint32_t c0 = 0; c0 < n; c0 += BIG_CHUNK) {
-    for (uint32_t j = threadIdx.x; j < BIG_CHUNK; j += NT) {
+  const uint32_t CH = n < BIG_CHUNK ? pow2ceil(n < 2 ? 2 : n) : BIG_CHUNK; // chunk no larger than the input
+  for (uint32_t c0 = 0; c0 < n; c0 += CH) {
+    for (uint32_t j = threadIdx.x; j < CH; j += NT) {
       const uint32_t g = c0 + j;
       ck[j] = g < n ? k0[g] : ~0ull;
       cv[j] = g < n ? v0[g] : 0xFFFFFFFFu;
     }
     __syncthreads();
-    bitonic<NT>(ck, cv, BIG_CHUNK);
-    for (uint32_t j = threadIdx.x; j < BIG_CHUNK; j += NT) {
+    bitonic<NT>(ck, cv, CH);
+    for (uint32_t j = threadIdx.x; j < CH; j += NT) {
       const uint32_t g = c0 + j;
       if (g < n) {
         k0[g] = ck[j];
@@ -215,7 +216,7 @@ __device__ int wg_sort(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1, u
   uint64_t *ka = k0, *kb = k1;
   uint32_t *va = v0, *vb = v1;
   int which = 0;
-  for (uint32_t w = BIG_CHUNK; w < n; w <<= 1) {
+  for (uint32_t w = CH; w < n; w <<= 1) {
     for (uint32_t j = threadIdx.x; j < n; j += NT) {
       const uint64_t kj = ka[j];
       const uint32_t run = j / w, i = j - run * w;
@@ -509,6 +510,17 @@ __global__ void __launch_bounds__(NT) k_big_merge(BatchIn b, const uint32_t *cou
   const uint64_t cap = 2ull * nbytes + 64;
   uint8_t *out = o.out + slot;
   bool om = false; // overlap mode: m.sord holds the run order of big_run_order
+  // diagnostic runs only (YMERGE_STAMPS=1 sets o.stamps): s_memtime per phase, slot 7 = marker
+  auto stamp = [&](uint32_t k) {
+    if (o.stamps) {
+      __syncthreads();
+      if (t == 0) {
+        o.stamps[(size_t)d * 16 + k] = __builtin_amdgcn_s_memtime();
+        o.stamps[(size_t)d * 16 + 7] = 0xB16;
+      }
+    }
+  };
+  stamp(0);
   auto finish = [&](uint8_t p, uint8_t st, uint64_t len) {
     if (t == 0) {
       if (p == 1) {
@@ -624,6 +636,7 @@ __global__ void __launch_bounds__(NT) k_big_merge(BatchIn b, const uint32_t *cou
   }
   __syncthreads();
 
+  stamp(1);
   // ---- 2 sort blocks by (client desc, clock asc, input order)
   const uint32_t *sval = m.v0;
   bool ident = true;
@@ -645,6 +658,7 @@ __global__ void __launch_bounds__(NT) k_big_merge(BatchIn b, const uint32_t *cou
   }
   auto srt = [&](uint32_t j) -> uint32_t { return om ? m.sord[j] : (ident ? j : sval[j]); };
 
+  stamp(2);
   // ---- 3 classify (tiles of NT sorted positions, carries between tiles):
   //      running end E (segmented max), keep / Skip / drop; first pass: a partial overlap
   //      or a same-clock block that is not a duplicate of the kept one -> overlap mode,
@@ -752,6 +766,7 @@ __global__ void __launch_bounds__(NT) k_big_merge(BatchIn b, const uint32_t *cou
     break;
   }
 
+  stamp(3);
   // ---- 4 sizes, offsets, write (LDS-staged per tile when the tile's bytes fit)
   uint64_t blocks_size = varlen(NC);
   bool ovf = false;
@@ -848,6 +863,7 @@ __global__ void __launch_bounds__(NT) k_big_merge(BatchIn b, const uint32_t *cou
     return;
   }
 
+  stamp(4);
   // ---- 5 DeleteSet: distinct clients and first occurrence (LDS hash, 64-bit CAS insert,
   //      atomicMin on a hit), sorted by client; yrs' table order (IdSet::merge inserts in
   //      first-occurrence order, hashbrown layout); live ranges sorted by (client, start);
@@ -888,35 +904,55 @@ __global__ void __launch_bounds__(NT) k_big_merge(BatchIn b, const uint32_t *cou
     finish(1, 0, 0);
     return;
   }
-  // sort the table (occupied slots first, by client); D distinct clients
-  {
-    uint32_t *tv = (uint32_t *)lscr; // values (unused by the order)
-    for (uint32_t j = t; j < BIG_DTAB; j += NT) tv[j] = j;
-    __syncthreads();
-    bitonic<NT>(dtab, tv, BIG_DTAB);
-  }
+  // D distinct clients.  Few (the usual case): the occupied slots are compacted and one
+  // wave sorts them in registers (by client, then the ranks by first occurrence); else the
+  // whole table is bitonic-sorted twice (occupied slots first).
   uint32_t D;
   {
     uint32_t c = 0;
     for (uint32_t j = t; j < BIG_DTAB; j += NT) c += dtab[j] != ~0ull;
-    bscan_sum<NT>(c, ws, D);
+    uint32_t pre = bscan_sum<NT>(c, ws, D);
+    if (D <= 64) {
+      uint64_t *cmp = (uint64_t *)lscr;
+      for (uint32_t j = t; j < BIG_DTAB; j += NT)
+        if (dtab[j] != ~0ull) cmp[pre++] = dtab[j];
+      __syncthreads();
+      if (t < 64) {
+        const uint64_t x = wave_bitonic64(t < D ? cmp[t] : ~0ull, t); // (client, first occurrence)
+        if (t < D) {
+          d_client[t] = (uint32_t)(x >> 32);
+          d_first[t] = (uint32_t)x;
+        }
+        const uint64_t y = wave_bitonic64(t < D ? ((x & 0xFFFFFFFFull) << 32) | t : ~0ull, t);
+        if (t < D) dtab[t] = y; // rank of the t-th first occurrence in the low half
+      }
+      __syncthreads();
+    }
   }
   if (D > BIG_DCAP) {
     finish(1, 0, 0);
     return;
   }
-  for (uint32_t j = t; j < D; j += NT) {
-    d_client[j] = (uint32_t)(dtab[j] >> 32);
-    d_first[j] = (uint32_t)dtab[j];
-  }
-  __syncthreads();
-  // first-occurrence order of the ranks (dtab reused as keys: first << 32 | rank)
-  for (uint32_t j = t; j < BIG_DTAB; j += NT) dtab[j] = j < D ? ((uint64_t)d_first[j] << 32) | j : ~0ull;
-  {
-    uint32_t *tv = (uint32_t *)lscr;
-    for (uint32_t j = t; j < BIG_DTAB; j += NT) tv[j] = j;
+  if (D > 64) {
+    {
+      uint32_t *tv = (uint32_t *)lscr; // values (unused by the order)
+      for (uint32_t j = t; j < BIG_DTAB; j += NT) tv[j] = j;
+      __syncthreads();
+      bitonic<NT>(dtab, tv, BIG_DTAB);
+    }
+    for (uint32_t j = t; j < D; j += NT) {
+      d_client[j] = (uint32_t)(dtab[j] >> 32);
+      d_first[j] = (uint32_t)dtab[j];
+    }
     __syncthreads();
-    bitonic<NT>(dtab, tv, BIG_DTAB);
+    // first-occurrence order of the ranks (dtab reused as keys: first << 32 | rank)
+    for (uint32_t j = t; j < BIG_DTAB; j += NT) dtab[j] = j < D ? ((uint64_t)d_first[j] << 32) | j : ~0ull;
+    {
+      uint32_t *tv = (uint32_t *)lscr;
+      for (uint32_t j = t; j < BIG_DTAB; j += NT) tv[j] = j;
+      __syncthreads();
+      bitonic<NT>(dtab, tv, BIG_DTAB);
+    }
   }
   // hashbrown emulation (single lane; D <= BIG_DCAP): slots hold rank + 1
   if (t == 0) {
@@ -1124,6 +1160,7 @@ __global__ void __launch_bounds__(NT) k_big_merge(BatchIn b, const uint32_t *cou
     w_var(w, cs);
     w_var(w, m.cend[j] - cs);
   }
+  stamp(5);
   finish(0, 0, total);
 }
 

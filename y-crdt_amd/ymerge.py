@@ -17,7 +17,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libymerge.so")
+LIB_PATH = os.environ.get("YMERGE_LIB") or os.path.join(_HERE, "lib", "libymerge.so")  # YMERGE_LIB: A/B experiments only
 
 ERRORS = {2: "InvalidVarInt", 3: "EndOfBuffer", 4: "UnexpectedValue", 5: "InvalidJSON", 6: "Other",
           7: "NotEnoughMemory", 20: "ReferencePanic", 21: "Unsupported", 30: "DeviceError"}
