@@ -68,6 +68,18 @@ def test_large_multi_client_docs(engine, oracle):
     assert engine.stats()["docs_exact"] == 0
 
 
+def test_large_docs_client_counts(engine, oracle):
+    """The tiled kernel's client counting sort (<= 8 clients) and its fallback to the
+    general stable sort (9-12 clients), at 8 and 9 clients exactly and above."""
+    docs = []
+    for k, (lo, hi) in enumerate(((8, 8), (9, 9), (10, 12))):
+        b = workloads.text_docs(2, 3000, seed=300 + k, min_clients=lo, max_clients=hi)
+        docs += [b.doc_updates(0), b.doc_updates(1)]
+    check_batch(engine, oracle, batch_of(docs))
+    st = engine.stats()
+    assert st["docs_exact"] == 0 and st["docs_big"] == 6, st
+
+
 def test_shuffled_large_docs(engine, oracle):
     """Updates in random order (clock order restored by the sort), duplicated updates."""
     rng = np.random.default_rng(5)

@@ -647,7 +647,117 @@ __global__ void __launch_bounds__(NT) k_big_merge(BatchIn b, const uint32_t *cou
       if (a > c) bad = 1;
     }
     ident = !__syncthreads_or(bad);
-    if (!ident) {
+    // Few clients (the usual case: a handful of editors): stable counting sort by client
+    // rank in tiles, then a clock-order check per client run; the general stable sort runs
+    // only when that check fails or there are more than 8 clients.
+    bool counted = false;
+    if (!ident && NB < (1u << 25)) {
+      uint64_t *btab = (uint64_t *)S.un; // [64] client << 32 | rank, ~0 = empty
+      for (uint32_t i = t; i < 64; i += NT) btab[i] = ~0ull;
+      if (t == 0) sc[3] = 0;
+      __syncthreads();
+      uint32_t ovf = 0;
+      for (uint32_t j = t; j < NB && !ovf; j += NT) {
+        const uint32_t c = m.bc[j];
+        if (j > 0 && m.bc[j - 1] == c) continue;
+        uint32_t h = mix32(c) >> 26;
+        for (uint32_t probe = 0;; probe++) {
+          if (probe == 64) {
+            ovf = 1;
+            break;
+          }
+          uint64_t cur = btab[h];
+          if (cur == ~0ull) {
+            const uint64_t prev = atomicCAS((unsigned long long *)&btab[h], ~0ull, (unsigned long long)c << 32);
+            if (prev == ~0ull) {
+              atomicAdd(&sc[3], 1u);
+              break;
+            }
+            cur = prev;
+          }
+          if ((uint32_t)(cur >> 32) == c) break;
+          h = (h + 1) & 63;
+        }
+      }
+      ovf = __syncthreads_or(ovf);
+      const uint32_t ncl = sc[3];
+      if (!ovf && ncl <= 8) {
+        // rank = number of distinct clients greater than this one (descending client order)
+        const uint64_t mine = t < 64 ? btab[t] : ~0ull;
+        uint32_t r = 0;
+        if (mine != ~0ull)
+          for (uint32_t q = 0; q < 64; q++) {
+            const uint64_t o2 = btab[q];
+            r += (o2 != ~0ull && (uint32_t)(o2 >> 32) > (uint32_t)(mine >> 32));
+          }
+        __syncthreads();
+        if (mine != ~0ull) btab[t] = (mine & 0xFFFFFFFF00000000ull) | r;
+        __syncthreads();
+        auto rank_of = [&](uint32_t c) -> uint32_t {
+          uint32_t h = mix32(c) >> 26;
+          while ((uint32_t)(btab[h] >> 32) != c) h = (h + 1) & 63;
+          return (uint32_t)btab[h];
+        };
+        // rank totals (per-lane 16-bit fields: < 2^25 / NT elements per lane), rank starts
+        uint64_t c0 = 0, c1 = 0;
+        for (uint32_t j = t; j < NB; j += NT) {
+          const uint32_t rr = rank_of(m.bc[j]);
+          if (rr < 4) c0 += 1ull << (16 * rr);
+          else c1 += 1ull << (16 * (rr - 4));
+        }
+        uint32_t start[8], carry[8];
+        {
+          uint32_t *rtot = (uint32_t *)(S.un + 64 * 8); // [8] LDS rank totals
+          if (t < 8) rtot[t] = 0;
+          __syncthreads();
+#pragma unroll
+          for (uint32_t q = 0; q < 8; q++) {
+            const uint32_t v = (uint32_t)(q < 4 ? (c0 >> (16 * q)) & 0xFFFF : (c1 >> (16 * (q - 4))) & 0xFFFF);
+            if (v) atomicAdd(&rtot[q], v);
+          }
+          __syncthreads();
+          uint32_t acc = 0;
+#pragma unroll
+          for (uint32_t q = 0; q < 8; q++) {
+            start[q] = acc;
+            carry[q] = 0;
+            acc += rtot[q];
+          }
+        }
+        // tiles in input order: within-tile prefix per rank (two packed scans), then place
+        for (uint32_t base = 0; base < NB; base += NT) {
+          const uint32_t j = base + t;
+          const bool valid = j < NB;
+          const uint32_t rr = valid ? rank_of(m.bc[j]) : 0;
+          const uint64_t i0 = valid && rr < 4 ? 1ull << (16 * rr) : 0, i1 = valid && rr >= 4 ? 1ull << (16 * (rr - 4)) : 0;
+          uint64_t T0, T1;
+          const uint64_t p0 = bscan_sum64<NT>(i0, S.ws64, T0), p1 = bscan_sum64<NT>(i1, S.ws64, T1);
+          if (valid) {
+            const uint32_t within = rr < 4 ? (uint32_t)((p0 >> (16 * rr)) & 0xFFFF) : (uint32_t)((p1 >> (16 * (rr - 4))) & 0xFFFF);
+            uint32_t st = 0, ca = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < 8; q++)
+              if (q == rr) {
+                st = start[q];
+                ca = carry[q];
+              }
+            const uint32_t pos = st + ca + within;
+            m.v1[pos] = j;
+            m.k1[pos] = ((uint64_t)(~m.bc[j]) << 32) | m.bk[j];
+          }
+#pragma unroll
+          for (uint32_t q = 0; q < 8; q++)
+            carry[q] += q < 4 ? (uint32_t)((T0 >> (16 * q)) & 0xFFFF) : (uint32_t)((T1 >> (16 * (q - 4))) & 0xFFFF);
+        }
+        __syncthreads();
+        uint32_t bad2 = 0;
+        for (uint32_t j = t; j + 1 < NB; j += NT)
+          if (m.k1[j] > m.k1[j + 1]) bad2 = 1;
+        counted = !__syncthreads_or(bad2);
+        if (counted) sval = m.v1;
+      }
+    }
+    if (!ident && !counted) {
       for (uint32_t j = t; j < NB; j += NT) {
         m.k0[j] = ((uint64_t)(~m.bc[j]) << 32) | m.bk[j];
         m.v0[j] = j;
