@@ -102,8 +102,9 @@ typedef struct {
 
 /* merge_updates_v1 over a batch whose arena (n_bytes) and offsets (n_updates + 1,
  * n_docs + 1) already live in HBM of the context's device.  The kernels load the arena
- * in aligned 4/16-byte words: d_bytes must stay readable for 16 bytes past n_bytes (pad
- * the allocation; the host entry points do).  Same for the update/SV arenas below.
+ * in aligned 4/16-byte words: d_bytes must be 16-byte aligned (hipMalloc's are) and stay
+ * readable for 16 bytes past n_bytes (pad the allocation; the host entry points do).  Same
+ * for the update/SV arenas below.
  * Returns 0 or YMERGE_ERR_DEVICE. */
 int ymerge_updates_v1_batch_device(ymerge_ctx *ctx, const uint8_t *d_bytes, uint64_t n_bytes,
                                    const uint64_t *d_upd_off, uint64_t n_updates, const uint64_t *d_doc_upd,

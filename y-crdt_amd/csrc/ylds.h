@@ -41,7 +41,8 @@ YM_INLINE bool lvar(LCur &c, uint32_t &v, bool &canon) {
   if (len < 4) val &= (1u << (7 * len)) - 1;
   else if (len == 5) val |= (b4 & 0x7Fu) << 28;
   const uint32_t last = len == 5 ? b4 : (x >> (8 * (len - 1))) & 0xFF;
-  canon = len == varlen(val) && (len != 5 || last < 16);
+  // minimal length <=> a one-byte varint, or a nonzero last group (that still fits in u32)
+  canon = len == 1 || (last != 0 && (len != 5 || last < 16));
   v = val;
   c.p += len;
   return true;

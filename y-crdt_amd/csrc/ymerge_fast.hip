@@ -111,11 +111,22 @@ __global__ void __launch_bounds__(DEC_NT) k_decode(const uint8_t *bytes, const u
   const uint64_t i = g0 + t;
   const uint64_t rl = n_upd - g0 < DEC_NT ? n_upd - g0 : DEC_NT;
   const uint64_t A = upd_off[g0], E = upd_off[g0 + rl];
-  const uint64_t sbase = A & ~3ull;
-  uint64_t nd = (E - sbase + 3) >> 2;
-  if (nd > DEC_STAGE / 4) nd = DEC_STAGE / 4;
-  const uint32_t *src = (const uint32_t *)(bytes + sbase);
-  for (uint32_t k = t; k < nd; k += DEC_NT) stage[k] = src[k];
+  // 16-byte loads, all issued before the first LDS store (one HBM round trip per lane)
+  const uint64_t sbase = A & ~15ull;
+  uint64_t n16 = (E - sbase + 15) >> 4;
+  if (n16 > DEC_STAGE / 16) n16 = DEC_STAGE / 16;
+  const uint64_t nd = 4 * n16;
+  {
+    constexpr uint32_t PL = DEC_STAGE / 16 / DEC_NT;
+    const uint4 *src = (const uint4 *)(bytes + sbase);
+    uint4 v[PL];
+#pragma unroll
+    for (uint32_t j = 0; j < PL; j++)
+      if (t + j * DEC_NT < n16) v[j] = src[t + j * DEC_NT];
+#pragma unroll
+    for (uint32_t j = 0; j < PL; j++)
+      if (t + j * DEC_NT < n16) ((uint4 *)stage)[t + j * DEC_NT] = v[j];
+  }
   if (t == 0) {
     ovf_top = 0;
     n_cx = 0;
