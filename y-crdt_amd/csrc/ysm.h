@@ -271,14 +271,24 @@ YM_INLINE void copy_window(uint8_t *dst, const uint8_t *src, uint32_t len) {
 // byte copy global -> (LDS stage or global) in groups of 16: the 16 byte loads of a group
 // are issued before any store (one memory latency per group), one instruction per byte
 // each way instead of the window's select tree per byte
+// Copies len bytes, 16 at a time: the (<= 5) aligned source dwords covering each 16-byte
+// piece are loaded together and realigned with alignbyte (5 loads instead of 16 byte loads
+// per piece); the destination is written bytewise (any alignment).  The source arena is
+// dword-aligned, so the covering dwords stay inside it.
 YM_INLINE void copy_bytes16(uint8_t *dst, const uint8_t *src, uint32_t len) {
+  const uint32_t mis = (uint32_t)((uintptr_t)src & 3);
+  const uint32_t *s4 = (const uint32_t *)(src - mis);
   for (uint32_t q0 = 0; q0 < len; q0 += 16) {
-    uint32_t x[16];
+    const uint32_t need = mis + len - q0; // bytes from the first covering dword on
+    uint32_t w[5];
 #pragma unroll
-    for (uint32_t k = 0; k < 16; k++) x[k] = q0 + k < len ? src[q0 + k] : 0u;
+    for (uint32_t k = 0; k < 5; k++) w[k] = 4 * k < need ? s4[(q0 >> 2) + k] : 0u;
+    uint32_t o[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) o[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], mis);
 #pragma unroll
     for (uint32_t k = 0; k < 16; k++)
-      if (q0 + k < len) dst[q0 + k] = (uint8_t)x[k];
+      if (q0 + k < len) dst[q0 + k] = (uint8_t)(o[k >> 2] >> (8 * (k & 3)));
   }
 }
 YM_INLINE bool equal_window(const uint8_t *a, const uint8_t *b, uint32_t len) {
