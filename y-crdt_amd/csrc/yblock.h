@@ -260,8 +260,11 @@ struct FastFill {
 
 // Writes one multi-record update (REC_COMPLEX) into its workgroup's overflow words:
 // [blocks: 5 words each (client, clock, length, position in update, meta)]
-// [entry clients] [ranges: 3 words each (start, end, entry index within the update)]
-// (the per-update table order of the entries is computed by k_fast_merge in LDS)
+// [entry clients] [entry table codes] [ranges: 3 words each (start, end, entry index
+// within the update)].  The table code is the entry's iteration position in the update's
+// DeleteSet HashMap | 0x80000000, or 0 if a later entry of the same client replaced it
+// (ds_order_packed, computed here at k_decode's occupancy rather than by one lane of the
+// merge workgroup).
 struct OvfFill {
   uint32_t *ov;
   uint32_t NBt, NEt; // totals of this update (RegSink pass)
@@ -285,13 +288,18 @@ struct OvfFill {
     return 0;
   }
   YM_INLINE void on_ds_range(uint32_t s0, uint32_t e0) {
-    uint32_t *w = ov + 5 * NBt + NEt + 3 * nr;
+    uint32_t *w = ov + 5 * NBt + 2 * NEt + 3 * nr;
     w[0] = s0;
     w[1] = e0;
     w[2] = ne - 1;
     nr++;
   }
-  YM_INLINE int on_ds_done() { return 0; }
+  YM_INLINE int on_ds_done() {
+    uint32_t *cl = ov + 5 * NBt;
+    if (ne == 1) cl[1] = 0x80000000u;
+    else if (ne >= 2) ds_order_packed(cl, ne, cl + ne, 0);
+    return 0;
+  }
 };
 
 // sink -> record (ykernels.h REC_*); positions stay relative to the update

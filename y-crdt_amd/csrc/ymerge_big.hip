@@ -619,10 +619,9 @@ __global__ void __launch_bounds__(NT) k_big_merge(BatchIn b, const uint32_t *cou
         ov += 5 * snb;
         for (uint32_t k = 0; k < sne; k++) {
           m.ec[pe + k] = ov[k];
-          m.et[pe + k] = 0x80000000u | (i << 8);
+          m.et[pe + k] = ov[sne + k] | (i << 8); // table code from k_decode
         }
-        if (sne >= 2) ds_order_packed(m.ec + pe, sne, m.et + pe, i << 8);
-        ov += sne;
+        ov += 2 * sne;
         for (uint32_t k = 0; k < snr; k++) {
           m.rs[pr + k] = ov[3 * k];
           m.re[pr + k] = ov[3 * k + 1];

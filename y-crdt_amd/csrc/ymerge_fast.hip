@@ -146,7 +146,7 @@ __global__ void __launch_bounds__(DEC_NT) k_decode(const uint8_t *bytes, const u
       // multi-record update: its records go to this workgroup's overflow words (LDS bump
       // allocation), written by the second walk below; if they do not fit, k_fast_merge
       // walks the update again
-      const uint32_t need = 5 * s.nb + s.ne + 3 * s.nr;
+      const uint32_t need = 5 * s.nb + 2 * s.ne + 3 * s.nr;
       const uint32_t off = need <= DEC_OVF ? atomicAdd(&ovf_top, need) : DEC_OVF;
       if (off + need <= DEC_OVF) {
         const uint32_t at = blockIdx.x * DEC_OVF + off;
@@ -343,7 +343,7 @@ __global__ void __launch_bounds__(NT, 3) k_fast_merge(BatchIn b, FastCaps caps, 
         }
       } else if (w0f & REC_OVF) { // multi-record update decoded by k_decode
         if (STAMPS) atomicAdd((unsigned long long *)&o.stamps[(size_t)blockIdx.x * 16 + 15],
-                              (unsigned long long)(5 * snb + sne + 3 * snr));
+                              (unsigned long long)(5 * snb + 2 * sne + 3 * snr));
         const uint32_t *ov = b.ovf + w4;
         {
           for (uint32_t k = 0; k < snb; k++) {
@@ -356,16 +356,15 @@ __global__ void __launch_bounds__(NT, 3) k_fast_merge(BatchIn b, FastCaps caps, 
           ov += 5 * snb;
           for (uint32_t k = 0; k < sne; k++) {
             ec[pe + k] = ov[k];
-            et[pe + k] = 0x80000000u | (i << 8);
+            et[pe + k] = ov[sne + k] | (i << 8); // table code from k_decode
           }
-          ov += sne;
+          ov += 2 * sne;
           for (uint32_t k = 0; k < snr; k++) {
             rs[pr + k] = ov[3 * k];
             re[pr + k] = ov[3 * k + 1];
             ri[pr + k] = pe + ov[3 * k + 2];
           }
         }
-        if (sne >= 2) ds_order_packed(ec + pe, sne, et + pe, i << 8);
       } else if (shape == REC_COMPLEX && !(flags & 2)) {
         // not a one-record shape: walk the update again over HBM at its scanned positions
         if (STAMPS) atomicAdd((unsigned long long *)&o.stamps[(size_t)blockIdx.x * 16 + 14], 1ull);
