@@ -183,11 +183,12 @@ def _ds_update(entries):
 
 def ds_heavy_docs(seed):
     """Documents whose updates carry many DeleteSet entries (around the 14-entry
-    in-register table and the former 64-entry limit), with repeated clients inside
+    in-register table, the 8 entries whose table codes k_decode packs into the record,
+    and the former 64-entry limit), with repeated clients inside
     one update (HashMap::insert replacement, id_set.rs decode)."""
     rng = np.random.default_rng(seed)
     docs = []
-    for n_ent in (2, 3, 13, 14, 15, 40, 56, 57, 64, 65, 120, 300):
+    for n_ent in (2, 3, 7, 8, 9, 13, 14, 15, 40, 56, 57, 64, 65, 120, 300):  # 8: packed table codes
         for rep in range(3):
             ups = []
             for _ in range(4):
