@@ -101,11 +101,14 @@ __host__ __device__ inline FastLayout fast_layout(const FastCaps &c) {
 // the fast walk's small register footprint.
 // Decoding here, rather than inside the per-document workgroup, runs the latency-bound
 // byte walk at full occupancy (16 KB LDS, no per-document phases holding registers).
-__global__ void __launch_bounds__(DEC_NT) k_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_upd,
-                                                   uint32_t *rec, uint32_t *ovf) {
+// 8 workgroups per CU (8 waves per SIMD): <= 64 VGPRs and < 20 KB of LDS (the second-walk
+// list keeps 16-bit lane / count fields)
+__global__ void __launch_bounds__(DEC_NT, 8) k_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_upd,
+                                                      uint32_t *rec, uint32_t *ovf) {
   __shared__ __align__(16) uint32_t stage[DEC_STAGE / 4 + 4];
   __shared__ uint32_t ovf_top, n_cx;
-  __shared__ uint32_t cx_lane[DEC_NT], cx_at[DEC_NT], cx_nb[DEC_NT], cx_ne[DEC_NT];
+  __shared__ uint32_t cx_at[DEC_NT];
+  __shared__ uint16_t cx_lane[DEC_NT], cx_nb[DEC_NT], cx_ne[DEC_NT];
   const uint64_t g0 = (uint64_t)blockIdx.x * DEC_NT;
   const uint32_t t = threadIdx.x;
   const uint64_t i = g0 + t;
@@ -155,8 +158,8 @@ __global__ void __launch_bounds__(DEC_NT) k_decode(const uint8_t *bytes, const u
         const uint32_t q = atomicAdd(&n_cx, 1u);
         cx_lane[q] = t;
         cx_at[q] = at;
-        cx_nb[q] = s.nb;
-        cx_ne[q] = s.ne;
+        cx_nb[q] = (uint16_t)s.nb; // need <= DEC_OVF words: counts < 2^16
+        cx_ne[q] = (uint16_t)s.ne;
       }
     }
     uint2 *o = (uint2 *)(rec + i * REC_WORDS);
