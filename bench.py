@@ -190,8 +190,10 @@ def run_merge(a, rank, world, dev):
     _, _, st = res.to_host()
     n_err = int((st != 0).sum())
     mean = lambda k: float(np.mean([s[k] for s in kstats]))  # noqa: E731
-    ms_decode, ms_fast, ms_big, ms_exact = mean("ms_decode"), mean("ms_fast"), mean("ms_big"), mean("ms_exact")
-    ms_pipe = ms_decode + ms_fast + ms_big + ms_exact
+    ms_lean, ms_decode, ms_fast = mean("ms_lean"), mean("ms_decode"), mean("ms_fast")
+    ms_big, ms_exact = mean("ms_big"), mean("ms_exact")
+    ms_pipe = ms_lean + ms_decode + ms_fast + ms_big + ms_exact
+    docs_lean = int(kstats[-1]["docs_lean"])
     docs_exact, docs_big = int(kstats[-1]["docs_exact"]), int(kstats[-1]["docs_big"])
     docs_tiny = int(kstats[-1]["docs_tiny"])
 
@@ -217,8 +219,9 @@ def run_merge(a, rank, world, dev):
     t_max = float(allst[:, 4].max())
     docs_total = float(allst[:, 0].sum()) * a.steps
     bytes_in_total = float(allst[:, 1].sum()) * a.steps
-    # roofline of the merge pipeline (k_decode -> k_fast_merge -> exact engine for handed-over
-    # documents; together they are the path), algorithmic bytes = input + output
+    # roofline of the merge pipeline (k_lean -> k_decode + k_fast_merge for the documents it
+    # hands over -> tiled / exact engines; together they are the path), algorithmic bytes =
+    # input + output
     alg_bytes = batch.n_bytes + out_bytes
     achieved = alg_bytes / (ms_pipe * 1e-3) / 1e9
     cpu = None
@@ -236,7 +239,8 @@ def run_merge(a, rank, world, dev):
                        **cfg),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(a.workload),
-                     "kernel": "k_decode+k_fast_merge(+k_big_merge, exact engine)", "kernel_ms": ms_pipe,
+                     "kernel": "k_lean(+k_decode+k_fast_merge, k_big_merge, exact engine)", "kernel_ms": ms_pipe,
+                     "k_lean_ms": ms_lean, "docs_lean": docs_lean,
                      "k_decode_ms": ms_decode, "k_fast_merge_ms": ms_fast, "big_path_ms": ms_big,
                      "exact_path_ms": ms_exact, "docs_big_path": docs_big, "docs_exact_path": docs_exact,
                      "docs_tiny_path": docs_tiny,

@@ -86,6 +86,8 @@ typedef struct {
   uint64_t docs_tiny; /* merge: documents of <= 4 updates (<= 4 KB) written one lane each by the
                          lane-per-document engine (not counted in docs_exact) */
   float ms_tiny;      /* merge: exact-engine stage time when it ran tiny documents only */
+  uint64_t docs_lean; /* merge: documents written by k_lean (one wavefront each; not in docs_fast) */
+  float ms_lean;      /* merge: k_lean (ms_decode / ms_fast then time the documents it handed over) */
 } ymerge_stats;
 
 /* Device-resident result, owned by the context, valid until the next batch.

@@ -134,14 +134,25 @@ def test_exact_engine_only(oracle):
         e.close()
 
 
-@pytest.mark.parametrize("threads", ["512", "1024"])
-def test_fast_path_workgroup_sizes(oracle, threads):
+def engine_with(**env):
+    """An Engine created under the given YMERGE_* environment knobs (read at creation)."""
     import ymerge
-    os.environ["YMERGE_FAST_THREADS"] = threads
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
     try:
-        e = ymerge.Engine(0)
+        return ymerge.Engine(0)
     finally:
-        del os.environ["YMERGE_FAST_THREADS"]
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("threads", ["256", "512", "1024"])
+def test_fast_path_workgroup_sizes(oracle, threads):
+    """k_decode + k_fast_merge alone (k_lean off) at every workgroup size."""
+    e = engine_with(YMERGE_FAST_THREADS=threads, YMERGE_LEAN=0)
     try:
         check_batch(e, oracle, workloads.text_docs(150, 1000, seed=11))
     finally:
@@ -149,10 +160,21 @@ def test_fast_path_workgroup_sizes(oracle, threads):
 
 
 def test_fast_path_coverage(engine, oracle):
-    """C2 documents must stay on the fast path (no silent exact-engine fallback)."""
+    """C2 documents must all be written by k_lean (no silent hand-over to the slower paths)."""
     check_batch(engine, oracle, workloads.text_docs(500, 1000, seed=21))
     st = engine.stats()
-    assert st["docs_exact"] == 0 and st["docs_fast"] == 500
+    assert st["docs_exact"] == 0 and st["docs_lean"] == 500 and st["docs_fast"] == 0
+
+
+def test_fast_path_coverage_without_lean(oracle):
+    """With k_lean off, C2 documents stay on k_fast_merge (no exact-engine fallback)."""
+    e = engine_with(YMERGE_LEAN=0)
+    try:
+        check_batch(e, oracle, workloads.text_docs(300, 1000, seed=21))
+        st = e.stats()
+        assert st["docs_exact"] == 0 and st["docs_fast"] == 300 and st["docs_lean"] == 0
+    finally:
+        e.close()
 
 
 def test_c1_automerge_trace(engine, oracle):

@@ -15,6 +15,7 @@ struct BatchIn {
   const uint32_t *rec; // per-update decode records (k_decode), REC_WORDS u32 each; fast path only
   const uint32_t *ovf; // their overflow words (DEC_OVF per decode workgroup)
   uint32_t v1x = 0;    // bytes are the internal v1x grammar (lib0 v2 path), not lib0 v1
+  uint32_t only_path3 = 0; // k_fast_merge: only the documents k_lean handed over (path == 3)
 };
 
 // Per-update decode record written by k_decode (one lane per update over the whole
@@ -45,9 +46,12 @@ struct FastOut {
   uint64_t *stamps; // diagnostic build only: s_memtime per phase (16 per document)
   uint32_t *npath;  // npath[p]: documents handed to path p (1 exact engine, 2 tiled kernel); [3] tiled
                     // kernel in overlap mode, [4] tiled kernel -> exact engine, [5] of [1]:
-                    // tiny documents (FastCaps.in_cap / u_cap)
+                    // tiny documents (FastCaps.in_cap / u_cap), [6] k_lean -> fast path
 };
 size_t fast_lds_bytes(const FastCaps &c);
+// one wavefront per document for the common editor shape (ymerge_lean.hip): writes the
+// document (path 0) or hands it to k_decode + k_fast_merge (path 3, counted in npath[6])
+void launch_lean(const BatchIn &b, const FastOut &o, hipStream_t s);
 void launch_fast_merge(const BatchIn &b, const FastCaps &caps, const FastOut &o, int nt, hipStream_t s);
 
 // documents over the fast path's LDS capacities (path == 2): tiled, HBM scratch

@@ -205,6 +205,7 @@ __global__ void __launch_bounds__(NT, 3) k_fast_merge(BatchIn b, FastCaps caps, 
   const FastLayout L = fast_layout(caps);
   const uint32_t d = blockIdx.x;
   if (d >= b.n_docs) return;
+  if (b.only_path3 && o.path[d] != 3) return; // written by k_lean
   const uint32_t t = threadIdx.x;
   uint32_t *misc = (uint32_t *)(smem + L.misc);
   // misc[0] err key, [1] flags, [2..] scan workspace (NT/64*2+2 words), [64..] scalars

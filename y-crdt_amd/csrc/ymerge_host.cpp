@@ -59,12 +59,13 @@ struct ymerge_ctx {
   DevBuf v2x, v2x_sz, v2x_off, v2_ust, v2_out, v2_osz, v2_ooff, v2_svoff, v2_svend, v2_pre;
   bool want_stamps = false;
   uint64_t *h_pinned = nullptr;
-  hipEvent_t ev[8];
+  hipEvent_t ev[10];
   ymerge_stats stats{};
   uint64_t stamps_docs = 0; // documents covered by `stamps` (last merge batch)
   // tiny-document updates / bytes, blocks (must equal FAST_BCAP, ymerge_fast.hip), DS entries, DS ranges
   ym::FastCaps caps{4, 4096, 1024, 512, 512};
   int fast_threads = 256;
+  bool lean = true; // k_lean first (env YMERGE_LEAN=0: every document through k_decode + k_fast_merge)
   std::mutex mu;
 };
 
@@ -82,6 +83,7 @@ static bool ctx_init(ymerge_ctx *c, int device) {
   if (const char *v = getenv("YMERGE_FAST_THREADS")) c->fast_threads = atoi(v);
   if (const char *v = getenv("YMERGE_STAMPS")) c->want_stamps = atoi(v) != 0;
   if (const char *v = getenv("YMERGE_TINY")) c->caps.in_cap = (uint32_t)atoi(v); // 0: no tiny path
+  if (const char *v = getenv("YMERGE_LEAN")) c->lean = atoi(v) != 0;
   // the fast kernel's LDS layout must fit one workgroup (160 KB on gfx950)
   int lds_max = 0;
   if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess) return false;
@@ -162,7 +164,6 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   uint64_t *ostart = c->out_start.as<uint64_t>(), *olen = c->out_len.as<uint64_t>();
   uint8_t *status = c->status.as<uint8_t>(), *path = c->path.as<uint8_t>();
   hipMemsetAsync(c->counter.p, 0, 64, c->s);
-  hipEventRecord(c->ev[0], c->s);
   uint64_t *stamps = nullptr;
   if (c->want_stamps) {
     if (!c->stamps.ensure(nn * 16 * 8)) return YMERGE_ERR_DEVICE;
@@ -171,7 +172,22 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     c->stamps_docs = n_docs;
   }
   ym::FastOut fo{arena, ostart, olen, status, path, stamps, c->counter.as<uint32_t>() + 4};
-  if (c->fast_threads) {
+  // k_lean: one wavefront per document for the common shape; the rest (path 3) goes on to
+  // k_decode + k_fast_merge, which are skipped when k_lean wrote every document
+  const bool lean = c->lean && c->fast_threads && !c->want_stamps;
+  uint32_t n_rej = n;
+  hipEventRecord(c->ev[7], c->s);
+  if (lean) {
+    ym::launch_lean(b, fo, c->s);
+    if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
+    hipMemcpyAsync(c->h_pinned + 16, c->counter.as<uint32_t>() + 10, 4, hipMemcpyDeviceToHost, c->s);
+    if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
+    n_rej = (uint32_t)(c->h_pinned[16] & 0xFFFFFFFFu);
+    b.only_path3 = 1;
+  }
+  hipEventRecord(c->ev[0], c->s);
+  const bool fast = c->fast_threads && n_rej > 0;
+  if (fast) {
     ym::launch_decode(d_bytes, d_upd_off, n_updates, c->rec.as<uint32_t>(), c->ovf.as<uint32_t>(), c->s);
     hipEventRecord(c->ev[5], c->s);
     ym::launch_fast_merge(b, c->caps, fo, c->fast_threads, c->s);
@@ -181,12 +197,12 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   else {
     hipEventRecord(c->ev[5], c->s);
     hipEventRecord(c->ev[6], c->s);
-    hipMemsetAsync(path, 1, n, c->s);
+    if (!c->fast_threads) hipMemsetAsync(path, 1, n, c->s);
   }
   // hand-over counts of the fast path (npath[1] exact engine, npath[2] tiled kernel): the
   // later stages are skipped when no document needs them
-  uint32_t n_p1 = n, n_p2 = 0;
-  if (c->fast_threads) {
+  uint32_t n_p1 = c->fast_threads ? 0 : n, n_p2 = 0;
+  if (fast) {
     hipMemcpyAsync(c->h_pinned + 12, c->counter.as<uint32_t>() + 4, 16, hipMemcpyDeviceToHost, c->s);
     if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
     const uint32_t *np = (const uint32_t *)(c->h_pinned + 12);
@@ -195,7 +211,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   }
   // documents over the LDS capacities (path == 2): count, scratch offsets, tiled kernel
   uint32_t n_big = 0;
-  if (c->fast_threads && n_p2) {
+  if (fast && n_p2) {
     ym::launch_big_count(b, fo, c->counts.as<uint32_t>(), c->need.as<uint64_t>(), c->counter.as<uint32_t>() + 2, c->s);
     ym::launch_scan_u64(c->need.as<uint64_t>(), c->scr_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
     hipMemcpyAsync(c->h_pinned + 10, c->scr_off.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, c->s);
@@ -249,23 +265,26 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   uint64_t total = 0;
   if (!read_words(c, c->pack_off.as<uint64_t>() + n, 8, &total)) return YMERGE_ERR_DEVICE;
   if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
-  float t01 = 0, t12 = 0, t23 = 0, t03 = 0, t05 = 0, t61 = 0;
+  float t01 = 0, t12 = 0, t23 = 0, t03 = 0, t05 = 0, t61 = 0, t70 = 0;
+  hipEventElapsedTime(&t70, c->ev[7], c->ev[0]);
   hipEventElapsedTime(&t05, c->ev[0], c->ev[5]);
   hipEventElapsedTime(&t01, c->ev[5], c->ev[6]);
   hipEventElapsedTime(&t61, c->ev[6], c->ev[1]);
   hipEventElapsedTime(&t12, c->ev[1], c->ev[2]);
   hipEventElapsedTime(&t23, c->ev[2], c->ev[3]);
-  hipEventElapsedTime(&t03, c->ev[0], c->ev[3]);
+  hipEventElapsedTime(&t03, c->ev[7], c->ev[3]);
   c->stats = ymerge_stats{};
   c->stats.n_docs = n_docs;
   c->stats.bytes_in = n_bytes;
+  c->stats.docs_lean = lean ? n_docs - n_rej : 0;
+  c->stats.ms_lean = lean ? t70 : 0.0f;
   c->stats.bytes_out = total;
   c->stats.docs_exact = n_exact - n_tiny;
   c->stats.docs_tiny = n_tiny;
   c->stats.ms_tiny = n_exact == n_tiny ? t12 : 0.0f;
   c->stats.docs_big = n_big;
   c->stats.docs_overlap = n_overlap;
-  c->stats.docs_fast = n_docs - n_exact - n_big;
+  c->stats.docs_fast = n_docs - n_exact - n_big - c->stats.docs_lean;
   c->stats.ms_big = t61;
   c->stats.ms_fast = t01;
   c->stats.ms_exact = t12;

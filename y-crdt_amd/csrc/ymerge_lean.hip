@@ -1,0 +1,807 @@
+// ymerge_lean.hip — merge_updates_v1 for documents of the common editor shape: ONE
+// WAVEFRONT per document, decode + placement + copy + DeleteSet union in a single pass,
+// nothing round-tripped through HBM but the input and output bytes.
+//
+// Shape handled (everything else is handed to k_decode + k_fast_merge, path 3):
+//   * every update is one client section with at most one block (Item with a Deleted or
+//     ASCII String content, or a GC), or no section at all, plus a DeleteSet of at most 4
+//     entries with distinct clients, non-empty ranges;
+//   * per client, the blocks in input order are contiguous in clock (each starts where the
+//     previous block of that client ended) — exactly the logs a sync server accumulates
+//     from editors that ship one transaction per update;
+//   * <= 16 distinct clients, document < 64 KB, every block < 1 KB, canonical encodings.
+// For such a document yrs' merge (yrs/src/update.rs:537-704) reduces to: clients in
+// descending order, each client's blocks verbatim in input order behind one section
+// header (count, client, first clock), then the union of all DeleteSets
+// (id_set.rs:129-164, 385-395) in the hashbrown order of first insertion
+// (update.rs:542-548, std HashMap + ClientHasher).  Nothing is sorted, split or squashed.
+//
+// Per document (one wave, 64 lanes, no s_barrier):
+//   1 decode, rounds of <= 64 updates: the round's bytes are staged into LDS with 16-byte
+//     loads (the next round's bytes and offsets are already in flight), each lane walks one
+//     update (ylds.h branch-free varints); clients -> buckets (LDS hash); per bucket the
+//     contiguity check (ballot over the bucket's lanes, predecessor's end by lane shuffle),
+//     counts and byte totals (LDS atomics); a 4-byte record per block (doc-relative source
+//     offset, byte length, bucket); DeleteSet ranges to the top of the same arena.
+//   2 layout: section order (client desc) and starts, section headers written.
+//   3 copy: blocks in input order, <= 64 per step: their source bytes staged again with
+//     16-byte loads, per-bucket prefix of byte lengths -> destination, LDS -> HBM stores
+//     (dword stores for the aligned middle, byte stores at the two ends).
+//   4 DeleteSet: bitmap union per client window in LDS (the arena is free by now), runs ->
+//     components, sizes, hashbrown client order (one lane, <= 16 clients), write.
+#include "ycodec.h"
+#include "ykernels.h"
+#include "ylds.h"
+#include "ywalk.h"
+
+namespace ym {
+
+constexpr uint32_t LN_STAGE = 1536;          // staged bytes per round / copy step
+constexpr uint32_t LN_SW = LN_STAGE / 4 + 4; // stage words (+ the word after the last one lvar reads)
+constexpr uint32_t LN_AW = 1792;             // arena words: block records grow up, DS ranges down
+constexpr uint32_t LN_BUF = LN_SW + LN_AW;   // stage + arena, reused whole by the DeleteSet phase
+constexpr uint32_t LN_NBK = 16;              // client buckets per document
+constexpr uint32_t LN_HT = 32;               // client hash slots
+constexpr uint32_t LN_MAXBLEN = 1024;        // block bytes (a copy step must always fit one block)
+constexpr uint32_t LN_NONE = 0xFFFFFFFFu;
+
+struct LeanLds {
+  uint32_t buf[LN_BUF];
+  uint64_t ht[LN_HT]; // client << 32 | (bucket + 1); 0 = empty
+  uint32_t client[LN_NBK], cnt[LN_NBK], first[LN_NBK], next[LN_NBK], bytes[LN_NBK];
+  uint32_t dsfirst[LN_NBK], dsmin[LN_NBK], dsmax[LN_NBK], cur[LN_NBK], eoff[LN_NBK];
+  uint32_t ord[LN_NBK], slots[2 * 2 * LN_NBK]; // DeleteSet client order (table emulation scratch)
+};
+
+// ------------------------------------------------------------------ wave primitives
+YM_INLINE void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+YM_INLINE uint32_t lanes_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+YM_INLINE uint32_t rdlane(uint32_t x, uint32_t l) { return __builtin_amdgcn_readlane(x, l); }
+YM_INLINE uint64_t rdlane64(uint64_t x, uint32_t l) {
+  return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(x >> 32), l) << 32) | __builtin_amdgcn_readlane((uint32_t)x, l);
+}
+// inclusive sum over the wave
+YM_INLINE uint32_t wincl(uint32_t x, uint32_t lane) {
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  return x;
+}
+// number of leading set bits of a lane mask (lanes 0.. that all satisfy a predicate)
+YM_INLINE uint32_t lead_ones(uint64_t m) { return m == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~m); }
+
+// ------------------------------------------------------------------ one update
+struct LeanUpd {
+  uint32_t has_blk, client, clock, len, bpos, blen; // block; bpos = stage byte position
+  uint32_t dspos, nent, nrng;                       // DeleteSet: stage position, entries, ranges
+  uint32_t c0, c1, c2, c3;                          // entry clients (stream order)
+};
+
+// Validating walk of one staged update (Update::decode_v1, yrs/src/update.rs:714-749,
+// decode_block :433-488, ItemContent::decode block.rs:1786-1835, IdSet::decode
+// id_set.rs:412-426) restricted to the lean shape; false = not the shape (or malformed:
+// the exact walk downstream owns the error codes).
+YM_INLINE bool lean_walk(const uint32_t *w, uint32_t start, uint32_t n, LeanUpd &r) {
+  LCur c{w, start, start + n};
+  bool cn;
+  uint32_t ncl, v;
+  r.has_blk = 0;
+  r.nent = r.nrng = 0;
+  r.c0 = r.c1 = r.c2 = r.c3 = 0;
+  if (!lvar(c, ncl, cn) || ncl > 1) return false;
+  if (ncl == 1) {
+    uint32_t nb, client, clock;
+    if (!lvar(c, nb, cn) || nb > 1 || !lvar(c, client, cn) || !lvar(c, clock, cn)) return false;
+    if (nb == 1) {
+      const uint32_t bpos = c.p;
+      if (c.p >= c.end) return false;
+      const uint32_t info = lds_byte(w, c.p++);
+      uint32_t len = 0;
+      bool keep = true;
+      if (info == 0 || info == 10) { // GC / Skip: canonical non-zero length
+        if (!lvar(c, len, cn) || !cn || len == 0) return false;
+        keep = info == 0; // a Skip is dropped by IntoBlocks (update.rs:1054)
+      } else {
+        // origin / right origin / parent, as fast_walk (ylds.h); any re-encoding -> not lean
+        bool ok = true;
+        if (info & 0x80) ok = lvar(c, v, cn) && cn && lvar(c, v, cn) && cn;
+        if (ok && (info & 0x40)) ok = lvar(c, v, cn) && cn && lvar(c, v, cn) && cn;
+        if (!ok) return false;
+        uint32_t want = info & 0xCF;
+        if ((info & 0xC0) == 0) {
+          uint32_t pi;
+          if (!lvar(c, pi, cn) || !cn || pi > 1) return false;
+          if (!lvar(c, v, cn) || !cn) return false;
+          if (pi == 1) {
+            if (v > c.end - c.p) return false;
+            c.p += v;
+          } else if (!lvar(c, v, cn) || !cn) {
+            return false;
+          }
+          if (info & 0x20) {
+            want |= 0x20;
+            if (!lvar(c, v, cn) || !cn || v > c.end - c.p) return false;
+            c.p += v;
+          }
+        }
+        if (want != info) return false;
+        const uint32_t ref = info & 15;
+        if (ref == 1) {
+          if (!lvar(c, len, cn) || !cn) return false;
+        } else if (ref == 4) {
+          if (!lvar(c, v, cn) || !cn || v > c.end - c.p) return false;
+          const uint32_t s0 = c.p;
+          c.p += v;
+          if (v > 1) { // UTF-16 length == byte length for ASCII only
+            uint32_t hi = 0;
+            const uint32_t e0 = s0 + v, q0 = s0 >> 2, q1 = (e0 - 1) >> 2;
+            for (uint32_t q = q0; q <= q1; q++) {
+              uint32_t x = w[q];
+              if (q == q0) x &= 0xFFFFFFFFu << (8 * (s0 & 3));
+              if (q == q1 && (e0 & 3)) x &= 0xFFFFFFFFu >> (8 * (4 - (e0 & 3)));
+              hi |= x;
+            }
+            if (hi & 0x80808080u) return false;
+          }
+          len = v;
+        } else {
+          return false;
+        }
+        keep = len != 0; // Item::new drops zero-length items
+      }
+      if (keep) {
+        if ((uint64_t)clock + len > 0xFFFFFFFFull || c.p - bpos > LN_MAXBLEN) return false;
+        r.has_blk = 1;
+        r.client = client;
+        r.clock = clock;
+        r.len = len;
+        r.bpos = bpos;
+        r.blen = c.p - bpos;
+      }
+    }
+  }
+  r.dspos = c.p;
+  uint32_t nds;
+  if (!lvar(c, nds, cn) || nds > 4) return false;
+  for (uint32_t e = 0; e < nds; e++) {
+    uint32_t client, nr;
+    if (!lvar(c, client, cn) || !lvar(c, nr, cn) || nr == 0 || nr > n) return false;
+    // a repeated client replaces the earlier entry (IdSet::decode inserts): not lean
+    if ((e > 0 && r.c0 == client) || (e > 1 && r.c1 == client) || (e > 2 && r.c2 == client)) return false;
+    if (e == 0) r.c0 = client;
+    else if (e == 1) r.c1 = client;
+    else if (e == 2) r.c2 = client;
+    else r.c3 = client;
+    for (uint32_t q = 0; q < nr; q++) {
+      uint32_t st, ln;
+      if (!lvar(c, st, cn) || !lvar(c, ln, cn)) return false;
+      if (ln == 0 || ln >= (1u << 28) || (uint64_t)st + ln > 0xFFFFFFFFull) return false;
+    }
+    r.nrng += nr;
+  }
+  r.nent = nds;
+  return true;
+}
+
+YM_INLINE uint32_t sel4(uint32_t i, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  return i == 0 ? a : i == 1 ? b : i == 2 ? c : d;
+}
+// Iteration positions of <= 4 distinct DeleteSet entries in their update's HashMap
+// (IdSet::decode inserts each in stream order; reserve(1) grows 0 -> 4 -> 8 buckets and
+// re-places the old entries in slot order) — ds_order_packed (ywalk.h) in registers.
+YM_INLINE void ds_pos4(uint32_t n, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t &p0, uint32_t &p1,
+                       uint32_t &p2, uint32_t &p3) {
+  uint64_t map = 0;
+  uint32_t buckets = 0, items = 0, growth = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    if (growth == 0) {
+      const uint32_t full = buckets ? (uint32_t)mask_to_cap(buckets - 1) : 0;
+      const uint32_t need = items + 1;
+      const uint32_t nb = (uint32_t)cap_to_buckets(need > full + 1 ? need : full + 1);
+      uint64_t nm = 0;
+      for (uint32_t s = 0; s < buckets; s++) {
+        const uint32_t en = (uint32_t)(map >> (4 * s)) & 15;
+        if (en) nm |= (uint64_t)en << (4 * hb_probe(nm, nb, sel4(en - 1, c0, c1, c2, c3)));
+      }
+      map = nm;
+      buckets = nb;
+      growth = (uint32_t)mask_to_cap(nb - 1) - items;
+    }
+    map |= (uint64_t)(i + 1) << (4 * hb_probe(map, buckets, sel4(i, c0, c1, c2, c3)));
+    items++;
+    growth--;
+  }
+  uint32_t k = 0;
+  p0 = p1 = p2 = p3 = 0;
+  for (uint32_t s = 0; s < buckets; s++) {
+    const uint32_t en = (uint32_t)(map >> (4 * s)) & 15;
+    if (en == 1) p0 = k++;
+    else if (en == 2) p1 = k++;
+    else if (en == 3) p2 = k++;
+    else if (en == 4) p3 = k++;
+  }
+}
+
+// ------------------------------------------------------------------ client buckets
+YM_INLINE int ht_find(const uint64_t *ht, uint32_t c) {
+  uint32_t h = (c * 0x9E3779B9u) >> 27;
+  for (uint32_t p = 0; p < LN_HT; p++) {
+    const uint64_t v = ht[h];
+    if (!v) return -1;
+    if ((uint32_t)(v >> 32) == c) return (int)(uint32_t)v - 1;
+    h = (h + 1) & (LN_HT - 1);
+  }
+  return -1;
+}
+// bucket of client c for the lanes with `want`; unknown clients are inserted one per
+// iteration (uniform loop).  false = more than LN_NBK clients.
+YM_INLINE bool bucket_of(LeanLds &L, uint32_t lane, uint32_t c, bool want, uint32_t &nbk, int &bk) {
+  bk = want ? ht_find(L.ht, c) : 0;
+  for (;;) {
+    const uint64_t m = __ballot(want && bk < 0);
+    if (!m) return true;
+    if (nbk == LN_NBK) return false;
+    const uint32_t cn = rdlane(c, (uint32_t)__builtin_ctzll(m));
+    if (lane == 0) {
+      uint32_t h = (cn * 0x9E3779B9u) >> 27;
+      while (L.ht[h]) h = (h + 1) & (LN_HT - 1);
+      L.ht[h] = ((uint64_t)cn << 32) | (nbk + 1);
+      L.client[nbk] = cn;
+    }
+    wsync();
+    if (want && bk < 0 && c == cn) bk = (int)nbk;
+    nbk++;
+  }
+}
+
+// ------------------------------------------------------------------ LDS -> HBM byte copy
+// n bytes from staged byte position so to dp: byte stores up to dp's dword alignment, dword
+// stores (two staged dwords aligned by v_alignbyte) for the middle, byte stores for the tail.
+YM_INLINE void copy_out(const uint32_t *st, uint32_t so, uint8_t *dp, uint32_t n) {
+  const uint8_t *sb = (const uint8_t *)st;
+  uint32_t head = (uint32_t)(0u - (uint32_t)(uintptr_t)dp) & 3u;
+  if (head > n) head = n;
+  for (uint32_t q = 0; q < head; q++) dp[q] = sb[so + q];
+  uint32_t p = so + head, rem = n - head;
+  uint8_t *dq = dp + head;
+  if (rem >= 4) {
+    const uint32_t sh = p & 3;
+    uint32_t q4 = p >> 2, lo = st[q4];
+    for (; rem >= 4; rem -= 4) {
+      const uint32_t hi = st[++q4];
+      *(uint32_t *)dq = __builtin_amdgcn_alignbyte(hi, lo, sh);
+      lo = hi;
+      dq += 4;
+      p += 4;
+    }
+  }
+  for (uint32_t q = 0; q < rem; q++) dq[q] = sb[p + q];
+}
+
+// 16-byte staging of absolute bytes [al, al + 16 * n16) (n16 <= LN_STAGE / 16) into buf
+YM_INLINE void stage_load(const uint8_t *bytes, uint64_t al, uint32_t n16, uint32_t lane, uint4 &v0, uint4 &v1) {
+  const uint4 *src = (const uint4 *)(bytes + al);
+  if (lane < n16) v0 = src[lane];
+  if (lane + 64 < n16) v1 = src[lane + 64];
+}
+YM_INLINE void stage_store(uint32_t *buf, uint32_t n16, uint32_t lane, const uint4 &v0, const uint4 &v1) {
+  if (lane < n16) ((uint4 *)buf)[lane] = v0;
+  if (lane + 64 < n16) ((uint4 *)buf)[lane + 64] = v1;
+}
+
+// DeleteSet client order: IdSet::merge (id_set.rs:385-395) inserts the clients of every
+// update's table into the result table in first-occurrence order (update.rs:542-548);
+// std's hashbrown with the identity ClientHasher (utils/client_hasher.rs) then iterates
+// in slot order.  Restated as k_fast_merge's emulation (ymerge_fast.hip, phase 5b) for
+// <= LN_NBK clients.  ord[] receives the buckets in iteration order; returns D.
+__device__ __noinline__ uint32_t lean_ds_order(uint32_t nbk, const uint32_t *client, const uint32_t *dsfirst,
+                                               uint32_t *ord, uint32_t *slot_arr) {
+  uint32_t D = 0;
+  for (uint32_t b = 0; b < nbk; b++) {
+    if (dsfirst[b] == LN_NONE) continue;
+    uint32_t j = D++;
+    while (j > 0 && dsfirst[ord[j - 1]] > dsfirst[b]) {
+      ord[j] = ord[j - 1];
+      j--;
+    }
+    ord[j] = b;
+  }
+  uint32_t *tmp = slot_arr + 2 * LN_NBK;
+  uint32_t buckets = 0, items = 0, growth = 0;
+  auto ctrl_empty = [&](uint32_t idx) -> bool {
+    if (idx < buckets) return slot_arr[idx] == 0;
+    if (buckets < 16) return idx < 16 ? true : slot_arr[idx - 16] == 0;
+    return slot_arr[idx - buckets] == 0;
+  };
+  auto find_slot = [&](uint32_t key) -> uint32_t {
+    const uint32_t mask = buckets - 1;
+    uint32_t pos = key & mask, stride = 0;
+    for (;;) {
+      for (uint32_t j = 0; j < 16; j++) {
+        if (ctrl_empty(pos + j)) {
+          const uint32_t index = (pos + j) & mask;
+          if (slot_arr[index] != 0)
+            for (uint32_t k = 0; k < buckets; k++)
+              if (slot_arr[k] == 0) return k;
+          return index;
+        }
+      }
+      stride += 16;
+      pos = (pos + stride) & mask;
+    }
+  };
+  for (uint32_t i = 0; i < D; i++) {
+    if (growth == 0) {
+      const uint64_t full = buckets ? mask_to_cap(buckets - 1) : 0;
+      const uint64_t need = items + 1;
+      const uint32_t nb = (uint32_t)cap_to_buckets(need > full + 1 ? need : full + 1); // <= 32 for 16 items
+      const uint32_t ob = buckets;
+      for (uint32_t q = 0; q < ob; q++) tmp[q] = slot_arr[q];
+      buckets = nb;
+      for (uint32_t q = 0; q < buckets; q++) slot_arr[q] = 0;
+      for (uint32_t q = 0; q < ob; q++)
+        if (tmp[q]) slot_arr[find_slot(client[tmp[q] - 1])] = tmp[q];
+      growth = (uint32_t)mask_to_cap(buckets - 1) - items;
+    }
+    slot_arr[find_slot(client[ord[i]])] = ord[i] + 1;
+    items++;
+    growth--;
+  }
+  uint32_t k = 0;
+  for (uint32_t q = 0; q < buckets; q++)
+    if (slot_arr[q]) ord[k++] = slot_arr[q] - 1;
+  return D;
+}
+
+// ------------------------------------------------------------------ the kernel
+template <int WPB> __global__ void __launch_bounds__(64 * WPB) k_lean(BatchIn b, FastOut o) {
+  __shared__ LeanLds lds[WPB];
+  const uint32_t lane = __lane_id();
+  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t d = blockIdx.x * WPB + w;
+  if (d >= b.n_docs) return;
+  LeanLds &L = lds[w];
+  const uint64_t u0 = b.doc_upd[d], u1 = b.doc_upd[d + 1];
+  const uint64_t B0 = b.upd_off[u0], B1 = b.upd_off[u1];
+  const uint32_t U = (uint32_t)(u1 - u0);
+  const uint64_t slot = 2 * B0 + 64ull * d;
+  uint8_t *out = o.out + slot;
+  auto reject = [&]() {
+    if (lane == 0) {
+      o.path[d] = 3;
+      atomicAdd(&o.npath[6], 1u);
+    }
+  };
+  if (U == 0 || B1 - B0 >= 65536 || u1 - u0 >= 65536) {
+    reject();
+    return;
+  }
+  if (lane < LN_HT) L.ht[lane] = 0;
+  if (lane < LN_NBK) {
+    L.cnt[lane] = L.bytes[lane] = 0;
+    L.dsfirst[lane] = L.dsmin[lane] = LN_NONE;
+    L.dsmax[lane] = 0;
+  }
+  wsync();
+
+  // ---------------------------------------------------------------- 1 decode
+  uint32_t nbk = 0, NBk = 0, NR = 0, blkmask = 0;
+  bool bad = false;
+  uint32_t ub = 0;
+  uint64_t A = B0;
+  // round pipeline: offsets of the round's updates (e = end of update ub + lane), its
+  // staged bytes; the next round's are loaded while this one is walked
+  uint64_t e = lane < U ? b.upd_off[u0 + 1 + lane] : 0;
+  uint64_t en = lane + 64 < U ? b.upd_off[u0 + 65 + lane] : 0; // the 64 after
+  uint32_t k, n16;
+  uint64_t al = A & ~15ull, E;
+  {
+    const uint64_t fm = __ballot(lane < U && e - al <= LN_STAGE);
+    k = lead_ones(fm);
+    if (k == 0) {
+      reject();
+      return;
+    }
+    E = rdlane64(e, k - 1);
+    n16 = (uint32_t)((E - al + 15) >> 4);
+  }
+  uint4 v0, v1;
+  stage_load(b.bytes, al, n16, lane, v0, v1);
+  while (ub < U) {
+    const uint64_t s = lane == 0 ? A : __shfl_up(e, 1, 64);
+    const bool act = lane < k;
+    const uint32_t i = ub + lane; // doc-relative update index
+    stage_store(L.buf, n16, lane, v0, v1);
+    // next round: shift the offset window by k, load the next offsets and bytes
+    const uint32_t ub2 = ub + k;
+    const uint64_t A2 = E;
+    uint64_t e2 = 0, en2 = 0;
+    uint32_t k2 = 0, n162 = 0;
+    uint64_t al2 = A2 & ~15ull, E2 = A2;
+    if (ub2 < U) {
+      // e2 = end of update ub2 + lane: from this round's window (e: ub.., en: ub + 64..)
+      const uint32_t sl = (lane + k) & 63;
+      const uint64_t x = __shfl(e, sl, 64), y = __shfl(en, sl, 64);
+      e2 = lane + k < 64 ? x : y;
+      // en2 = end of update ub2 + 64 + lane: loaded now, needed one round later
+      const uint32_t gi = ub2 + 64 + lane;
+      en2 = gi < U ? b.upd_off[u0 + 1 + gi] : 0;
+      const uint64_t fm = __ballot(ub2 + lane < U && e2 - al2 <= LN_STAGE);
+      k2 = lead_ones(fm);
+      if (k2 > 0) {
+        E2 = rdlane64(e2, k2 - 1);
+        n162 = (uint32_t)((E2 - al2 + 15) >> 4);
+      }
+    }
+    uint4 w0 = make_uint4(0, 0, 0, 0), w1 = w0;
+    if (k2 > 0) stage_load(b.bytes, al2, n162, lane, w0, w1);
+    wsync();
+    // walk this round's updates
+    LeanUpd r;
+    bool ok = true;
+    r.has_blk = r.nent = r.nrng = 0;
+    r.c0 = r.c1 = r.c2 = r.c3 = 0;
+    r.client = r.clock = r.len = r.bpos = r.blen = r.dspos = 0;
+    if (act) ok = lean_walk(L.buf, (uint32_t)(s - al), (uint32_t)(e - s), r);
+    if (__ballot(act && !ok)) {
+      bad = true;
+      break;
+    }
+    // blocks: buckets, contiguity, counts, records
+    const bool hb = act && r.has_blk;
+    int bk;
+    if (!bucket_of(L, lane, r.client, hb, nbk, bk)) {
+      bad = true;
+      break;
+    }
+    const uint64_t mall = __ballot(hb);
+    const uint32_t nbr = (uint32_t)__builtin_popcountll(mall);
+    const bool hd = act && r.nent > 0;
+    const uint32_t nr = hd ? r.nrng : 0;
+    const uint32_t rin = wincl(nr, lane), rtot = rdlane(rin, 63);
+    if (NBk + nbr + 2 * (NR + rtot) > LN_AW) { // arena full: not lean
+      bad = true;
+      break;
+    }
+    if (mall) {
+      int prevl = -1;
+      uint32_t exp0 = 0;
+      uint64_t rem = mall;
+      const uint32_t endv = r.clock + r.len;
+      while (rem) {
+        const uint32_t lead = (uint32_t)__builtin_ctzll(rem);
+        const uint32_t bb = rdlane((uint32_t)bk, lead);
+        const uint64_t mb = __ballot(hb && (uint32_t)bk == bb);
+        rem &= ~mb;
+        const uint32_t last = 63 - (uint32_t)__builtin_clzll(mb);
+        const uint32_t c0 = rdlane(r.clock, lead), nend = rdlane(endv, last);
+        const bool had = (blkmask >> bb) & 1;
+        const uint32_t nxt = had ? L.next[bb] : c0;
+        if (hb && (uint32_t)bk == bb) {
+          const uint64_t lt = mb & ((1ull << lane) - 1);
+          prevl = lt ? 63 - (int)__builtin_clzll(lt) : -1;
+          exp0 = nxt;
+        }
+        if (lane == 0) {
+          if (!had) L.first[bb] = c0;
+          L.next[bb] = nend;
+        }
+        blkmask |= 1u << bb;
+      }
+      const uint32_t pend = __shfl(endv, prevl < 0 ? (int)lane : prevl, 64);
+      const bool okc = !hb || r.clock == (prevl < 0 ? exp0 : pend);
+      if (__ballot(!okc)) {
+        bad = true;
+        break;
+      }
+      if (hb) {
+        atomicAdd(&L.cnt[bk], 1u);
+        atomicAdd(&L.bytes[bk], r.blen);
+        const uint32_t src = (uint32_t)(al + r.bpos - B0);
+        L.buf[LN_SW + NBk + lanes_below(mall)] = src | (r.blen << 16) | ((uint32_t)bk << 27);
+      }
+      NBk += nbr;
+    }
+    // DeleteSet entries: buckets, table positions, ranges to the arena top
+    if (__ballot(hd)) {
+      int k0, k1 = 0, k2b = 0, k3 = 0;
+      bool okb = bucket_of(L, lane, r.c0, hd, nbk, k0);
+      if (okb && __ballot(hd && r.nent > 1)) okb = bucket_of(L, lane, r.c1, hd && r.nent > 1, nbk, k1);
+      if (okb && __ballot(hd && r.nent > 2)) okb = bucket_of(L, lane, r.c2, hd && r.nent > 2, nbk, k2b);
+      if (okb && __ballot(hd && r.nent > 3)) okb = bucket_of(L, lane, r.c3, hd && r.nent > 3, nbk, k3);
+      if (!okb) {
+        bad = true;
+        break;
+      }
+      if (hd) {
+        uint32_t p0 = 0, p1 = 1, p2 = 2, p3 = 3;
+        if (r.nent >= 2) ds_pos4(r.nent, r.c0, r.c1, r.c2, r.c3, p0, p1, p2, p3);
+        LCur c{L.buf, r.dspos, (uint32_t)(e - al)};
+        bool cn;
+        uint32_t nds, x, nre;
+        lvar(c, nds, cn);
+        uint32_t slot_r = NR + rin - nr;
+        for (uint32_t q = 0; q < nds; q++) {
+          lvar(c, x, cn); // client (bucketed above)
+          lvar(c, nre, cn);
+          const uint32_t bq = (uint32_t)sel4(q, (uint32_t)k0, (uint32_t)k1, (uint32_t)k2b, (uint32_t)k3);
+          atomicMin(&L.dsfirst[bq], (i << 8) | sel4(q, p0, p1, p2, p3));
+          uint32_t mn = LN_NONE, mx = 0;
+          for (uint32_t t = 0; t < nre; t++) {
+            uint32_t st, ln;
+            lvar(c, st, cn);
+            lvar(c, ln, cn);
+            L.buf[LN_BUF - 2 - 2 * slot_r] = st;
+            L.buf[LN_BUF - 1 - 2 * slot_r] = ln | (bq << 28);
+            slot_r++;
+            mn = st < mn ? st : mn;
+            mx = st + ln > mx ? st + ln : mx;
+          }
+          atomicMin(&L.dsmin[bq], mn);
+          atomicMax(&L.dsmax[bq], mx);
+        }
+      }
+      NR += rtot;
+    }
+    // advance
+    ub = ub2;
+    A = A2;
+    e = e2;
+    en = en2;
+    if (ub < U && k2 == 0) { // one update larger than the stage: not lean
+      bad = true;
+      break;
+    }
+    k = k2;
+    n16 = n162;
+    al = al2;
+    E = E2;
+    v0 = w0;
+    v1 = w1;
+    wsync();
+  }
+  if (bad) {
+    reject();
+    return;
+  }
+  wsync();
+
+  // ---------------------------------------------------------------- 2 layout
+  const bool lb = lane < nbk;
+  const uint32_t cnt = lb ? L.cnt[lane] : 0, cl = lb ? L.client[lane] : 0, fst = lb ? L.first[lane] : 0,
+                 byt = lb ? L.bytes[lane] : 0;
+  const bool hasb = cnt > 0;
+  const uint64_t hbm = __ballot(hasb);
+  const uint32_t NC = (uint32_t)__builtin_popcountll(hbm);
+  uint32_t rank = 0;
+  for (uint32_t q = 0; q < nbk; q++) {
+    const uint32_t cq = rdlane(cl, q);
+    rank += (((hbm >> q) & 1) && cq > cl) ? 1u : 0u;
+  }
+  const uint32_t hdr = hasb ? varlen(cnt) + varlen(cl) + varlen(fst) : 0;
+  const uint32_t ssz = hasb ? hdr + byt : 0;
+  uint32_t sst = varlen(NC), blocks_size = varlen(NC);
+  for (uint32_t q = 0; q < nbk; q++) {
+    const uint32_t rq = rdlane(rank, q), sq = rdlane(ssz, q);
+    blocks_size += sq;
+    if (((hbm >> q) & 1) && rq < rank) sst += sq;
+  }
+  // DeleteSet windows: bitmap words per client, checked before anything is written
+  const uint32_t dsf = lb ? L.dsfirst[lane] : LN_NONE;
+  const bool hasd = dsf != LN_NONE;
+  const uint32_t dmn = hasd ? L.dsmin[lane] : 0, dmx = hasd ? L.dsmax[lane] : 0;
+  const uint32_t words = hasd ? ((dmx - 1) >> 5) - (dmn >> 5) + 1 : 0;
+  const uint32_t win = wincl(words, lane), W = rdlane(win, 63), woff = win - words;
+  const uint32_t D = (uint32_t)__builtin_popcountll(__ballot(hasd));
+  if (W + 2 * NR > LN_BUF) {
+    reject();
+    return;
+  }
+  // section headers (count, client, first clock: update.rs encode_diff :490-535) and NC
+  if (lane == 0) {
+    Writer wr{out, 0};
+    w_var(wr, NC);
+  }
+  if (hasb) {
+    Writer wr{out, sst};
+    w_var(wr, cnt);
+    w_var(wr, cl);
+    w_var(wr, fst);
+    L.cur[lane] = sst + hdr;
+  }
+  wsync();
+
+  // ---------------------------------------------------------------- 3 copy blocks
+  {
+    uint32_t r0 = 0;
+    uint4 c0 = make_uint4(0, 0, 0, 0), c1 = c0;
+    uint32_t rec = 0, kk = 0, cn16 = 0;
+    uint64_t cal = 0;
+    auto plan = [&](uint32_t base) {
+      const uint32_t j = base + lane;
+      const bool v = j < NBk;
+      rec = v ? L.buf[LN_SW + j] : 0;
+      const uint32_t src = rec & 0xFFFF, bl = (rec >> 16) & 0x7FF;
+      cal = (B0 + rdlane(src, 0)) & ~15ull;
+      const uint64_t ae = B0 + src + bl;
+      kk = lead_ones(__ballot(v && ae - cal <= LN_STAGE));
+      const uint64_t Ek = rdlane64(ae, kk - 1);
+      cn16 = (uint32_t)((Ek - cal + 15) >> 4);
+    };
+    if (NBk) {
+      plan(0);
+      stage_load(b.bytes, cal, cn16, lane, c0, c1);
+    }
+    while (r0 < NBk) {
+      const uint32_t myrec = rec, k1 = kk, n1 = cn16;
+      const uint64_t al1 = cal;
+      stage_store(L.buf, n1, lane, c0, c1);
+      const uint32_t r1 = r0 + k1;
+      if (r1 < NBk) { // next step's plan and bytes in flight during this one
+        plan(r1);
+        stage_load(b.bytes, cal, cn16, lane, c0, c1);
+      }
+      wsync();
+      const bool act = lane < k1;
+      const uint32_t src = myrec & 0xFFFF, bl = (myrec >> 16) & 0x7FF, bq = (myrec >> 27) & 15;
+      uint32_t off = 0;
+      uint64_t rem = __ballot(act);
+      while (rem) {
+        const uint32_t bb = rdlane(bq, (uint32_t)__builtin_ctzll(rem));
+        const bool mine = act && bq == bb;
+        rem &= ~__ballot(mine);
+        const uint32_t inc = wincl(mine ? bl : 0u, lane), tot = rdlane(inc, 63);
+        const uint32_t base = L.cur[bb]; // (LDS operations of one wave complete in order)
+        if (mine) off = base + inc - bl;
+        if (lane == 0) L.cur[bb] = base + tot;
+      }
+      if (act) copy_out(L.buf, (uint32_t)(B0 + src - al1), out + off, bl);
+      wsync();
+      r0 = r1;
+    }
+  }
+
+  // ---------------------------------------------------------------- 4 DeleteSet
+  // bitmap over each client's window [dbase, dmax) (stage + arena bottom; ranges stay at the
+  // arena top until they are scattered)
+  uint32_t *bmp = L.buf;
+  const uint32_t dbase = dmn & ~31u;
+  for (uint32_t q = lane; q < W; q += 64) bmp[q] = 0;
+  if (hasd) {
+    L.cur[lane] = woff;   // cursors are free after the copy
+    L.eoff[lane] = dbase; // entry offsets are computed after the scatter
+  }
+  wsync();
+  for (uint32_t j = lane; j < NR; j += 64) {
+    const uint32_t st = L.buf[LN_BUF - 2 - 2 * j], lw = L.buf[LN_BUF - 1 - 2 * j];
+    const uint32_t bq = lw >> 28, ln = lw & 0x0FFFFFFFu;
+    const uint32_t wo = L.cur[bq], bs = L.eoff[bq];
+    uint32_t a = st - bs;
+    const uint32_t z = a + ln;
+    while (a < z) {
+      const uint32_t wi = a >> 5, bo = a & 31, nb = (z - a < 32 - bo) ? z - a : 32 - bo;
+      const uint32_t mask = (nb == 32 ? 0xFFFFFFFFu : ((1u << nb) - 1)) << bo;
+      atomicOr(&bmp[wo + wi], mask);
+      a += nb;
+    }
+  }
+  wsync();
+  // runs -> components: cst[c] / cen[c] per bucket in bucket-index order
+  uint32_t *cst = L.buf + W, *cen = L.buf + W + NR;
+  uint32_t ncomp = 0, cbase = 0, NCD = 0;
+  for (uint32_t q = 0; q < nbk; q++) {
+    const uint32_t wc = rdlane(words, q);
+    if (!wc) continue;
+    const uint32_t wo = rdlane(woff, q), base = rdlane(dbase, q);
+    const uint32_t first_c = NCD;
+    for (uint32_t w0 = 0; w0 < wc; w0 += 64) {
+      const uint32_t kw = w0 + lane;
+      const bool v = kw < wc;
+      const uint32_t bits = v ? bmp[wo + kw] : 0;
+      const uint32_t prev = (v && kw > 0) ? bmp[wo + kw - 1] >> 31 : 0;
+      const uint32_t nxt = (v && kw + 1 < wc) ? bmp[wo + kw + 1] & 1 : 0;
+      const uint32_t stb = bits & ~((bits << 1) | prev), enb = bits & ~((bits >> 1) | (nxt << 31));
+      const uint32_t ns = (uint32_t)__builtin_popcount(stb);
+      const uint32_t inc = wincl(ns, lane), tot = rdlane(inc, 63);
+      const uint32_t cb = NCD + inc - ns, clk0 = base + 32 * kw;
+      uint32_t x = stb;
+      while (x) {
+        const uint32_t bpos = (uint32_t)__builtin_ctz(x);
+        cst[cb + (uint32_t)__builtin_popcount(stb & ((1u << bpos) - 1))] = clk0 + bpos;
+        x &= x - 1;
+      }
+      x = enb;
+      while (x) {
+        const uint32_t bpos = (uint32_t)__builtin_ctz(x);
+        const uint32_t upto = bpos == 31 ? stb : (stb & ((2u << bpos) - 1));
+        cen[cb + (uint32_t)__builtin_popcount(upto) - 1] = clk0 + bpos + 1;
+        x &= x - 1;
+      }
+      NCD += tot;
+    }
+    if (lane == q) {
+      ncomp = NCD - first_c;
+      cbase = first_c;
+    }
+  }
+  wsync();
+  // component bytes per client
+  uint32_t dsb = 0;
+  for (uint32_t q = 0; q < nbk; q++) {
+    const uint32_t nq = rdlane(ncomp, q), cq = rdlane(cbase, q);
+    uint32_t acc = 0;
+    for (uint32_t c0 = 0; c0 < nq; c0 += 64) {
+      const uint32_t c = cq + c0 + lane;
+      const uint32_t sz = c0 + lane < nq ? varlen(cst[c]) + varlen(cen[c] - cst[c]) : 0;
+      acc += rdlane(wincl(sz, lane), 63);
+    }
+    if (lane == q) dsb = acc;
+  }
+  // client order and entry offsets (one lane, D <= 16)
+  const uint32_t ds_start = blocks_size;
+  if (hasd) {
+    L.dsfirst[lane] = dsf;
+    L.bytes[lane] = varlen(cl) + varlen(ncomp) + dsb; // entry size (bytes[] is free after the copy)
+  }
+  wsync();
+  uint32_t total = 0;
+  if (lane == 0) {
+    lean_ds_order(nbk, L.client, L.dsfirst, L.ord, L.slots);
+    uint32_t pos = ds_start + varlen(D);
+    for (uint32_t i2 = 0; i2 < D; i2++) {
+      const uint32_t bq = L.ord[i2];
+      L.eoff[bq] = pos;
+      pos += L.bytes[bq];
+    }
+    total = pos;
+    Writer wr{out, ds_start};
+    w_var(wr, D);
+  }
+  total = rdlane(total, 0);
+  wsync();
+  if (hasd) {
+    Writer wr{out, L.eoff[lane]};
+    w_var(wr, cl);
+    w_var(wr, ncomp);
+  }
+  for (uint32_t q = 0; q < nbk; q++) {
+    const uint32_t nq = rdlane(ncomp, q), cq = rdlane(cbase, q);
+    if (!nq) continue;
+    const uint32_t eo = L.eoff[q] + varlen(rdlane(cl, q)) + varlen(nq);
+    uint32_t acc = 0;
+    for (uint32_t c0 = 0; c0 < nq; c0 += 64) {
+      const uint32_t c = cq + c0 + lane;
+      const bool v = c0 + lane < nq;
+      const uint32_t s0 = v ? cst[c] : 0, ln = v ? cen[c] - s0 : 0;
+      const uint32_t sz = v ? varlen(s0) + varlen(ln) : 0;
+      const uint32_t inc = wincl(sz, lane);
+      if (v) {
+        Writer wr{out, eo + acc + inc - sz};
+        w_var(wr, s0);
+        w_var(wr, ln);
+      }
+      acc += rdlane(inc, 63);
+    }
+  }
+  if (lane == 0) {
+    o.path[d] = 0;
+    o.status[d] = 0;
+    o.out_len[d] = total;
+    o.out_start[d] = slot;
+  }
+}
+
+void launch_lean(const BatchIn &b, const FastOut &o, hipStream_t s) {
+  if (!b.n_docs) return;
+  constexpr int WPB = 1;
+  hipLaunchKernelGGL((k_lean<WPB>), dim3((b.n_docs + WPB - 1) / WPB), dim3(64 * WPB), 0, s, b, o);
+}
+
+} // namespace ym
