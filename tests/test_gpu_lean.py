@@ -5,7 +5,7 @@ wrote the documents."""
 import numpy as np
 import pytest
 
-from test_gpu_parity import batch_of, check_batch, engine_with
+from test_gpu_parity import batch_of, check_batch, engine, engine_with  # noqa: F401 (engine: fixture)
 
 pytestmark = pytest.mark.gpu
 

@@ -4,7 +4,7 @@ import csv
 import glob
 import sys
 
-KEEP = ("k_decode", "k_fast_merge", "k_big", "k_seq", "k_plan", "k_exec", "k_pack")
+KEEP = ("k_lean", "k_decode", "k_fast_merge", "k_big", "k_seq", "k_plan", "k_exec", "k_pack")
 
 
 def main(d):

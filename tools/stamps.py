@@ -63,7 +63,36 @@ def main_zipf(n):
                   + ", ".join(f"{nm} {d[sel, i].mean():.0f}" for i, nm in enumerate(NAMES) if nm != "-"))
 
 
+LEAN_NAMES = ["init", "decode", "layout", "copy", "ds_union", "ds_write"]
+LEAN_SUB = ["stage+prefetch", "walk", "blocks", "deleteset"]
+
+
+def main_lean(kind, n):
+    """k_lean documents (marker 0x1EA4 in slot 15): phase cycles, decode sub-phases per round."""
+    b = workloads.text_docs(n, 1000) if kind == "c2" else workloads.zipf_docs(n, seed=0x5EED)
+    e = ymerge.Engine(0)
+    e.merge_host(b.data, b.upd_off, b.doc_upd)
+    L = ymerge.lib()
+    L.ymerge_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+    st = np.zeros((n, 16), np.uint64)
+    assert L.ymerge_debug_stamps(e._ctx, n, st.ctypes.data) == 0
+    ok = st[:, 15] == 0x1EA4
+    U = np.diff(b.doc_upd.astype(np.int64))[ok]
+    d = np.diff(st[ok][:, :7].astype(np.int64), axis=1)
+    tot = d.sum(axis=1)
+    rounds = st[ok][:, 12].astype(np.float64)
+    print(f"lean docs {ok.sum()} of {n}: cycles/doc mean {tot.mean():.0f}, rounds/doc {rounds.mean():.1f}, "
+          f"updates/doc {U.mean():.0f}")
+    for i, nm in enumerate(LEAN_NAMES):
+        print(f"  {nm:10s} {d[:, i].mean():10.0f} cycles  {100 * d[:, i].mean() / tot.mean():5.1f}%")
+    for i, nm in enumerate(LEAN_SUB):
+        v = st[ok][:, 8 + i].astype(np.float64)
+        print(f"  decode/{nm:16s} {v.mean():10.0f} cycles/doc  {(v / np.maximum(rounds, 1)).mean():8.0f} per round")
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "lean":
+        return main_lean(sys.argv[2] if len(sys.argv) > 2 else "c2", int(sys.argv[3]) if len(sys.argv) > 3 else 10000)
     if len(sys.argv) > 1 and sys.argv[1] == "zipf":
         os.environ["YMERGE_TINY"] = "0"
         return main_zipf(int(sys.argv[2]) if len(sys.argv) > 2 else 20000)

@@ -44,6 +44,7 @@ struct FastOut {
   uint64_t *out_start, *out_len;
   uint8_t *status, *path;
   uint64_t *stamps; // diagnostic build only: s_memtime per phase (16 per document)
+  uint32_t *dbg = nullptr; // k_lean diagnostics (env YMERGE_LEAN_DEBUG): 8 words per document
   uint32_t *npath;  // npath[p]: documents handed to path p (1 exact engine, 2 tiled kernel); [3] tiled
                     // kernel in overlap mode, [4] tiled kernel -> exact engine, [5] of [1]:
                     // tiny documents (FastCaps.in_cap / u_cap), [6] k_lean -> fast path

@@ -153,7 +153,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   if (!c->status.ensure(nn) || !c->path.ensure(nn) || !c->out_start.ensure(nn * 8) || !c->out_len.ensure(nn * 8) ||
       !c->pack_off.ensure(nn * 8) || !c->counts.ensure(4 * nn * 4) || !c->need.ensure(nn * 8) ||
       !c->scr_off.ensure(nn * 8) || !c->sizes.ensure(nn * 8) || !c->spill_off.ensure(nn * 8) ||
-      !c->scan_tmp.ensure(ym::scan_tmp_elems(n) * 8 + 64) || !c->counter.ensure(64) ||
+      !c->scan_tmp.ensure(ym::scan_tmp_elems(n) * 8 + 64) || !c->counter.ensure(128) ||
       !ensure_keep(c, c->arena, slots + slots / 8 + 4096, 0) ||
       (c->fast_threads && (!c->rec.ensure((n_updates + 1) * ym::REC_WORDS * 4) ||
                            !c->ovf.ensure(((n_updates + ym::DEC_NT - 1) / ym::DEC_NT + 1) * ym::DEC_OVF * 4))))
@@ -163,7 +163,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   uint8_t *arena = c->arena.as<uint8_t>();
   uint64_t *ostart = c->out_start.as<uint64_t>(), *olen = c->out_len.as<uint64_t>();
   uint8_t *status = c->status.as<uint8_t>(), *path = c->path.as<uint8_t>();
-  hipMemsetAsync(c->counter.p, 0, 64, c->s);
+  hipMemsetAsync(c->counter.p, 0, 128, c->s);
   uint64_t *stamps = nullptr;
   if (c->want_stamps) {
     if (!c->stamps.ensure(nn * 16 * 8)) return YMERGE_ERR_DEVICE;
@@ -171,10 +171,15 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     stamps = c->stamps.as<uint64_t>();
     c->stamps_docs = n_docs;
   }
-  ym::FastOut fo{arena, ostart, olen, status, path, stamps, c->counter.as<uint32_t>() + 4};
+  ym::FastOut fo{arena, ostart, olen, status, path, stamps, nullptr, c->counter.as<uint32_t>() + 4};
+  static DevBuf dbgbuf;
+  if (getenv("YMERGE_LEAN_DEBUG") && dbgbuf.ensure(nn * 32)) {
+    hipMemsetAsync(dbgbuf.p, 0xFF, nn * 32, c->s);
+    fo.dbg = dbgbuf.as<uint32_t>();
+  }
   // k_lean: one wavefront per document for the common shape; the rest (path 3) goes on to
   // k_decode + k_fast_merge, which are skipped when k_lean wrote every document
-  const bool lean = c->lean && c->fast_threads && !c->want_stamps;
+  const bool lean = c->lean && c->fast_threads;
   uint32_t n_rej = n;
   hipEventRecord(c->ev[7], c->s);
   if (lean) {
@@ -184,6 +189,20 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
     n_rej = (uint32_t)(c->h_pinned[16] & 0xFFFFFFFFu);
     b.only_path3 = 1;
+    if (n_rej && getenv("YMERGE_LEAN_DEBUG")) {
+      uint32_t why[7];
+      hipMemcpy(why, c->counter.as<uint32_t>() + 11, sizeof why, hipMemcpyDeviceToHost);
+      fprintf(stderr, "k_lean handed over %u/%u docs: size %u stage %u walk %u clients %u arena %u contiguity %u window %u\n",
+              n_rej, n, why[0], why[1], why[2], why[3], why[4], why[5], why[6]);
+      std::vector<uint32_t> g(8 * (size_t)n);
+      hipMemcpy(g.data(), fo.dbg, g.size() * 4, hipMemcpyDeviceToHost);
+      for (uint32_t q = 0, shown = 0; q < n && shown < 4; q++)
+        if (g[8 * q] != 0xFFFFFFFFu) {
+          fprintf(stderr, "  doc %u: lane %u clock %u prevl %d exp0 %u pend %u bk %u end0 %u ub %u\n", q, g[8 * q],
+                  g[8 * q + 1], (int)g[8 * q + 2], g[8 * q + 3], g[8 * q + 4], g[8 * q + 5], g[8 * q + 6], g[8 * q + 7]);
+          shown++;
+        }
+    }
   }
   hipEventRecord(c->ev[0], c->s);
   const bool fast = c->fast_threads && n_rej > 0;

@@ -43,10 +43,15 @@ constexpr uint32_t LN_BUF = LN_SW + LN_AW;   // stage + arena, reused whole by t
 constexpr uint32_t LN_NBK = 16;              // client buckets per document
 constexpr uint32_t LN_HT = 32;               // client hash slots
 constexpr uint32_t LN_MAXBLEN = 1024;        // block bytes (a copy step must always fit one block)
+constexpr uint32_t LN_DSB = 1024;            // DeleteSet item bytes buffered between DS passes
+constexpr uint32_t LN_DSI = 64;              // DeleteSet items per DS pass (one per lane)
+constexpr uint32_t LN_DSMAXI = 252;          // bytes of one update's DeleteSet
 constexpr uint32_t LN_NONE = 0xFFFFFFFFu;
 
 struct LeanLds {
   uint32_t buf[LN_BUF];
+  uint32_t dsb[LN_DSB / 4 + 4];              // DeleteSet items (4-byte aligned), + lvar's read-ahead word
+  uint32_t dsi_off[LN_DSI], dsi_upd[LN_DSI]; // item byte offset | length << 16; doc-relative update
   uint64_t ht[LN_HT]; // client << 32 | (bucket + 1); 0 = empty
   uint32_t client[LN_NBK], cnt[LN_NBK], first[LN_NBK], next[LN_NBK], bytes[LN_NBK];
   uint32_t dsfirst[LN_NBK], dsmin[LN_NBK], dsmax[LN_NBK], cur[LN_NBK], eoff[LN_NBK];
@@ -65,11 +70,20 @@ YM_INLINE uint32_t rdlane(uint32_t x, uint32_t l) { return __builtin_amdgcn_read
 YM_INLINE uint64_t rdlane64(uint64_t x, uint32_t l) {
   return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(x >> 32), l) << 32) | __builtin_amdgcn_readlane((uint32_t)x, l);
 }
+// Cross-lane results are pinned where they are computed: the backend may otherwise sink a
+// ds_bpermute into a branch whose exec mask excludes its source lanes (observed: the
+// shuffle feeding a `lane < k` block read inactive lanes).
+template <class T> YM_INLINE T pin(T x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+YM_INLINE uint32_t shfl(uint32_t x, int l) { return pin(__shfl(x, l, 64)); }
+YM_INLINE uint64_t shfl(uint64_t x, int l) { return pin(__shfl(x, l, 64)); }
 // inclusive sum over the wave
 YM_INLINE uint32_t wincl(uint32_t x, uint32_t lane) {
 #pragma unroll
   for (uint32_t o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o, 64);
+    const uint32_t y = pin(__shfl_up(x, o, 64));
     if (lane >= o) x += y;
   }
   return x;
@@ -80,21 +94,24 @@ YM_INLINE uint32_t lead_ones(uint64_t m) { return m == ~0ull ? 64u : (uint32_t)_
 // ------------------------------------------------------------------ one update
 struct LeanUpd {
   uint32_t has_blk, client, clock, len, bpos, blen; // block; bpos = stage byte position
-  uint32_t dspos, nent, nrng;                       // DeleteSet: stage position, entries, ranges
-  uint32_t c0, c1, c2, c3;                          // entry clients (stream order)
+  uint32_t dspos, nent;                             // DeleteSet: stage position (its nds varint), entries
+};
+struct LeanDs {
+  uint32_t nent, nrng;     // entries, ranges
+  uint32_t c0, c1, c2, c3; // entry clients (stream order)
 };
 
 // Validating walk of one staged update (Update::decode_v1, yrs/src/update.rs:714-749,
 // decode_block :433-488, ItemContent::decode block.rs:1786-1835, IdSet::decode
 // id_set.rs:412-426) restricted to the lean shape; false = not the shape (or malformed:
-// the exact walk downstream owns the error codes).
+// the exact walk downstream owns the error codes).  The DeleteSet is only located here (and
+// its entry count read): ds_walk decodes it in a batched DS pass.
 YM_INLINE bool lean_walk(const uint32_t *w, uint32_t start, uint32_t n, LeanUpd &r) {
   LCur c{w, start, start + n};
   bool cn;
   uint32_t ncl, v;
   r.has_blk = 0;
-  r.nent = r.nrng = 0;
-  r.c0 = r.c1 = r.c2 = r.c3 = 0;
+  r.nent = 0;
   if (!lvar(c, ncl, cn) || ncl > 1) return false;
   if (ncl == 1) {
     uint32_t nb, client, clock;
@@ -170,10 +187,23 @@ YM_INLINE bool lean_walk(const uint32_t *w, uint32_t start, uint32_t n, LeanUpd 
   r.dspos = c.p;
   uint32_t nds;
   if (!lvar(c, nds, cn) || nds > 4) return false;
+  r.nent = nds;
+  return true;
+}
+
+// One update's DeleteSet (IdSet::decode, id_set.rs:412-426) from the DS item buffer:
+// <= 4 entries with distinct clients (a repeated client replaces the earlier entry: not
+// lean), non-empty ranges.
+YM_INLINE bool ds_walk(const uint32_t *w, uint32_t start, uint32_t n, LeanDs &r) {
+  LCur c{w, start, start + n};
+  bool cn;
+  uint32_t nds;
+  r.nent = r.nrng = 0;
+  r.c0 = r.c1 = r.c2 = r.c3 = 0;
+  if (!lvar(c, nds, cn) || nds > 4) return false;
   for (uint32_t e = 0; e < nds; e++) {
     uint32_t client, nr;
     if (!lvar(c, client, cn) || !lvar(c, nr, cn) || nr == 0 || nr > n) return false;
-    // a repeated client replaces the earlier entry (IdSet::decode inserts): not lean
     if ((e > 0 && r.c0 == client) || (e > 1 && r.c1 == client) || (e > 2 && r.c2 == client)) return false;
     if (e == 0) r.c0 = client;
     else if (e == 1) r.c1 = client;
@@ -361,26 +391,42 @@ __device__ __noinline__ uint32_t lean_ds_order(uint32_t nbk, const uint32_t *cli
 }
 
 // ------------------------------------------------------------------ the kernel
-template <int WPB> __global__ void __launch_bounds__(64 * WPB) k_lean(BatchIn b, FastOut o) {
+// Diagnostic build only (STAMPS, env YMERGE_STAMPS): lane 0 records s_memtime at phase
+// boundaries into o.stamps[doc * 16 + k] (k 0..6), per-round sub-phase cycle sums (8..11),
+// rounds (12), marker 0x1EA4 (15); never part of a timed run.
+template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB) k_lean(BatchIn b, FastOut o) {
   __shared__ LeanLds lds[WPB];
   const uint32_t lane = __lane_id();
   const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t d = blockIdx.x * WPB + w;
   if (d >= b.n_docs) return;
   LeanLds &L = lds[w];
+  uint64_t tst[16];
+  auto stamp = [&](int k) {
+    if (STAMPS) tst[k] = __builtin_amdgcn_s_memtime();
+  };
+  auto acc = [&](int k, uint64_t t0) {
+    if (STAMPS) tst[k] += __builtin_amdgcn_s_memtime() - t0;
+  };
+  if (STAMPS)
+    for (int q = 0; q < 16; q++) tst[q] = 0;
+  stamp(0);
   const uint64_t u0 = b.doc_upd[d], u1 = b.doc_upd[d + 1];
   const uint64_t B0 = b.upd_off[u0], B1 = b.upd_off[u1];
   const uint32_t U = (uint32_t)(u1 - u0);
   const uint64_t slot = 2 * B0 + 64ull * d;
   uint8_t *out = o.out + slot;
-  auto reject = [&]() {
+  // hand-over; why: 0 size/empty, 1 stage, 2 walk, 3 clients, 4 arena, 5 contiguity, 6 DS window
+  // (npath[7 + why]: diagnostics, env YMERGE_LEAN_DEBUG)
+  auto reject = [&](uint32_t why) {
     if (lane == 0) {
       o.path[d] = 3;
       atomicAdd(&o.npath[6], 1u);
+      atomicAdd(&o.npath[7 + (why < 7 ? why : 0)], 1u);
     }
   };
   if (U == 0 || B1 - B0 >= 65536 || u1 - u0 >= 65536) {
-    reject();
+    reject(0);
     return;
   }
   if (lane < LN_HT) L.ht[lane] = 0;
@@ -393,7 +439,7 @@ template <int WPB> __global__ void __launch_bounds__(64 * WPB) k_lean(BatchIn b,
 
   // ---------------------------------------------------------------- 1 decode
   uint32_t nbk = 0, NBk = 0, NR = 0, blkmask = 0;
-  bool bad = false;
+  uint32_t bad = 0; // why + 1
   uint32_t ub = 0;
   uint64_t A = B0;
   // round pipeline: offsets of the round's updates (e = end of update ub + lane), its
@@ -406,16 +452,82 @@ template <int WPB> __global__ void __launch_bounds__(64 * WPB) k_lean(BatchIn b,
     const uint64_t fm = __ballot(lane < U && e - al <= LN_STAGE);
     k = lead_ones(fm);
     if (k == 0) {
-      reject();
+      reject(1);
       return;
     }
     E = rdlane64(e, k - 1);
     n16 = (uint32_t)((E - al + 15) >> 4);
   }
+  // DeleteSet pass: one buffered item per lane — validate, bucket the entry clients,
+  // table positions, ranges to the arena top, first occurrence / window per client
+  uint32_t dsn = 0, dsused = 0;
+  auto ds_pass = [&]() {
+    const bool it = lane < dsn;
+    const uint32_t io = it ? L.dsi_off[lane] : 0, iu = it ? L.dsi_upd[lane] : 0;
+    LeanDs r;
+    bool ok = true;
+    r.nent = r.nrng = r.c0 = r.c1 = r.c2 = r.c3 = 0;
+    if (it) ok = ds_walk(L.dsb, io & 0xFFFF, io >> 16, r);
+    if (__ballot(it && !ok)) {
+      bad = 3;
+      return;
+    }
+    int k0 = 0, k1 = 0, k2b = 0, k3 = 0;
+    bool okb = bucket_of(L, lane, r.c0, it, nbk, k0);
+    if (okb && __ballot(it && r.nent > 1)) okb = bucket_of(L, lane, r.c1, it && r.nent > 1, nbk, k1);
+    if (okb && __ballot(it && r.nent > 2)) okb = bucket_of(L, lane, r.c2, it && r.nent > 2, nbk, k2b);
+    if (okb && __ballot(it && r.nent > 3)) okb = bucket_of(L, lane, r.c3, it && r.nent > 3, nbk, k3);
+    if (!okb) {
+      bad = 4;
+      return;
+    }
+    const uint32_t nr = it ? r.nrng : 0;
+    const uint32_t rin = wincl(nr, lane), rtot = rdlane(rin, 63);
+    if (NBk + 2 * (NR + rtot) > LN_AW) {
+      bad = 5;
+      return;
+    }
+    if (it) {
+      uint32_t p0 = 0, p1 = 1, p2 = 2, p3 = 3;
+      if (r.nent >= 2) ds_pos4(r.nent, r.c0, r.c1, r.c2, r.c3, p0, p1, p2, p3);
+      LCur c{L.dsb, io & 0xFFFF, (io & 0xFFFF) + (io >> 16)};
+      bool cn;
+      uint32_t nds, x, nre;
+      lvar(c, nds, cn);
+      uint32_t slot_r = NR + rin - nr;
+      for (uint32_t q = 0; q < nds; q++) {
+        lvar(c, x, cn); // client (bucketed above)
+        lvar(c, nre, cn);
+        const uint32_t bq = (uint32_t)sel4(q, (uint32_t)k0, (uint32_t)k1, (uint32_t)k2b, (uint32_t)k3);
+        atomicMin(&L.dsfirst[bq], (iu << 8) | sel4(q, p0, p1, p2, p3));
+        uint32_t mn = LN_NONE, mx = 0;
+        for (uint32_t t = 0; t < nre; t++) {
+          uint32_t st, ln;
+          lvar(c, st, cn);
+          lvar(c, ln, cn);
+          L.buf[LN_BUF - 2 - 2 * slot_r] = st;
+          L.buf[LN_BUF - 1 - 2 * slot_r] = ln | (bq << 28);
+          slot_r++;
+          mn = st < mn ? st : mn;
+          mx = st + ln > mx ? st + ln : mx;
+        }
+        atomicMin(&L.dsmin[bq], mn);
+        atomicMax(&L.dsmax[bq], mx);
+      }
+    }
+    NR += rtot;
+    dsn = 0;
+    dsused = 0;
+    wsync();
+  };
   uint4 v0, v1;
   stage_load(b.bytes, al, n16, lane, v0, v1);
+  stamp(1);
   while (ub < U) {
-    const uint64_t s = lane == 0 ? A : __shfl_up(e, 1, 64);
+    const uint64_t tr0 = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+    if (STAMPS) tst[12]++;
+    const uint64_t sprev = shfl(e, lane ? (int)lane - 1 : 0); // every lane takes part in the shuffle
+    const uint64_t s = lane == 0 ? A : sprev;
     const bool act = lane < k;
     const uint32_t i = ub + lane; // doc-relative update index
     stage_store(L.buf, n16, lane, v0, v1);
@@ -428,7 +540,7 @@ template <int WPB> __global__ void __launch_bounds__(64 * WPB) k_lean(BatchIn b,
     if (ub2 < U) {
       // e2 = end of update ub2 + lane: from this round's window (e: ub.., en: ub + 64..)
       const uint32_t sl = (lane + k) & 63;
-      const uint64_t x = __shfl(e, sl, 64), y = __shfl(en, sl, 64);
+      const uint64_t x = shfl(e, (int)sl), y = shfl(en, (int)sl);
       e2 = lane + k < 64 ? x : y;
       // en2 = end of update ub2 + 64 + lane: loaded now, needed one round later
       const uint32_t gi = ub2 + 64 + lane;
@@ -443,31 +555,31 @@ template <int WPB> __global__ void __launch_bounds__(64 * WPB) k_lean(BatchIn b,
     uint4 w0 = make_uint4(0, 0, 0, 0), w1 = w0;
     if (k2 > 0) stage_load(b.bytes, al2, n162, lane, w0, w1);
     wsync();
+    acc(8, tr0);
+    const uint64_t tr1 = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
     // walk this round's updates
     LeanUpd r;
     bool ok = true;
-    r.has_blk = r.nent = r.nrng = 0;
-    r.c0 = r.c1 = r.c2 = r.c3 = 0;
+    r.has_blk = r.nent = 0;
     r.client = r.clock = r.len = r.bpos = r.blen = r.dspos = 0;
     if (act) ok = lean_walk(L.buf, (uint32_t)(s - al), (uint32_t)(e - s), r);
     if (__ballot(act && !ok)) {
-      bad = true;
+      bad = 3;
       break;
     }
+    acc(9, tr1);
+    const uint64_t tr2 = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
     // blocks: buckets, contiguity, counts, records
     const bool hb = act && r.has_blk;
     int bk;
     if (!bucket_of(L, lane, r.client, hb, nbk, bk)) {
-      bad = true;
+      bad = 4;
       break;
     }
     const uint64_t mall = __ballot(hb);
     const uint32_t nbr = (uint32_t)__builtin_popcountll(mall);
-    const bool hd = act && r.nent > 0;
-    const uint32_t nr = hd ? r.nrng : 0;
-    const uint32_t rin = wincl(nr, lane), rtot = rdlane(rin, 63);
-    if (NBk + nbr + 2 * (NR + rtot) > LN_AW) { // arena full: not lean
-      bad = true;
+    if (NBk + nbr + 2 * NR > LN_AW) { // arena full: not lean
+      bad = 5;
       break;
     }
     if (mall) {
@@ -495,10 +607,10 @@ template <int WPB> __global__ void __launch_bounds__(64 * WPB) k_lean(BatchIn b,
         }
         blkmask |= 1u << bb;
       }
-      const uint32_t pend = __shfl(endv, prevl < 0 ? (int)lane : prevl, 64);
+      const uint32_t pend = shfl(endv, prevl < 0 ? (int)lane : prevl);
       const bool okc = !hb || r.clock == (prevl < 0 ? exp0 : pend);
       if (__ballot(!okc)) {
-        bad = true;
+        bad = 6;
         break;
       }
       if (hb) {
@@ -509,54 +621,45 @@ template <int WPB> __global__ void __launch_bounds__(64 * WPB) k_lean(BatchIn b,
       }
       NBk += nbr;
     }
-    // DeleteSet entries: buckets, table positions, ranges to the arena top
-    if (__ballot(hd)) {
-      int k0, k1 = 0, k2b = 0, k3 = 0;
-      bool okb = bucket_of(L, lane, r.c0, hd, nbk, k0);
-      if (okb && __ballot(hd && r.nent > 1)) okb = bucket_of(L, lane, r.c1, hd && r.nent > 1, nbk, k1);
-      if (okb && __ballot(hd && r.nent > 2)) okb = bucket_of(L, lane, r.c2, hd && r.nent > 2, nbk, k2b);
-      if (okb && __ballot(hd && r.nent > 3)) okb = bucket_of(L, lane, r.c3, hd && r.nent > 3, nbk, k3);
-      if (!okb) {
-        bad = true;
-        break;
-      }
-      if (hd) {
-        uint32_t p0 = 0, p1 = 1, p2 = 2, p3 = 3;
-        if (r.nent >= 2) ds_pos4(r.nent, r.c0, r.c1, r.c2, r.c3, p0, p1, p2, p3);
-        LCur c{L.buf, r.dspos, (uint32_t)(e - al)};
-        bool cn;
-        uint32_t nds, x, nre;
-        lvar(c, nds, cn);
-        uint32_t slot_r = NR + rin - nr;
-        for (uint32_t q = 0; q < nds; q++) {
-          lvar(c, x, cn); // client (bucketed above)
-          lvar(c, nre, cn);
-          const uint32_t bq = (uint32_t)sel4(q, (uint32_t)k0, (uint32_t)k1, (uint32_t)k2b, (uint32_t)k3);
-          atomicMin(&L.dsfirst[bq], (i << 8) | sel4(q, p0, p1, p2, p3));
-          uint32_t mn = LN_NONE, mx = 0;
-          for (uint32_t t = 0; t < nre; t++) {
-            uint32_t st, ln;
-            lvar(c, st, cn);
-            lvar(c, ln, cn);
-            L.buf[LN_BUF - 2 - 2 * slot_r] = st;
-            L.buf[LN_BUF - 1 - 2 * slot_r] = ln | (bq << 28);
-            slot_r++;
-            mn = st < mn ? st : mn;
-            mx = st + ln > mx ? st + ln : mx;
-          }
-          atomicMin(&L.dsmin[bq], mn);
-          atomicMax(&L.dsmax[bq], mx);
+    acc(10, tr2);
+    const uint64_t tr3 = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+    // DeleteSets: copied (4-byte aligned) into the item buffer, decoded 64 at a time by ds_pass
+    {
+      const bool hd = act && r.nent > 0;
+      const uint32_t ilen = hd ? (uint32_t)(e - al) - r.dspos : 0;
+      const uint64_t hm = __ballot(hd);
+      if (hm) {
+        const uint32_t isz = (ilen + 3) & ~3u;
+        const uint32_t binc = wincl(isz, lane), btot = rdlane(binc, 63);
+        const uint32_t nit = (uint32_t)__builtin_popcountll(hm);
+        if (__ballot(ilen > LN_DSMAXI) || btot > LN_DSB) {
+          bad = 3;
+          break;
         }
+        if (dsn + nit > LN_DSI || dsused + btot > LN_DSB) {
+          ds_pass();
+          if (bad) break;
+        }
+        if (hd) {
+          const uint32_t idx = dsn + lanes_below(hm), off = dsused + binc - isz;
+          const uint32_t sh = r.dspos & 3, q0 = r.dspos >> 2;
+          for (uint32_t t = 0; t < isz / 4; t++)
+            L.dsb[off / 4 + t] = __builtin_amdgcn_alignbyte(L.buf[q0 + t + 1], L.buf[q0 + t], sh);
+          L.dsi_off[idx] = off | (ilen << 16);
+          L.dsi_upd[idx] = i;
+        }
+        dsn += nit;
+        dsused += btot;
       }
-      NR += rtot;
     }
+    acc(11, tr3);
     // advance
     ub = ub2;
     A = A2;
     e = e2;
     en = en2;
     if (ub < U && k2 == 0) { // one update larger than the stage: not lean
-      bad = true;
+      bad = 2;
       break;
     }
     k = k2;
@@ -567,11 +670,13 @@ template <int WPB> __global__ void __launch_bounds__(64 * WPB) k_lean(BatchIn b,
     v1 = w1;
     wsync();
   }
+  if (!bad && dsn) ds_pass();
   if (bad) {
-    reject();
+    reject(bad - 1);
     return;
   }
   wsync();
+  stamp(2);
 
   // ---------------------------------------------------------------- 2 layout
   const bool lb = lane < nbk;
@@ -601,7 +706,7 @@ template <int WPB> __global__ void __launch_bounds__(64 * WPB) k_lean(BatchIn b,
   const uint32_t win = wincl(words, lane), W = rdlane(win, 63), woff = win - words;
   const uint32_t D = (uint32_t)__builtin_popcountll(__ballot(hasd));
   if (W + 2 * NR > LN_BUF) {
-    reject();
+    reject(6);
     return;
   }
   // section headers (count, client, first clock: update.rs encode_diff :490-535) and NC
@@ -618,6 +723,7 @@ template <int WPB> __global__ void __launch_bounds__(64 * WPB) k_lean(BatchIn b,
   }
   wsync();
 
+  stamp(3);
   // ---------------------------------------------------------------- 3 copy blocks
   {
     uint32_t r0 = 0;
@@ -668,6 +774,7 @@ template <int WPB> __global__ void __launch_bounds__(64 * WPB) k_lean(BatchIn b,
     }
   }
 
+  stamp(4);
   // ---------------------------------------------------------------- 4 DeleteSet
   // bitmap over each client's window [dbase, dmax) (stage + arena bottom; ranges stay at the
   // arena top until they are scattered)
@@ -732,6 +839,7 @@ template <int WPB> __global__ void __launch_bounds__(64 * WPB) k_lean(BatchIn b,
     }
   }
   wsync();
+  stamp(5);
   // component bytes per client
   uint32_t dsb = 0;
   for (uint32_t q = 0; q < nbk; q++) {
@@ -796,12 +904,20 @@ template <int WPB> __global__ void __launch_bounds__(64 * WPB) k_lean(BatchIn b,
     o.out_len[d] = total;
     o.out_start[d] = slot;
   }
+  stamp(6);
+  if (STAMPS && lane == 0) {
+    tst[15] = 0x1EA4;
+    for (int q = 0; q < 16; q++) o.stamps[(size_t)d * 16 + q] = tst[q];
+  }
 }
 
 void launch_lean(const BatchIn &b, const FastOut &o, hipStream_t s) {
   if (!b.n_docs) return;
   constexpr int WPB = 1;
-  hipLaunchKernelGGL((k_lean<WPB>), dim3((b.n_docs + WPB - 1) / WPB), dim3(64 * WPB), 0, s, b, o);
+  if (o.stamps)
+    hipLaunchKernelGGL((k_lean<WPB, true>), dim3((b.n_docs + WPB - 1) / WPB), dim3(64 * WPB), 0, s, b, o);
+  else
+    hipLaunchKernelGGL((k_lean<WPB, false>), dim3((b.n_docs + WPB - 1) / WPB), dim3(64 * WPB), 0, s, b, o);
 }
 
 } // namespace ym
