@@ -107,14 +107,18 @@ def test_lean_shapes_accepted(engine, oracle):
         [upd(5, 0, gc(3)), upd(5, 3, gc(2)), upd(5, 5, item("q"))],                 # GC runs
         [upd(5, 0, item(deleted=4)), upd(5, 4, item(deleted=1))],                    # Deleted content
         [upd(9, 0, item("k", sub="key")), upd(9, 1, item("m", parent=(9, 0)))],      # parent_sub, ID parent
-        [upd(ds=[(4, [(0, 3)])]), upd(ds=[(4, [(3, 2)]), (8, [(10, 1)])])],          # DeleteSet only
+        [upd(4, 0, item("abcdef")), upd(8, 0, item("0123456789ab")),
+         upd(ds=[(4, [(0, 3)])]), upd(ds=[(4, [(3, 2)]), (8, [(10, 1)])])],          # DeleteSets
         [upd(1, 0, item("a")), upd(ds=[(1, [(0, 1)])]), upd(ds=[(1, [(0, 1)])])],     # duplicate ranges
         [upd(2, 0, item("")), upd(2, 0, item("abc"))],                               # zero-length item dropped
         [upd(2, 0, skip(5)), upd(2, 0, item("abc"))],                                # Skip dropped
         [upd(2, 0, None), upd(2, 0, item("abc"))],                                   # empty section
         [upd(6, 0, item("x" * 1000))],                                              # block of ~1 KB
         [upd(c, 0, item("z")) for c in range(16)],                                   # 16 clients
-        [upd(ds=[(c, [(c, 1)]) for c in (11, 5, 1 << 31, 2)])],                      # 4 entries, table order
+        [upd(c, 0, item("xyzw" * 4)) for c in (11, 5, 1 << 31, 2)]
+        + [upd(ds=[(c, [(c % 7, 1)]) for c in (11, 5, 1 << 31, 2)])],                # 4 entries, table order
+        [upd(3, 0, item("a" * 600)), upd(3, 600, item("b" * 300)),
+         upd(ds=[(3, [(10, 700)])]), upd(ds=[(3, [(2, 3), (5, 255), (260, 256)])])],  # ranges > 255 split
         [bytes([1, 1, 0x86, 0, 0, 0x04, 1, 1, ord("t"), 1, ord("a"), 0])],           # non-canonical client
         [upd(3, 0, item("abcdefgh" * 12))] + [upd(3, 96 + i, item("b")) for i in range(200)],
     ]
@@ -139,7 +143,9 @@ def test_lean_shapes_handed_over(engine, oracle):
         [upd(6, 0, item("x" * 1030))],                                              # block > 1 KB
         [upd(6, 0, item("é"))],                                                      # non-ASCII string
         [upd(6, 0, gc(0))],                                                          # zero-length GC
-        [upd(ds=[(4, [(0, 1)])]), upd(ds=[(4, [(3_000_000, 1)])])],                 # DS window too wide
+        [upd(ds=[(4, [(0, 1)])]), upd(ds=[(4, [(3_000_000, 1)])])],                 # DS without blocks
+        [upd(4, 5, item("abc")), upd(ds=[(4, [(0, 3)])])],                          # range below the blocks
+        [upd(4, 0, item("abc")), upd(ds=[(4, [(0, 1)]), (9, [(0, 1)])])],           # client without blocks
         [b""],                                                                       # EOS
         [upd(6, 0, item("ab"))[:-2]],                                                # truncated
         [bytes([1, 1, 6, 0, 0x04, 1, 1, ord("t"), 0x81, 0, ord("a"), 0])],           # non-canonical length

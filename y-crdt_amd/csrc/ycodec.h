@@ -637,7 +637,9 @@ struct SlowRes {
 // Embed / Format with Any values); in lib0 v1 input they are ItemContent::decode's
 // UnexpectedValue (yrs/src/block.rs:1786-1835).  Every kernel that parses content states its
 // batch's grammar first with ym_set_grammar (from every lane, before any parse: no barrier
-// needed); a kernel that never set it reads garbage, which is not the magic: v1 behaviour.
+// needed).  LDS is not cleared between kernels, so a kernel that skipped the call could see a
+// previous kernel's magic: every kernel including this header calls it at entry (k_decode
+// and k_lean with v1: their walks bail on contents they do not restate).
 static __shared__ uint32_t s_grammar_v1x;
 constexpr uint32_t GRAMMAR_V1X_MAGIC = 0x76317821u;
 YM_INLINE void ym_set_grammar(uint32_t v1x) { s_grammar_v1x = v1x ? GRAMMAR_V1X_MAGIC : 0u; }

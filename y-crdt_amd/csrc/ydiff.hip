@@ -1111,6 +1111,7 @@ __device__ __forceinline__ const uint32_t *plan_ops(const DiffBatch &b, const Pl
 // ops (OP_EMIT / OP_WALK / OP_DSQ / OP_DSS: general-planner shapes) are k_exec_cold's, so
 // this kernel keeps a small register footprint (no emit_block call).
 __global__ void __launch_bounds__(256) k_exec(DiffBatch b, PlanScratch ps, const uint64_t *out_off, uint8_t *out) {
+  ym_set_grammar(b.v1x);
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t d = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   if (d >= b.n_docs) return;

@@ -107,6 +107,7 @@ __global__ void __launch_bounds__(DEC_NT, 8) k_decode(const uint8_t *bytes, cons
                                                       uint32_t *rec, uint32_t *ovf) {
   __shared__ __align__(16) uint32_t stage[DEC_STAGE / 4 + 4];
   __shared__ uint32_t ovf_top, n_cx;
+  ym_set_grammar(0); // fast_walk bails on every content it does not restate; v1 by construction
   __shared__ uint32_t cx_at[DEC_NT];
   __shared__ uint16_t cx_lane[DEC_NT], cx_nb[DEC_NT], cx_ne[DEC_NT];
   const uint64_t g0 = (uint64_t)blockIdx.x * DEC_NT;

@@ -38,24 +38,26 @@ namespace ym {
 
 constexpr uint32_t LN_STAGE = 1536;          // staged bytes per round / copy step
 constexpr uint32_t LN_SW = LN_STAGE / 4 + 4; // stage words (+ the word after the last one lvar reads)
-constexpr uint32_t LN_AW = 1792;             // arena words: block records grow up, DS ranges down
+constexpr uint32_t LN_AW = 1280;             // arena words: block records grow up, DS ranges down
 constexpr uint32_t LN_BUF = LN_SW + LN_AW;   // stage + arena, reused whole by the DeleteSet phase
 constexpr uint32_t LN_NBK = 16;              // client buckets per document
-constexpr uint32_t LN_HT = 32;               // client hash slots
 constexpr uint32_t LN_MAXBLEN = 1024;        // block bytes (a copy step must always fit one block)
-constexpr uint32_t LN_DSB = 1024;            // DeleteSet item bytes buffered between DS passes
+constexpr uint32_t LN_DSB = 448;             // DeleteSet item bytes buffered between DS passes (<= 8 per lane)
 constexpr uint32_t LN_DSI = 64;              // DeleteSet items per DS pass (one per lane)
 constexpr uint32_t LN_DSMAXI = 252;          // bytes of one update's DeleteSet
+constexpr uint32_t LN_ORD = 5 * LN_NBK;      // DeleteSet client order scratch (end of buf, after the scatter)
 constexpr uint32_t LN_NONE = 0xFFFFFFFFu;
 
+// buf = [stage | arena]: block records (src | blen << 16 | bucket << 27) from the arena
+// bottom, DeleteSet range records (clock - first block clock of the client | len << 20 |
+// bucket << 28, ranges longer than 255 split) from the top.
 struct LeanLds {
   uint32_t buf[LN_BUF];
-  uint32_t dsb[LN_DSB / 4 + 4];              // DeleteSet items (4-byte aligned), + lvar's read-ahead word
-  uint32_t dsi_off[LN_DSI], dsi_upd[LN_DSI]; // item byte offset | length << 16; doc-relative update
-  uint64_t ht[LN_HT]; // client << 32 | (bucket + 1); 0 = empty
-  uint32_t client[LN_NBK], cnt[LN_NBK], first[LN_NBK], next[LN_NBK], bytes[LN_NBK];
+  uint32_t dsb[LN_DSB / 4 + 4];              // DeleteSet items, byte-packed (a pure varint stream) + read-ahead
+  uint32_t dsv[LN_DSB];                      // their decoded varints (one per terminating byte)
+  uint32_t dsi[LN_DSI];                      // item: byte offset | length << 9 | doc-relative update << 17
+  uint32_t client[LN_NBK], first[LN_NBK], bytes[LN_NBK];
   uint32_t dsfirst[LN_NBK], dsmin[LN_NBK], dsmax[LN_NBK], cur[LN_NBK], eoff[LN_NBK];
-  uint32_t ord[LN_NBK], slots[2 * 2 * LN_NBK]; // DeleteSet client order (table emulation scratch)
 };
 
 // ------------------------------------------------------------------ wave primitives
@@ -79,13 +81,15 @@ template <class T> YM_INLINE T pin(T x) {
 }
 YM_INLINE uint32_t shfl(uint32_t x, int l) { return pin(__shfl(x, l, 64)); }
 YM_INLINE uint64_t shfl(uint64_t x, int l) { return pin(__shfl(x, l, 64)); }
-// inclusive sum over the wave
-YM_INLINE uint32_t wincl(uint32_t x, uint32_t lane) {
-#pragma unroll
-  for (uint32_t o = 1; o < 64; o <<= 1) {
-    const uint32_t y = pin(__shfl_up(x, o, 64));
-    if (lane >= o) x += y;
-  }
+// inclusive sum over the wave in DPP (VALU lane moves, no LDS crossbar round trips): row_shr
+// 1, 2, 4, 8 scans each row of 16 lanes, row_bcast:15 / row_bcast:31 carry the row totals
+YM_INLINE uint32_t wincl(uint32_t x, uint32_t) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false); // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false); // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false); // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false); // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false); // row_bcast:15 -> rows 1, 3
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false); // row_bcast:31 -> rows 2, 3
   return x;
 }
 // number of leading set bits of a lane mask (lanes 0.. that all satisfy a predicate)
@@ -96,128 +100,134 @@ struct LeanUpd {
   uint32_t has_blk, client, clock, len, bpos, blen; // block; bpos = stage byte position
   uint32_t dspos, nent;                             // DeleteSet: stage position (its nds varint), entries
 };
-struct LeanDs {
-  uint32_t nent, nrng;     // entries, ranges
-  uint32_t c0, c1, c2, c3; // entry clients (stream order)
+
+// Branch-free LEB128 u32 at byte p of staged words (read_var_u32, yrs/src/encoding/varint.rs
+// :244-260, wrapping_shl: a 5th byte contributes its low 4 bits): value, length; fine = it
+// ends within 5 bytes and before `end`; canon = re-encoding gives the same bytes.
+struct VarR {
+  uint32_t v, n;
+  bool fine, canon;
 };
+YM_INLINE VarR var_at(const uint32_t *w, uint32_t p, uint32_t end) {
+  const uint32_t q = p >> 2;
+  const uint64_t d = ((uint64_t)w[q + 1] << 32) | w[q];
+  const uint64_t x = d >> ((p & 3) * 8); // >= 5 valid bytes
+  const uint64_t stop = ~x & 0x8080808080ull;
+  const uint32_t n = ((uint32_t)__builtin_ctzll(stop | (1ull << 47)) >> 3) + 1; // 6: no end in 5 bytes
+  const uint32_t xl = (uint32_t)x;
+  uint32_t v = (xl & 0x7Fu) | ((xl >> 1) & 0x3F80u) | ((xl >> 2) & 0x1FC000u) | ((xl >> 3) & 0xFE00000u) |
+               ((uint32_t)(x >> 4) & 0xF0000000u);
+  v &= n < 5 ? (1u << (7 * n)) - 1 : 0xFFFFFFFFu;
+  const uint32_t last = (uint32_t)(x >> (8 * (n - 1))) & 0xFF;
+  VarR r;
+  r.v = v;
+  r.n = n;
+  r.fine = n <= 5 && p + n <= end;
+  r.canon = n == 1 || (last != 0 && (n < 5 || last < 16));
+  return r;
+}
 
 // Validating walk of one staged update (Update::decode_v1, yrs/src/update.rs:714-749,
-// decode_block :433-488, ItemContent::decode block.rs:1786-1835, IdSet::decode
-// id_set.rs:412-426) restricted to the lean shape; false = not the shape (or malformed:
-// the exact walk downstream owns the error codes).  The DeleteSet is only located here (and
-// its entry count read): ds_walk decodes it in a batched DS pass.
-YM_INLINE bool lean_walk(const uint32_t *w, uint32_t start, uint32_t n, LeanUpd &r) {
-  LCur c{w, start, start + n};
-  bool cn;
-  uint32_t ncl, v;
+// decode_block :433-488, ItemContent::decode block.rs:1786-1835) restricted to the lean
+// shape; false = not the shape (or malformed: the exact walk downstream owns the error
+// codes).  Straight-line with an accumulated `ok` (no early exits): lanes of one shape stay
+// converged.  The DeleteSet is only located here (its entry count read); ds_pass decodes it.
+YM_INLINE bool lean_walk(const uint32_t *w, uint32_t p, uint32_t n, LeanUpd &r) {
+  const uint32_t end = p + n;
   r.has_blk = 0;
   r.nent = 0;
-  if (!lvar(c, ncl, cn) || ncl > 1) return false;
-  if (ncl == 1) {
-    uint32_t nb, client, clock;
-    if (!lvar(c, nb, cn) || nb > 1 || !lvar(c, client, cn) || !lvar(c, clock, cn)) return false;
-    if (nb == 1) {
-      const uint32_t bpos = c.p;
-      if (c.p >= c.end) return false;
-      const uint32_t info = lds_byte(w, c.p++);
+  const VarR ncl = var_at(w, p, end);
+  bool ok = ncl.fine && ncl.v <= 1;
+  p += ncl.n;
+  if (ok && ncl.v == 1) {
+    const VarR nb = var_at(w, p, end);
+    const VarR cl = var_at(w, p + nb.n, end);
+    const VarR ck = var_at(w, p + nb.n + cl.n, end);
+    ok = nb.fine && cl.fine && ck.fine && nb.v <= 1;
+    p += nb.n + cl.n + ck.n;
+    if (ok && nb.v == 1) {
+      const uint32_t bpos = p;
+      const uint32_t info = lds_byte(w, p);
+      p++;
       uint32_t len = 0;
       bool keep = true;
       if (info == 0 || info == 10) { // GC / Skip: canonical non-zero length
-        if (!lvar(c, len, cn) || !cn || len == 0) return false;
+        const VarR l = var_at(w, p, end);
+        ok = l.fine && l.canon && l.v != 0;
+        p += l.n;
+        len = l.v;
         keep = info == 0; // a Skip is dropped by IntoBlocks (update.rs:1054)
       } else {
-        // origin / right origin / parent, as fast_walk (ylds.h); any re-encoding -> not lean
-        bool ok = true;
-        if (info & 0x80) ok = lvar(c, v, cn) && cn && lvar(c, v, cn) && cn;
-        if (ok && (info & 0x40)) ok = lvar(c, v, cn) && cn && lvar(c, v, cn) && cn;
-        if (!ok) return false;
+        // origin / right origin (ID = 2 varints each), canonical: the block is copied verbatim
+        if (info & 0x80) {
+          const VarR a0 = var_at(w, p, end), a1 = var_at(w, p + a0.n, end);
+          ok = ok && a0.fine && a0.canon && a1.fine && a1.canon;
+          p += a0.n + a1.n;
+        }
+        if (info & 0x40) {
+          const VarR a0 = var_at(w, p, end), a1 = var_at(w, p + a0.n, end);
+          ok = ok && a0.fine && a0.canon && a1.fine && a1.canon;
+          p += a0.n + a1.n;
+        }
         uint32_t want = info & 0xCF;
-        if ((info & 0xC0) == 0) {
-          uint32_t pi;
-          if (!lvar(c, pi, cn) || !cn || pi > 1) return false;
-          if (!lvar(c, v, cn) || !cn) return false;
-          if (pi == 1) {
-            if (v > c.end - c.p) return false;
-            c.p += v;
-          } else if (!lvar(c, v, cn) || !cn) {
-            return false;
+        if ((info & 0xC0) == 0) { // parent: named root type (1) or ID (0), then parent_sub
+          const VarR pi = var_at(w, p, end), x = var_at(w, p + pi.n, end);
+          ok = ok && pi.fine && pi.canon && pi.v <= 1 && x.fine && x.canon;
+          p += pi.n + x.n;
+          if (pi.v == 1) {
+            ok = ok && x.v <= end - p;
+            p += x.v;
+          } else {
+            const VarR y = var_at(w, p, end);
+            ok = ok && y.fine && y.canon;
+            p += y.n;
           }
           if (info & 0x20) {
             want |= 0x20;
-            if (!lvar(c, v, cn) || !cn || v > c.end - c.p) return false;
-            c.p += v;
+            const VarR sl = var_at(w, p, end);
+            ok = ok && sl.fine && sl.canon && sl.v <= end - (p + sl.n);
+            p += sl.n + sl.v;
           }
         }
-        if (want != info) return false;
         const uint32_t ref = info & 15;
-        if (ref == 1) {
-          if (!lvar(c, len, cn) || !cn) return false;
-        } else if (ref == 4) {
-          if (!lvar(c, v, cn) || !cn || v > c.end - c.p) return false;
-          const uint32_t s0 = c.p;
-          c.p += v;
-          if (v > 1) { // UTF-16 length == byte length for ASCII only
+        const VarR c = var_at(w, p, end);
+        ok = ok && want == info && (ref == 1 || ref == 4) && c.fine && c.canon;
+        p += c.n;
+        len = c.v;
+        if (ok && ref == 4) { // String: UTF-16 length == byte length for ASCII only
+          ok = c.v <= end - p;
+          const uint32_t s0 = p;
+          p += c.v;
+          if (ok && c.v > 1) {
             uint32_t hi = 0;
-            const uint32_t e0 = s0 + v, q0 = s0 >> 2, q1 = (e0 - 1) >> 2;
+            const uint32_t e0 = s0 + c.v, q0 = s0 >> 2, q1 = (e0 - 1) >> 2;
             for (uint32_t q = q0; q <= q1; q++) {
               uint32_t x = w[q];
               if (q == q0) x &= 0xFFFFFFFFu << (8 * (s0 & 3));
               if (q == q1 && (e0 & 3)) x &= 0xFFFFFFFFu >> (8 * (4 - (e0 & 3)));
               hi |= x;
             }
-            if (hi & 0x80808080u) return false;
+            ok = !(hi & 0x80808080u);
           }
-          len = v;
-        } else {
-          return false;
         }
         keep = len != 0; // Item::new drops zero-length items
       }
-      if (keep) {
-        if ((uint64_t)clock + len > 0xFFFFFFFFull || c.p - bpos > LN_MAXBLEN) return false;
+      ok = ok && p <= end;
+      if (ok && keep) {
+        ok = (uint64_t)ck.v + len <= 0xFFFFFFFFull && p - bpos <= LN_MAXBLEN;
         r.has_blk = 1;
-        r.client = client;
-        r.clock = clock;
+        r.client = cl.v;
+        r.clock = ck.v;
         r.len = len;
         r.bpos = bpos;
-        r.blen = c.p - bpos;
+        r.blen = p - bpos;
       }
     }
   }
-  r.dspos = c.p;
-  uint32_t nds;
-  if (!lvar(c, nds, cn) || nds > 4) return false;
-  r.nent = nds;
-  return true;
-}
-
-// One update's DeleteSet (IdSet::decode, id_set.rs:412-426) from the DS item buffer:
-// <= 4 entries with distinct clients (a repeated client replaces the earlier entry: not
-// lean), non-empty ranges.
-YM_INLINE bool ds_walk(const uint32_t *w, uint32_t start, uint32_t n, LeanDs &r) {
-  LCur c{w, start, start + n};
-  bool cn;
-  uint32_t nds;
-  r.nent = r.nrng = 0;
-  r.c0 = r.c1 = r.c2 = r.c3 = 0;
-  if (!lvar(c, nds, cn) || nds > 4) return false;
-  for (uint32_t e = 0; e < nds; e++) {
-    uint32_t client, nr;
-    if (!lvar(c, client, cn) || !lvar(c, nr, cn) || nr == 0 || nr > n) return false;
-    if ((e > 0 && r.c0 == client) || (e > 1 && r.c1 == client) || (e > 2 && r.c2 == client)) return false;
-    if (e == 0) r.c0 = client;
-    else if (e == 1) r.c1 = client;
-    else if (e == 2) r.c2 = client;
-    else r.c3 = client;
-    for (uint32_t q = 0; q < nr; q++) {
-      uint32_t st, ln;
-      if (!lvar(c, st, cn) || !lvar(c, ln, cn)) return false;
-      if (ln == 0 || ln >= (1u << 28) || (uint64_t)st + ln > 0xFFFFFFFFull) return false;
-    }
-    r.nrng += nr;
-  }
-  r.nent = nds;
-  return true;
+  r.dspos = p;
+  const VarR nds = var_at(w, p, end);
+  r.nent = nds.v;
+  return ok && nds.fine && nds.v <= 4;
 }
 
 YM_INLINE uint32_t sel4(uint32_t i, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
@@ -260,32 +270,23 @@ YM_INLINE void ds_pos4(uint32_t n, uint32_t c0, uint32_t c1, uint32_t c2, uint32
 }
 
 // ------------------------------------------------------------------ client buckets
-YM_INLINE int ht_find(const uint64_t *ht, uint32_t c) {
-  uint32_t h = (c * 0x9E3779B9u) >> 27;
-  for (uint32_t p = 0; p < LN_HT; p++) {
-    const uint64_t v = ht[h];
-    if (!v) return -1;
-    if ((uint32_t)(v >> 32) == c) return (int)(uint32_t)v - 1;
-    h = (h + 1) & (LN_HT - 1);
-  }
-  return -1;
+// Client buckets live in registers: lane b of `tabc` holds the client of bucket b < nbk
+// (wave-uniform count), so a lookup is nbk readlane + compare steps, no memory round trip.
+YM_INLINE int tab_find(uint32_t tabc, uint32_t nbk, uint32_t c) {
+  int r = -1;
+  for (uint32_t q = 0; q < nbk; q++) r = rdlane(tabc, q) == c ? (int)q : r;
+  return r;
 }
-// bucket of client c for the lanes with `want`; unknown clients are inserted one per
+// bucket of client c for the lanes with `want`; unknown clients are appended one per
 // iteration (uniform loop).  false = more than LN_NBK clients.
-YM_INLINE bool bucket_of(LeanLds &L, uint32_t lane, uint32_t c, bool want, uint32_t &nbk, int &bk) {
-  bk = want ? ht_find(L.ht, c) : 0;
+YM_INLINE bool bucket_of(uint32_t lane, uint32_t &tabc, uint32_t c, bool want, uint32_t &nbk, int &bk) {
+  bk = want ? tab_find(tabc, nbk, c) : 0;
   for (;;) {
     const uint64_t m = __ballot(want && bk < 0);
     if (!m) return true;
     if (nbk == LN_NBK) return false;
     const uint32_t cn = rdlane(c, (uint32_t)__builtin_ctzll(m));
-    if (lane == 0) {
-      uint32_t h = (cn * 0x9E3779B9u) >> 27;
-      while (L.ht[h]) h = (h + 1) & (LN_HT - 1);
-      L.ht[h] = ((uint64_t)cn << 32) | (nbk + 1);
-      L.client[nbk] = cn;
-    }
-    wsync();
+    if (lane == nbk) tabc = cn;
     if (want && bk < 0 && c == cn) bk = (int)nbk;
     nbk++;
   }
@@ -313,6 +314,29 @@ YM_INLINE void copy_out(const uint32_t *st, uint32_t so, uint8_t *dp, uint32_t n
     }
   }
   for (uint32_t q = 0; q < rem; q++) dq[q] = sb[p + q];
+}
+
+// n bytes LDS -> LDS (byte positions sp -> dp): byte stores up to dp's dword alignment and
+// for the tail, dword stores (v_alignbyte of two source dwords) between
+YM_INLINE void copy_lds(const uint32_t *sw, uint32_t sp, uint32_t *dw, uint32_t dp, uint32_t n) {
+  const uint8_t *sb = (const uint8_t *)sw;
+  uint8_t *db = (uint8_t *)dw;
+  uint32_t head = (4u - (dp & 3)) & 3u;
+  if (head > n) head = n;
+  for (uint32_t q = 0; q < head; q++) db[dp + q] = sb[sp + q];
+  uint32_t p = sp + head, d = dp + head, rem = n - head;
+  if (rem >= 4) {
+    const uint32_t sh = p & 3;
+    uint32_t q4 = p >> 2, lo = sw[q4];
+    for (; rem >= 4; rem -= 4) {
+      const uint32_t hi = sw[++q4];
+      dw[d >> 2] = __builtin_amdgcn_alignbyte(hi, lo, sh);
+      lo = hi;
+      d += 4;
+      p += 4;
+    }
+  }
+  for (uint32_t q = 0; q < rem; q++) db[d + q] = sb[p + q];
 }
 
 // 16-byte staging of absolute bytes [al, al + 16 * n16) (n16 <= LN_STAGE / 16) into buf
@@ -394,8 +418,9 @@ __device__ __noinline__ uint32_t lean_ds_order(uint32_t nbk, const uint32_t *cli
 // Diagnostic build only (STAMPS, env YMERGE_STAMPS): lane 0 records s_memtime at phase
 // boundaries into o.stamps[doc * 16 + k] (k 0..6), per-round sub-phase cycle sums (8..11),
 // rounds (12), marker 0x1EA4 (15); never part of a timed run.
-template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB) k_lean(BatchIn b, FastOut o) {
+template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB, 4) k_lean(BatchIn b, FastOut o) {
   __shared__ LeanLds lds[WPB];
+  ym_set_grammar(b.v1x);
   const uint32_t lane = __lane_id();
   const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t d = blockIdx.x * WPB + w;
@@ -425,13 +450,12 @@ template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB) k_le
       atomicAdd(&o.npath[7 + (why < 7 ? why : 0)], 1u);
     }
   };
-  if (U == 0 || B1 - B0 >= 65536 || u1 - u0 >= 65536) {
+  if (U == 0 || B1 - B0 >= 65536 || U >= 16384) {
     reject(0);
     return;
   }
-  if (lane < LN_HT) L.ht[lane] = 0;
   if (lane < LN_NBK) {
-    L.cnt[lane] = L.bytes[lane] = 0;
+    L.bytes[lane] = 0;
     L.dsfirst[lane] = L.dsmin[lane] = LN_NONE;
     L.dsmax[lane] = 0;
   }
@@ -439,6 +463,8 @@ template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB) k_le
 
   // ---------------------------------------------------------------- 1 decode
   uint32_t nbk = 0, NBk = 0, NR = 0, blkmask = 0;
+  // per bucket (lane = bucket): client, first / next clock, block count
+  uint32_t tabc = 0, bfirst = 0, bnext = 0, bcnt = 0;
   uint32_t bad = 0; // why + 1
   uint32_t ub = 0;
   uint64_t A = B0;
@@ -458,67 +484,139 @@ template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB) k_le
     E = rdlane64(e, k - 1);
     n16 = (uint32_t)((E - al + 15) >> 4);
   }
-  // DeleteSet pass: one buffered item per lane — validate, bucket the entry clients,
-  // table positions, ranges to the arena top, first occurrence / window per client
+  // DeleteSet pass over the item buffer (IdSet::decode, id_set.rs:412-426).  The buffer is
+  // a pure varint stream, so it is decoded wave-parallel: lane j takes bytes [8j, 8j + 8),
+  // its terminating bytes (bit 7 clear) get varint indices by a prefix sum, and each lane
+  // decodes the varints ending in its bytes into dsv.  Then one lane per item assigns the
+  // roles (nds, then per entry client, nr, nr x (start, len)) reading dsv at computable
+  // indices: entry clients -> buckets (unknown clients inserted between steps, uniform
+  // loop), ranges -> arena records (slots by an LDS atomic per entry: the union does not
+  // depend on their order), window per client, first-occurrence keys with the update's
+  // table position (ds_pos4) for multi-entry updates.
   uint32_t dsn = 0, dsused = 0;
   auto ds_pass = [&]() {
+    const uint64_t tp0 = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+    if (STAMPS) tst[14]++;
+    // 1 terminators and varint indices
+    const uint32_t b0 = 8 * lane;
+    const uint32_t vmask = b0 >= dsused ? 0u : (b0 + 8 <= dsused ? 0xFFu : (1u << (dsused - b0)) - 1);
+    const uint32_t wl = L.dsb[2 * lane], wh = L.dsb[2 * lane + 1];
+    const uint32_t tl = ~wl & 0x80808080u, th = ~wh & 0x80808080u;
+    const uint32_t tm = (((tl >> 7) & 1) | ((tl >> 14) & 2) | ((tl >> 21) & 4) | ((tl >> 28) & 8) |
+                         (((th >> 7) & 1) << 4) | (((th >> 14) & 2) << 4) | (((th >> 21) & 4) << 4) |
+                         (((th >> 28) & 8) << 4)) & vmask;
+    const uint32_t ns = (uint32_t)__builtin_popcount(tm);
+    const uint32_t ginc = wincl(ns, lane), gbase = ginc - ns;
+    // 2 decode: a varint starts at byte 0 and after every terminator; its index = the
+    // terminators before it
+    const uint32_t tprev = shfl(tm, lane ? (int)lane - 1 : 0);
+    uint32_t sm = ((tm << 1) | (lane == 0 ? 1u : (tprev >> 7) & 1)) & vmask;
+    bool vok = true;
+    while (sm) {
+      const uint32_t kb = (uint32_t)__builtin_ctz(sm);
+      const VarR r = var_at(L.dsb, b0 + kb, dsused);
+      vok = vok && r.fine;
+      L.dsv[gbase + (uint32_t)__builtin_popcount(tm & ((1u << kb) - 1))] = r.v;
+      sm &= sm - 1;
+    }
+    if (__ballot(!vok)) {
+      bad = 3;
+      return;
+    }
+    wsync();
+    // 3 roles, one lane per item, entries in lockstep (uniform loop over the entry index)
     const bool it = lane < dsn;
-    const uint32_t io = it ? L.dsi_off[lane] : 0, iu = it ? L.dsi_upd[lane] : 0;
-    LeanDs r;
-    bool ok = true;
-    r.nent = r.nrng = r.c0 = r.c1 = r.c2 = r.c3 = 0;
-    if (it) ok = ds_walk(L.dsb, io & 0xFFFF, io >> 16, r);
+    const uint32_t io = it ? L.dsi[lane] : 0, iu = io >> 17;
+    const uint32_t st0 = io & 0x1FF, iend = st0 + ((io >> 9) & 0xFF);
+    const uint32_t ja = st0 >> 3, jz = (iend - 1) >> 3;
+    const uint32_t gba = shfl(gbase, (int)(ja & 63)), tma = shfl(tm, (int)(ja & 63));
+    const uint32_t gbz = shfl(gbase, (int)(jz & 63)), tmz = shfl(tm, (int)(jz & 63));
+    const uint32_t g0 = gba + (uint32_t)__builtin_popcount(tma & ((1u << (st0 & 7)) - 1));
+    const uint32_t zb = (iend - 1) & 7;
+    const uint32_t gend = gbz + (uint32_t)__builtin_popcount(tmz & ((2u << zb) - 1)); // one past the item's varints
+    bool ok = !it || ((tmz >> zb) & 1); // the item's last byte ends a varint
+    const uint32_t nds = it ? L.dsv[g0] : 0;
+    ok = ok && (!it || (nds >= 1 && nds <= 4 && g0 < gend));
+    const uint32_t nent = it && ok ? nds : 0;
+    uint32_t g = g0 + 1;
+    uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+    int b0k = 0, b1k = 0, b2k = 0, b3k = 0;
+#pragma unroll
+    for (uint32_t e = 0; e < 4; e++) {
+      bool ae = ok && e < nent;
+      if (!__ballot(ae)) break;
+      uint32_t cv = 0, nr = 0;
+      if (ae) {
+        ae = g + 2 <= gend;
+        if (ae) {
+          cv = L.dsv[g];
+          nr = L.dsv[g + 1];
+          ae = nr >= 1 && nr <= iend - st0 && g + 2 + 2 * nr <= gend && !(e > 0 && c0 == cv) &&
+               !(e > 1 && c1 == cv) && !(e > 2 && c2 == cv);
+        }
+        ok = ae;
+      }
+      int bq;
+      if (!bucket_of(lane, tabc, cv, ae, nbk, bq)) {
+        bad = 4;
+        return;
+      }
+      if (e == 0) { c0 = cv; b0k = bq; }
+      else if (e == 1) { c1 = cv; b1k = bq; }
+      else if (e == 2) { c2 = cv; b2k = bq; }
+      else { c3 = cv; b3k = bq; }
+      // records relative to the client's first block clock: a deleted range lies in the
+      // client's block window (a delete follows the insert it removes), else not lean
+      const uint32_t fq = shfl(bfirst, bq & 63);
+      const uint32_t f0 = ((blkmask >> (bq & 31)) & 1) ? fq : LN_NONE;
+      uint32_t nrec = 0, mn = LN_NONE, mx = 0;
+      if (ae) {
+        for (uint32_t t = 0; t < nr; t++) {
+          const uint32_t a = L.dsv[g + 2 + 2 * t], l = L.dsv[g + 3 + 2 * t];
+          ae = ae && l != 0 && a >= f0 && a - f0 + l <= (1u << 20) && (uint64_t)a + l <= 0xFFFFFFFFull;
+          nrec += (l + 254) / 255;
+          mn = a < mn ? a : mn;
+          mx = a + l > mx ? a + l : mx;
+        }
+        ok = ae;
+      }
+      const uint32_t rin = wincl(ae ? nrec : 0u, lane), rt = rdlane(rin, 63);
+      if (NBk + NR + rt > LN_AW) {
+        bad = 5;
+        return;
+      }
+      if (ae) {
+        uint32_t sl = NR + rin - nrec;
+        for (uint32_t t = 0; t < nr; t++) {
+          const uint32_t a = L.dsv[g + 2 + 2 * t], l = L.dsv[g + 3 + 2 * t];
+          for (uint32_t q = 0; 255 * q < l; q++) {
+            const uint32_t ln = l - 255 * q < 255 ? l - 255 * q : 255;
+            L.buf[LN_BUF - 1 - sl++] = (a - f0 + 255 * q) | (ln << 20) | ((uint32_t)bq << 28);
+          }
+        }
+        atomicMin(&L.dsmin[bq], mn);
+        atomicMax(&L.dsmax[bq], mx);
+        g += 2 + 2 * nr;
+      }
+      NR += rt;
+    }
+    ok = ok && (!it || g == gend); // no varints after the DeleteSet (trailing bytes: not lean)
     if (__ballot(it && !ok)) {
       bad = 3;
       return;
     }
-    int k0 = 0, k1 = 0, k2b = 0, k3 = 0;
-    bool okb = bucket_of(L, lane, r.c0, it, nbk, k0);
-    if (okb && __ballot(it && r.nent > 1)) okb = bucket_of(L, lane, r.c1, it && r.nent > 1, nbk, k1);
-    if (okb && __ballot(it && r.nent > 2)) okb = bucket_of(L, lane, r.c2, it && r.nent > 2, nbk, k2b);
-    if (okb && __ballot(it && r.nent > 3)) okb = bucket_of(L, lane, r.c3, it && r.nent > 3, nbk, k3);
-    if (!okb) {
-      bad = 4;
-      return;
-    }
-    const uint32_t nr = it ? r.nrng : 0;
-    const uint32_t rin = wincl(nr, lane), rtot = rdlane(rin, 63);
-    if (NBk + 2 * (NR + rtot) > LN_AW) {
-      bad = 5;
-      return;
-    }
     if (it) {
       uint32_t p0 = 0, p1 = 1, p2 = 2, p3 = 3;
-      if (r.nent >= 2) ds_pos4(r.nent, r.c0, r.c1, r.c2, r.c3, p0, p1, p2, p3);
-      LCur c{L.dsb, io & 0xFFFF, (io & 0xFFFF) + (io >> 16)};
-      bool cn;
-      uint32_t nds, x, nre;
-      lvar(c, nds, cn);
-      uint32_t slot_r = NR + rin - nr;
-      for (uint32_t q = 0; q < nds; q++) {
-        lvar(c, x, cn); // client (bucketed above)
-        lvar(c, nre, cn);
-        const uint32_t bq = (uint32_t)sel4(q, (uint32_t)k0, (uint32_t)k1, (uint32_t)k2b, (uint32_t)k3);
-        atomicMin(&L.dsfirst[bq], (iu << 8) | sel4(q, p0, p1, p2, p3));
-        uint32_t mn = LN_NONE, mx = 0;
-        for (uint32_t t = 0; t < nre; t++) {
-          uint32_t st, ln;
-          lvar(c, st, cn);
-          lvar(c, ln, cn);
-          L.buf[LN_BUF - 2 - 2 * slot_r] = st;
-          L.buf[LN_BUF - 1 - 2 * slot_r] = ln | (bq << 28);
-          slot_r++;
-          mn = st < mn ? st : mn;
-          mx = st + ln > mx ? st + ln : mx;
-        }
-        atomicMin(&L.dsmin[bq], mn);
-        atomicMax(&L.dsmax[bq], mx);
-      }
+      if (nent >= 2) ds_pos4(nent, c0, c1, c2, c3, p0, p1, p2, p3);
+      atomicMin(&L.dsfirst[b0k], (iu << 8) | p0);
+      if (nent > 1) atomicMin(&L.dsfirst[b1k], (iu << 8) | p1);
+      if (nent > 2) atomicMin(&L.dsfirst[b2k], (iu << 8) | p2);
+      if (nent > 3) atomicMin(&L.dsfirst[b3k], (iu << 8) | p3);
     }
-    NR += rtot;
+    wsync();
     dsn = 0;
     dsused = 0;
-    wsync();
+    acc(13, tp0);
   };
   uint4 v0, v1;
   stage_load(b.bytes, al, n16, lane, v0, v1);
@@ -572,13 +670,13 @@ template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB) k_le
     // blocks: buckets, contiguity, counts, records
     const bool hb = act && r.has_blk;
     int bk;
-    if (!bucket_of(L, lane, r.client, hb, nbk, bk)) {
+    if (!bucket_of(lane, tabc, r.client, hb, nbk, bk)) {
       bad = 4;
       break;
     }
     const uint64_t mall = __ballot(hb);
     const uint32_t nbr = (uint32_t)__builtin_popcountll(mall);
-    if (NBk + nbr + 2 * NR > LN_AW) { // arena full: not lean
+    if (NBk + nbr + NR > LN_AW) { // arena full: not lean
       bad = 5;
       break;
     }
@@ -595,15 +693,16 @@ template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB) k_le
         const uint32_t last = 63 - (uint32_t)__builtin_clzll(mb);
         const uint32_t c0 = rdlane(r.clock, lead), nend = rdlane(endv, last);
         const bool had = (blkmask >> bb) & 1;
-        const uint32_t nxt = had ? L.next[bb] : c0;
+        const uint32_t nxt = had ? rdlane(bnext, bb) : c0;
         if (hb && (uint32_t)bk == bb) {
           const uint64_t lt = mb & ((1ull << lane) - 1);
           prevl = lt ? 63 - (int)__builtin_clzll(lt) : -1;
           exp0 = nxt;
         }
-        if (lane == 0) {
-          if (!had) L.first[bb] = c0;
-          L.next[bb] = nend;
+        if (lane == bb) {
+          if (!had) bfirst = c0;
+          bnext = nend;
+          bcnt += (uint32_t)__builtin_popcountll(mb);
         }
         blkmask |= 1u << bb;
       }
@@ -614,7 +713,6 @@ template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB) k_le
         break;
       }
       if (hb) {
-        atomicAdd(&L.cnt[bk], 1u);
         atomicAdd(&L.bytes[bk], r.blen);
         const uint32_t src = (uint32_t)(al + r.bpos - B0);
         L.buf[LN_SW + NBk + lanes_below(mall)] = src | (r.blen << 16) | ((uint32_t)bk << 27);
@@ -623,14 +721,13 @@ template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB) k_le
     }
     acc(10, tr2);
     const uint64_t tr3 = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
-    // DeleteSets: copied (4-byte aligned) into the item buffer, decoded 64 at a time by ds_pass
+    // DeleteSets: copied byte-packed into the item buffer, decoded by ds_pass
     {
       const bool hd = act && r.nent > 0;
       const uint32_t ilen = hd ? (uint32_t)(e - al) - r.dspos : 0;
       const uint64_t hm = __ballot(hd);
       if (hm) {
-        const uint32_t isz = (ilen + 3) & ~3u;
-        const uint32_t binc = wincl(isz, lane), btot = rdlane(binc, 63);
+        const uint32_t binc = wincl(ilen, lane), btot = rdlane(binc, 63);
         const uint32_t nit = (uint32_t)__builtin_popcountll(hm);
         if (__ballot(ilen > LN_DSMAXI) || btot > LN_DSB) {
           bad = 3;
@@ -641,12 +738,9 @@ template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB) k_le
           if (bad) break;
         }
         if (hd) {
-          const uint32_t idx = dsn + lanes_below(hm), off = dsused + binc - isz;
-          const uint32_t sh = r.dspos & 3, q0 = r.dspos >> 2;
-          for (uint32_t t = 0; t < isz / 4; t++)
-            L.dsb[off / 4 + t] = __builtin_amdgcn_alignbyte(L.buf[q0 + t + 1], L.buf[q0 + t], sh);
-          L.dsi_off[idx] = off | (ilen << 16);
-          L.dsi_upd[idx] = i;
+          const uint32_t idx = dsn + lanes_below(hm), off = dsused + binc - ilen;
+          copy_lds(L.buf, r.dspos, L.dsb, off, ilen);
+          L.dsi[idx] = off | (ilen << 9) | (i << 17);
         }
         dsn += nit;
         dsused += btot;
@@ -680,8 +774,11 @@ template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB) k_le
 
   // ---------------------------------------------------------------- 2 layout
   const bool lb = lane < nbk;
-  const uint32_t cnt = lb ? L.cnt[lane] : 0, cl = lb ? L.client[lane] : 0, fst = lb ? L.first[lane] : 0,
-                 byt = lb ? L.bytes[lane] : 0;
+  const uint32_t cnt = lb ? bcnt : 0, cl = lb ? tabc : 0, fst = lb ? bfirst : 0, byt = lb ? L.bytes[lane] : 0;
+  if (lb) {
+    L.client[lane] = cl;
+    L.first[lane] = fst;
+  }
   const bool hasb = cnt > 0;
   const uint64_t hbm = __ballot(hasb);
   const uint32_t NC = (uint32_t)__builtin_popcountll(hbm);
@@ -705,7 +802,7 @@ template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB) k_le
   const uint32_t words = hasd ? ((dmx - 1) >> 5) - (dmn >> 5) + 1 : 0;
   const uint32_t win = wincl(words, lane), W = rdlane(win, 63), woff = win - words;
   const uint32_t D = (uint32_t)__builtin_popcountll(__ballot(hasd));
-  if (W + 2 * NR > LN_BUF) {
+  if (W + 2 * NR + LN_ORD > LN_BUF) { // bitmap, component starts / ends, order scratch
     reject(6);
     return;
   }
@@ -787,10 +884,10 @@ template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB) k_le
   }
   wsync();
   for (uint32_t j = lane; j < NR; j += 64) {
-    const uint32_t st = L.buf[LN_BUF - 2 - 2 * j], lw = L.buf[LN_BUF - 1 - 2 * j];
-    const uint32_t bq = lw >> 28, ln = lw & 0x0FFFFFFFu;
+    const uint32_t lw = L.buf[LN_BUF - 1 - j];
+    const uint32_t bq = lw >> 28, ln = (lw >> 20) & 0xFF;
     const uint32_t wo = L.cur[bq], bs = L.eoff[bq];
-    uint32_t a = st - bs;
+    uint32_t a = L.first[bq] + (lw & 0xFFFFF) - bs;
     const uint32_t z = a + ln;
     while (a < z) {
       const uint32_t wi = a >> 5, bo = a & 31, nb = (z - a < 32 - bo) ? z - a : 32 - bo;
@@ -861,10 +958,10 @@ template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB) k_le
   wsync();
   uint32_t total = 0;
   if (lane == 0) {
-    lean_ds_order(nbk, L.client, L.dsfirst, L.ord, L.slots);
+    lean_ds_order(nbk, L.client, L.dsfirst, L.buf + LN_BUF - LN_ORD, L.buf + LN_BUF - 4 * LN_NBK);
     uint32_t pos = ds_start + varlen(D);
     for (uint32_t i2 = 0; i2 < D; i2++) {
-      const uint32_t bq = L.ord[i2];
+      const uint32_t bq = L.buf[LN_BUF - LN_ORD + i2];
       L.eoff[bq] = pos;
       pos += L.bytes[bq];
     }
