@@ -12,7 +12,8 @@
  * inputs, a library-owned `char *` result with its length in `*out_len`, NULL on
  * a decode failure (yffi/src/lib.rs:802-829), error codes as yffi's
  * (yffi/src/lib.rs:1137-1174): 2 VAR_INT, 3 EOS, 4 UNEXPECTED_VALUE, 5 INVALID_JSON,
- * 6 OTHER, 7 NOT_ENOUGH_MEMORY, plus 20 REFERENCE_PANIC (yrs itself would panic)
+ * 6 OTHER, 7 NOT_ENOUGH_MEMORY, plus 20 REFERENCE_PANIC (yrs panics, or overflows u32
+ * clock arithmetic that only a debug build checks: see INTEGRATION.md)
  * and 21 UNSUPPORTED (content class not restated on the device yet).
  *
  * Batched entry points take one contiguous byte arena for many documents:
@@ -59,9 +60,11 @@ char *ydiff_updates_v2(const char *update, uint32_t update_len, const char *stat
 char *yencode_state_vector_from_update_v2(const char *update, uint32_t update_len, uint32_t *out_len);
 /* frees a buffer returned by the three calls above */
 void ymerge_binary_destroy(char *ptr, uint32_t len);
-/* yffi's name, exported as a WEAK symbol: alone it frees this library's buffers; in a
- * process that also links yffi, yffi's (strong) ybinary_destroy wins and this library's
- * buffers must be freed with ymerge_binary_destroy. */
+/* yffi's name, exported as a WEAK symbol for processes that link this library alone.
+ * When yffi is loaded too, the dynamic linker binds the name to whichever shared object
+ * comes first in lookup order (glibc does not rank weak below strong across DSOs), so
+ * which library's buffers it frees depends on link/load order: ymerge_binary_destroy is
+ * the only safe way to free this library's buffers. */
 void ybinary_destroy(char *ptr, uint32_t len);
 /* error code of the last failed call on this thread (0 after a success) */
 uint8_t ymerge_last_error(void);
@@ -182,6 +185,20 @@ int ydiff_updates_v2_batch(ymerge_ctx *ctx, const uint8_t *bytes, const uint64_t
 int yencode_state_vector_from_update_v2_batch(ymerge_ctx *ctx, const uint8_t *bytes, const uint64_t *upd_off,
                                               uint64_t n_docs, ymerge_batch_result **res);
 void ymerge_batch_result_destroy(ymerge_batch_result *res);
+
+/* ---------------------------------------------------------------- multi-device (one node)
+ * The host-memory merge / diff over n_ctx contexts (one per device, ymerge_ctx_create(dev)).
+ * Documents are independent (yrs/src/alt.rs:15-81), so document d is owned by context
+ * splitmix64(id) % n_ctx, id = doc_ids[d] (NULL: id = d); every context merges its shard on
+ * its own host thread and stream, with no cross-device traffic; *res lists the documents in
+ * input order, each byte-identical to the single-context call.  Contexts must not be used by
+ * other threads during the call. */
+int ymerge_updates_v1_batch_multi(ymerge_ctx *const *ctxs, uint32_t n_ctx, const uint8_t *bytes,
+                                  const uint64_t *upd_off, uint64_t n_updates, const uint64_t *doc_upd,
+                                  uint64_t n_docs, const uint64_t *doc_ids, ymerge_batch_result **res);
+int ydiff_updates_v1_batch_multi(ymerge_ctx *const *ctxs, uint32_t n_ctx, const uint8_t *bytes,
+                                 const uint64_t *upd_off, const uint8_t *sv, const uint64_t *sv_off,
+                                 uint64_t n_docs, const uint64_t *doc_ids, ymerge_batch_result **res);
 
 #ifdef __cplusplus
 }

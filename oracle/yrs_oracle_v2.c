@@ -156,6 +156,9 @@ static int usize_buf(const uint8_t *p, size_t n, size_t *idx, span_t *out) {
     if (b < 128) break;
     if (len > 128) return YO_ERR_VAR_INT;
   }
+  /* start + len overflows usize (decoder.rs:268-269): a debug build panics on the add, a
+   * release build on &buf[start..end] with the wrapped end below start */
+  if (num > UINT64_MAX - (uint64_t)*idx) return YO_ERR_REFERENCE_PANIC;
   if (num > n - *idx) return YO_ERR_EOS;
   out->p = p + *idx;
   out->n = (uint32_t)num;

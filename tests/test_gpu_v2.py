@@ -143,4 +143,7 @@ def test_corrupted_v2_updates(engine, oracle):
                 else:
                     u.insert(i, int(rng.integers(256)))
             docs.append([bytes(u) for u in mut])
+    # column lengths at the usize edge: 2^64 - 1 (start + len overflows: panic), 2^63 - 1 (EOS)
+    docs.append([bytes([0] + [0xFF] * 9 + [0x01])])
+    docs.append([bytes([0] + [0xFF] * 8 + [0x7F])])
     _check_merge(engine, oracle, docs)

@@ -1,8 +1,8 @@
 """Multi-process path on CPU (gloo, world_size 2): the doc-hash partition used by
 bench.py / dist.py is disjoint and complete, every rank merges only its shard, and
 the per-rank stats all-gather + max-over-ranks reduction reproduce the single-process
-totals.  The merge itself is the CPU oracle here (test infrastructure; the GPU engine
-runs the same shards on the box)."""
+totals.  The merge in each rank is the CPU oracle in the CPU test, and the HIP engine
+(ymerge.Engine on cuda:0, both ranks sharing the box's one GPU) in the `gpu` variant."""
 import os
 import socket
 
@@ -22,7 +22,7 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, q):
+def _rank_main(rank, world, port, q, use_gpu=False):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     for p in (os.path.join(root, "y-crdt_amd"), os.path.join(root, "oracle")):
@@ -35,7 +35,14 @@ def _rank_main(rank, world, port, q):
     r, w, _ = dist.init_from_env("gloo")
     ids = dist.shard(N_DOCS, r, w)
     b = workloads.text_docs(len(ids), OPS, ids=ids)
-    out, off, st = oracle.merge_batch(b.data, b.upd_off, b.doc_upd, mode=1, threads=2)
+    if use_gpu:
+        import ymerge
+        eng = ymerge.Engine(0)
+        out, off, st = eng.merge_host(b.data, b.upd_off, b.doc_upd)
+        out = out.tobytes()
+        eng.close()
+    else:
+        out, off, st = oracle.merge_batch(b.data, b.upd_off, b.doc_upd, mode=1, threads=2)
     per_doc = {int(ids[k]): out[int(off[k]):int(off[k + 1])] for k in range(len(ids))}
     dist.barrier()
     stats = dist.gather_stats([len(ids), b.n_bytes, len(out), int((st != 0).sum()), 0.1 * (r + 1)])
@@ -46,12 +53,13 @@ def _rank_main(rank, world, port, q):
     dist.finalize()
 
 
-def test_two_rank_sharded_merge(oracle):
+@pytest.mark.parametrize("use_gpu", [False, pytest.param(True, marks=pytest.mark.gpu)])
+def test_two_rank_sharded_merge(oracle, use_gpu):
     import workloads
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, q, use_gpu)) for r in range(world)]
     for p in procs:
         p.start()
     stats, gathered = q.get(timeout=240)

@@ -114,4 +114,7 @@ def test_v2_errors(oracle):
     assert oracle.status_of(oracle.merge_updates_v2, [b""])[0] == 2
     assert oracle.status_of(oracle.merge_updates_v2, [bytes([0, 5, 1])])[0] == 3
     assert oracle.status_of(oracle.merge_updates_v2, [bytes([0, 0x80])])[0] == 20
+    # column length 2^64 - 1 (10-byte varint): start + len overflows usize (decoder.rs:268-269)
+    assert oracle.status_of(oracle.merge_updates_v2, [bytes([0] + [0xFF] * 9 + [0x01])])[0] == 20
+    assert oracle.status_of(oracle.merge_updates_v2, [bytes([0] + [0xFF] * 8 + [0x7F])])[0] == 3
     assert oracle.status_of(oracle.merge_updates_v2, [V2_HEADER])[0] == 3  # no block count in the rest

@@ -6,7 +6,7 @@ TAG=${1:-r}; shift
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu --maxfail=10 -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
 rc=$?
 tail -3 $OUT/pytest_gpu.log
 [ $rc -ne 0 ] && exit $rc

@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "ykernels.h"
@@ -653,6 +654,113 @@ extern "C" void ymerge_batch_result_destroy(ymerge_batch_result *r) {
   free(r);
 }
 
+// ---------------------------------------------------------------- multi-device (one node)
+// Documents are independent (yrs/src/alt.rs:15-81 take one document's updates), so a batch
+// spreads over the contexts' devices by document hash with no cross-device traffic: document
+// d goes to context splitmix64(id) % n_ctx (id = doc_ids[d], else d: the partition bench.py
+// uses across ranks, workloads.shard_ids).  Each shard's sub-batch is gathered from the
+// caller's arena and run on its own host thread (one HIP stream per context); the outputs
+// are put back in input order.
+static uint64_t doc_hash(uint64_t id) {
+  uint64_t z = id + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+struct Shard {
+  std::vector<uint64_t> docs;           // input document indices, ascending
+  std::vector<uint8_t> bytes;           // gathered arena (+16 readable bytes)
+  std::vector<uint64_t> upd_off, doc_upd, sv_off;
+  std::vector<uint8_t> sv;
+  ymerge_batch_result *res = nullptr;
+  int rc = 0;
+};
+
+// op: 0 merge (doc_upd groups updates), 1 diff (one update + one state vector per document)
+static int run_multi(ymerge_ctx *const *ctxs, uint32_t n_ctx, int op, const uint8_t *bytes, const uint64_t *upd_off,
+                     const uint64_t *doc_upd, const uint8_t *sv, const uint64_t *sv_off, uint64_t n_docs,
+                     const uint64_t *doc_ids, ymerge_batch_result **out) {
+  if (!ctxs || !n_ctx || !out) return YMERGE_ERR_OTHER;
+  for (uint32_t k = 0; k < n_ctx; k++)
+    if (!ctxs[k]) return YMERGE_ERR_OTHER;
+  std::vector<Shard> sh(n_ctx);
+  std::vector<uint32_t> owner(n_docs);
+  for (uint64_t d = 0; d < n_docs; d++) {
+    const uint32_t k = (uint32_t)(doc_hash(doc_ids ? doc_ids[d] : d) % n_ctx);
+    owner[d] = k;
+    sh[k].docs.push_back(d);
+  }
+  auto work = [&](uint32_t k) {
+    Shard &s = sh[k];
+    const uint64_t n = s.docs.size();
+    s.upd_off.push_back(0);
+    if (op == 0) s.doc_upd.push_back(0);
+    else s.sv_off.push_back(0);
+    for (uint64_t d : s.docs) {
+      const uint64_t u0 = op == 0 ? doc_upd[d] : d, u1 = op == 0 ? doc_upd[d + 1] : d + 1;
+      const uint64_t base = s.bytes.size();
+      s.bytes.insert(s.bytes.end(), bytes + upd_off[u0], bytes + upd_off[u1]);
+      for (uint64_t u = u0; u < u1; u++) s.upd_off.push_back(base + upd_off[u + 1] - upd_off[u0]);
+      if (op == 0) s.doc_upd.push_back(s.upd_off.size() - 1);
+      else {
+        s.sv.insert(s.sv.end(), sv + sv_off[d], sv + sv_off[d + 1]);
+        s.sv_off.push_back(s.sv.size());
+      }
+    }
+    s.bytes.resize(s.bytes.size() + 16, 0);
+    if (op == 1) s.sv.resize(s.sv.size() + 16, 0);
+    if (op == 0)
+      s.rc = ymerge_updates_v1_batch(ctxs[k], s.bytes.data(), s.upd_off.data(), s.upd_off.size() - 1,
+                                     s.doc_upd.data(), n, &s.res);
+    else
+      s.rc = ydiff_updates_v1_batch(ctxs[k], s.bytes.data(), s.upd_off.data(), s.sv.data(), s.sv_off.data(), n,
+                                    &s.res);
+  };
+  std::vector<std::thread> th;
+  for (uint32_t k = 1; k < n_ctx; k++) th.emplace_back(work, k);
+  work(0);
+  for (auto &t : th) t.join();
+  int rc = 0;
+  uint64_t total = 0;
+  for (auto &s : sh) {
+    if (s.rc && !rc) rc = s.rc;
+    if (s.res) total += s.res->out_bytes;
+  }
+  ymerge_batch_result *r = rc ? nullptr : alloc_result(n_docs, total);
+  if (!rc && !r) rc = YMERGE_ERR_NOT_ENOUGH_MEMORY;
+  if (!rc) {
+    std::vector<uint64_t> pos(n_ctx, 0);
+    uint64_t o = 0;
+    r->out_off[0] = 0;
+    for (uint64_t d = 0; d < n_docs; d++) {
+      const uint32_t k = owner[d];
+      const ymerge_batch_result *sr = sh[k].res;
+      const uint64_t i = pos[k]++;
+      const uint64_t a = sr->out_off[i], len = sr->out_off[i + 1] - a;
+      if (len) memcpy(r->out + o, sr->out + a, len);
+      o += len;
+      r->out_off[d + 1] = o;
+      r->status[d] = sr->status[i];
+    }
+    *out = r;
+  }
+  for (auto &s : sh) ymerge_batch_result_destroy(s.res);
+  return rc;
+}
+
+extern "C" int ymerge_updates_v1_batch_multi(ymerge_ctx *const *ctxs, uint32_t n_ctx, const uint8_t *bytes,
+                                             const uint64_t *upd_off, uint64_t n_updates, const uint64_t *doc_upd,
+                                             uint64_t n_docs, const uint64_t *doc_ids, ymerge_batch_result **res) {
+  (void)n_updates;
+  return run_multi(ctxs, n_ctx, 0, bytes, upd_off, doc_upd, nullptr, nullptr, n_docs, doc_ids, res);
+}
+extern "C" int ydiff_updates_v1_batch_multi(ymerge_ctx *const *ctxs, uint32_t n_ctx, const uint8_t *bytes,
+                                            const uint64_t *upd_off, const uint8_t *sv, const uint64_t *sv_off,
+                                            uint64_t n_docs, const uint64_t *doc_ids, ymerge_batch_result **res) {
+  return run_multi(ctxs, n_ctx, 1, bytes, upd_off, nullptr, sv, sv_off, n_docs, doc_ids, res);
+}
+
 // ---------------------------------------------------------------- single document API
 // The single-document calls run on one lazily created context per device; the device is
 // ymerge_set_default_device(), else env YMERGE_DEVICE, else 0.
@@ -914,7 +1022,8 @@ extern "C" char *yencode_state_vector_from_update_v2(const char *update, uint32_
 }
 
 extern "C" void ymerge_binary_destroy(char *ptr, uint32_t) { free(ptr); }
-// yffi-compatible name, exported WEAK: a process that also links yffi (whose strong
-// ybinary_destroy frees yrs' buffers) keeps yffi's definition and must free this library's
-// buffers with ymerge_binary_destroy; alone, ybinary_destroy resolves here.
+// yffi-compatible name for processes that link this library alone.  Next to yffi the
+// dynamic linker binds it to the first DSO in lookup order (weak does not lose to strong
+// across shared objects), so include/ymerge.h names ymerge_binary_destroy as the only safe
+// free for this library's buffers.
 extern "C" __attribute__((weak)) void ybinary_destroy(char *ptr, uint32_t len) { ymerge_binary_destroy(ptr, len); }

@@ -161,6 +161,9 @@ __device__ int usize_buf(const uint8_t *p, uint32_t n, uint32_t &idx, uint32_t &
     len += 7;
     if (b < 128) break;
   }
+  // start + len overflows usize: panics in a debug build (add) and in a release build too
+  // (the wrapped end is below start: slice index order panic)
+  if (num > ~0ull - idx) return E_PANIC;
   if (num > (uint64_t)(n - idx)) return E_EOS;
   bp = idx;
   bl = (uint32_t)num;

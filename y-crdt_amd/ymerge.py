@@ -47,6 +47,20 @@ class _DevRes(ctypes.Structure):
                 ("d_status", ctypes.c_void_p), ("arena_bytes", ctypes.c_uint64), ("out_bytes", ctypes.c_uint64)]
 
 
+class _BatchRes(ctypes.Structure):
+    _fields_ = [("out", ctypes.c_void_p), ("out_off", ctypes.c_void_p), ("status", ctypes.c_void_p),
+                ("n_docs", ctypes.c_uint64), ("out_bytes", ctypes.c_uint64)]
+
+
+# host-memory batch entries (include/ymerge.h, "batched, host memory"): name -> argument kinds
+# (b = byte arena, o = u64 offsets, n = count); every one ends with (n_docs, result**)
+HOST_BATCH = {
+    "ymerge_updates_v1_batch": "bono", "ymerge_updates_v2_batch": "bono",
+    "ydiff_updates_v1_batch": "bobo", "ydiff_updates_v2_batch": "bobo",
+    "yencode_state_vector_from_update_v1_batch": "bo", "yencode_state_vector_from_update_v2_batch": "bo",
+    "ysync_step1_v1_batch": "bo", "ysync_step2_v1_batch": "bobo",
+}
+
 _lib = None
 
 
@@ -95,6 +109,8 @@ def lib():
     L.ydiff_updates_v1_batch.argtypes = [vp, vp, vp, vp, vp, u64, c.POINTER(c.c_void_p)]
     L.yencode_state_vector_from_update_v1_batch.argtypes = [vp, vp, vp, u64, c.POINTER(c.c_void_p)]
     L.ymerge_batch_result_destroy.argtypes = [vp]
+    for name, kinds in HOST_BATCH.items():
+        getattr(L, name).argtypes = [vp] + [u64 if k == "n" else vp for k in kinds] + [u64, c.POINTER(c.c_void_p)]
     _lib = L
     return L
 
@@ -162,6 +178,56 @@ def encode_state_vector_from_update_v2(update):
     return _take(lib().yencode_state_vector_from_update_v2(u, len(u), ctypes.byref(n)), n)
 
 
+def _multi(fn_name, engines, arrays, doc_ids):
+    L = lib()
+    n_ctx = len(engines)
+    ctxs = (ctypes.c_void_p * n_ctx)(*[e._ctx for e in engines])
+    keep, args = [], []
+    for k, a in arrays:
+        if k == "n":
+            args.append(ctypes.c_uint64(int(a)))
+            continue
+        a = np.ascontiguousarray(a, dtype=np.uint8 if k == "b" else np.uint64)
+        if not len(a):
+            a = np.zeros(1, a.dtype)
+        keep.append(a)
+        args.append(ctypes.c_void_p(a.ctypes.data))
+    n_docs = len(arrays[-1][1]) - 1
+    ids = None if doc_ids is None else np.ascontiguousarray(doc_ids, dtype=np.uint64)
+    pres = ctypes.c_void_p()
+    rc = getattr(L, fn_name)(ctxs, ctypes.c_uint32(n_ctx), *args, ctypes.c_uint64(n_docs),
+                             ctypes.c_void_p(ids.ctypes.data if ids is not None else 0), ctypes.byref(pres))
+    if rc:
+        raise DeviceError(f"{fn_name} failed ({rc})")
+    return _read_batch_result(pres, n_docs)
+
+
+def merge_multi(engines, data, upd_off, doc_upd, doc_ids=None):
+    """ymerge_updates_v1_batch_multi: the batch spread over several contexts (devices) by
+    document hash; outputs in input order: (out, out_off, status)."""
+    return _multi("ymerge_updates_v1_batch_multi", engines,
+                  [("b", data), ("o", upd_off), ("n", len(upd_off) - 1), ("o", doc_upd)], doc_ids)
+
+
+def diff_multi(engines, ubytes, u_off, svbytes, sv_off, doc_ids=None):
+    """ydiff_updates_v1_batch_multi (one update + one remote state vector per document)."""
+    return _multi("ydiff_updates_v1_batch_multi", engines,
+                  [("b", ubytes), ("o", u_off), ("b", svbytes), ("o", sv_off)], doc_ids)
+
+
+def _read_batch_result(pres, n_docs):
+    try:
+        r = _BatchRes.from_address(pres.value)
+        nb = int(r.out_bytes)
+        out = np.ctypeslib.as_array((ctypes.c_uint8 * max(1, nb)).from_address(r.out))[:nb].copy()
+        off = np.ctypeslib.as_array((ctypes.c_uint64 * (n_docs + 1)).from_address(r.out_off)).copy()
+        st = (np.ctypeslib.as_array((ctypes.c_uint8 * n_docs).from_address(r.status)).copy() if n_docs
+              else np.zeros(0, np.uint8))
+    finally:
+        lib().ymerge_batch_result_destroy(pres)
+    return out, off, st
+
+
 class DeviceResult:
     def __init__(self, engine, res, n_docs):
         self.engine, self.res, self.n_docs = engine, res, n_docs
@@ -203,7 +269,10 @@ class Engine:
             pass
 
     def merge_device(self, d_bytes, n_bytes, d_upd_off, n_updates, d_doc_upd, n_docs, version=1):
-        """Inputs are device pointers (ints) into HBM; returns a DeviceResult.  version 2 = lib0 v2."""
+        """Inputs are device pointers (ints) into HBM; returns a DeviceResult.  version 2 = lib0 v2.
+
+        The byte arena must stay readable 16 bytes past n_bytes (the kernels stage whole
+        16-byte groups): allocate it from `padded(data)`, as `merge_host` does."""
         res = _DevRes()
         fn = lib().ymerge_updates_v2_batch_device if version == 2 else lib().ymerge_updates_v1_batch_device
         rc = fn(self._ctx, d_bytes, n_bytes, d_upd_off, n_updates, d_doc_upd, n_docs, ctypes.byref(res))
@@ -212,6 +281,8 @@ class Engine:
         return DeviceResult(self, res, n_docs)
 
     def diff_device(self, d_bytes, d_upd_off, d_sv, d_sv_off, n_docs, version=1):
+        """Device pointers in, DeviceResult out; the update arena must stay readable 16 bytes
+        past its end (`padded`), as for merge_device."""
         res = _DevRes()
         fn = lib().ydiff_updates_v2_batch_device if version == 2 else lib().ydiff_updates_v1_batch_device
         rc = fn(self._ctx, d_bytes, d_upd_off, d_sv, d_sv_off, n_docs, ctypes.byref(res))
@@ -262,6 +333,30 @@ class Engine:
         s = _Stats()
         lib().ymerge_last_stats(self._ctx, ctypes.byref(s))
         return {k: getattr(s, k) for k, _ in _Stats._fields_}
+
+    def host_batch(self, name, *arrays):
+        """Calls a host-memory batch entry of the C ABI (HOST_BATCH: the server-facing form,
+        host pointers in, a library-owned ymerge_batch_result out) and copies the result:
+        (out bytes, out_off[n_docs + 1], status[n_docs]).  Arrays are passed in the
+        order of the C signature without the trailing n_docs, which is taken from the
+        last offsets array."""
+        kinds = HOST_BATCH[name]
+        keep, args = [], []
+        for k, a in zip(kinds, arrays):
+            if k == "n":
+                args.append(int(a))
+                continue
+            a = np.ascontiguousarray(a, dtype=np.uint8 if k == "b" else np.uint64)
+            if not len(a):
+                a = np.zeros(1, a.dtype)
+            keep.append(a)
+            args.append(a.ctypes.data)
+        n_docs = len(arrays[-1]) - 1
+        pres = ctypes.c_void_p()
+        rc = getattr(lib(), name)(self._ctx, *args, n_docs, ctypes.byref(pres))
+        if rc:
+            raise DeviceError(f"{name} failed ({rc})")
+        return _read_batch_result(pres, n_docs)
 
     def _host_batch(self, args_dev, fn):
         import torch
