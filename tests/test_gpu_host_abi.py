@@ -47,7 +47,8 @@ def test_merge_v1_batch(engine, oracle):
 
 
 def test_merge_v2_batch(engine, oracle):
-    docs = [[oracle.convert_update_v1_to_v2(u) for u in ups] for ups in _docs() if all(ups)]
+    docs = [ups for ups in _docs() if all(oracle.status_of(oracle.convert_update_v1_to_v2, u)[0] == 0 for u in ups)]
+    docs = [[oracle.convert_update_v1_to_v2(u) for u in ups] for ups in docs]
     b = batch_of(docs)
     got = engine.host_batch("ymerge_updates_v2_batch", b.data, b.upd_off, len(b.upd_off) - 1, b.doc_upd)
     _same(got, oracle.merge_batch(b.data, b.upd_off, b.doc_upd, mode=1, threads=8, version=2))
@@ -64,8 +65,10 @@ def _merged(oracle):
 
 
 def _remote(oracle, ub, uoff):
-    sv, svoff, _ = oracle.sv_batch(ub, uoff, threads=8)
-    rsv, rsv_off = workloads.remote_svs(np.frombuffer(sv, np.uint8), svoff)
+    sv, svoff, st = oracle.sv_batch(ub, uoff, threads=8)
+    svs = [bytes(sv[int(svoff[d]):int(svoff[d + 1])]) if st[d] == 0 else b"\x00" for d in range(len(uoff) - 1)]
+    sva = np.frombuffer(b"".join(svs), np.uint8)
+    rsv, rsv_off = workloads.remote_svs(sva, np.cumsum([0] + [len(x) for x in svs]).astype(np.uint64))
     svs = [rsv[int(rsv_off[d]):int(rsv_off[d + 1])].tobytes() for d in range(len(uoff) - 1)]
     svs[-4] = bytes(ALT_DIFF[1])
     svs[-1] = b"\x05"  # truncated state vector

@@ -89,8 +89,8 @@ def main_lean(kind, n):
         v = st[ok][:, 8 + i].astype(np.float64)
         print(f"  decode/{nm:16s} {v.mean():10.0f} cycles/doc  {(v / np.maximum(rounds, 1)).mean():8.0f} per round")
     dsp, npass = st[ok][:, 13].astype(np.float64), st[ok][:, 14].astype(np.float64)
-    print(f"  of which ds_pass: {dsp.mean():.0f} cycles/doc, {npass.mean():.1f} passes/doc, "
-          f"{(dsp / np.maximum(npass, 1)).mean():.0f} cycles/pass")
+    print(f"  ds_union = DeleteSet batches: {dsp.mean():.0f} cycles/doc, {npass.mean():.1f} batches/doc, "
+          f"{(dsp / np.maximum(npass, 1)).mean():.0f} cycles/batch")
 
 
 def main():

@@ -42,22 +42,20 @@ constexpr uint32_t LN_AW = 1280;             // arena words: block records grow 
 constexpr uint32_t LN_BUF = LN_SW + LN_AW;   // stage + arena, reused whole by the DeleteSet phase
 constexpr uint32_t LN_NBK = 16;              // client buckets per document
 constexpr uint32_t LN_MAXBLEN = 1024;        // block bytes (a copy step must always fit one block)
-constexpr uint32_t LN_DSB = 448;             // DeleteSet item bytes buffered between DS passes (<= 8 per lane)
-constexpr uint32_t LN_DSI = 64;              // DeleteSet items per DS pass (one per lane)
 constexpr uint32_t LN_DSMAXI = 252;          // bytes of one update's DeleteSet
-constexpr uint32_t LN_ORD = 5 * LN_NBK;      // DeleteSet client order scratch (end of buf, after the scatter)
+constexpr uint32_t LN_DSW = 1024;            // DeleteSet batch window: 16 staged bytes per lane
+constexpr uint32_t LN_ORD = 7 * LN_NBK;      // DeleteSet client order scratch (end of buf, after the scatter):
+                                             // order, hash slots (2x) + copy, clients, entry offsets
 constexpr uint32_t LN_NONE = 0xFFFFFFFFu;
 
 // buf = [stage | arena]: block records (src | blen << 16 | bucket << 27) from the arena
-// bottom, DeleteSet range records (clock - first block clock of the client | len << 20 |
-// bucket << 28, ranges longer than 255 split) from the top.
+// bottom; from the top, one word per DeleteSet item: its end offset in the document's DS
+// scratch (the items themselves are copied verbatim to HBM, see phase 1).
 struct LeanLds {
   uint32_t buf[LN_BUF];
-  uint32_t dsb[LN_DSB / 4 + 4];              // DeleteSet items, byte-packed (a pure varint stream) + read-ahead
-  uint32_t dsv[LN_DSB];                      // their decoded varints (one per terminating byte)
-  uint32_t dsi[LN_DSI];                      // item: byte offset | length << 9 | doc-relative update << 17
-  uint32_t client[LN_NBK], first[LN_NBK], bytes[LN_NBK];
-  uint32_t dsfirst[LN_NBK], dsmin[LN_NBK], dsmax[LN_NBK], cur[LN_NBK], eoff[LN_NBK];
+  // per-bucket values updated by LDS atomics from many lanes; the rest of the per-bucket
+  // state is register-resident (lane b = bucket b: client, first / next clock, copy cursor)
+  uint32_t bytes[LN_NBK], dsfirst[LN_NBK];
 };
 
 // ------------------------------------------------------------------ wave primitives
@@ -131,7 +129,7 @@ YM_INLINE VarR var_at(const uint32_t *w, uint32_t p, uint32_t end) {
 // decode_block :433-488, ItemContent::decode block.rs:1786-1835) restricted to the lean
 // shape; false = not the shape (or malformed: the exact walk downstream owns the error
 // codes).  Straight-line with an accumulated `ok` (no early exits): lanes of one shape stay
-// converged.  The DeleteSet is only located here (its entry count read); ds_pass decodes it.
+// converged.  The DeleteSet is only located here (its entry count read); phase 4 decodes it.
 YM_INLINE bool lean_walk(const uint32_t *w, uint32_t p, uint32_t n, LeanUpd &r) {
   const uint32_t end = p + n;
   r.has_blk = 0;
@@ -418,7 +416,8 @@ __device__ __noinline__ uint32_t lean_ds_order(uint32_t nbk, const uint32_t *cli
 // Diagnostic build only (STAMPS, env YMERGE_STAMPS): lane 0 records s_memtime at phase
 // boundaries into o.stamps[doc * 16 + k] (k 0..6), per-round sub-phase cycle sums (8..11),
 // rounds (12), marker 0x1EA4 (15); never part of a timed run.
-template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB, 4) k_lean(BatchIn b, FastOut o) {
+template <int WPB, int OCC, bool STAMPS>
+__global__ void __launch_bounds__(64 * WPB, OCC) k_lean(BatchIn b, FastOut o) {
   __shared__ LeanLds lds[WPB];
   ym_set_grammar(b.v1x);
   const uint32_t lane = __lane_id();
@@ -456,13 +455,16 @@ template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB, 4) k
   }
   if (lane < LN_NBK) {
     L.bytes[lane] = 0;
-    L.dsfirst[lane] = L.dsmin[lane] = LN_NONE;
-    L.dsmax[lane] = 0;
+    L.dsfirst[lane] = LN_NONE;
   }
   wsync();
 
   // ---------------------------------------------------------------- 1 decode
-  uint32_t nbk = 0, NBk = 0, NR = 0, blkmask = 0;
+  uint32_t nbk = 0, NBk = 0, NI = 0, blkmask = 0;
+  // DeleteSet scratch: the upper half of this document's output slot (capacity 2 x input +
+  // 64; a lean document's output is at most its input + 10 bytes), DSB bytes used
+  uint8_t *const dscr = out + (B1 - B0) + 64;
+  uint32_t DSB = 0;
   // per bucket (lane = bucket): client, first / next clock, block count
   uint32_t tabc = 0, bfirst = 0, bnext = 0, bcnt = 0;
   uint32_t bad = 0; // why + 1
@@ -484,140 +486,6 @@ template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB, 4) k
     E = rdlane64(e, k - 1);
     n16 = (uint32_t)((E - al + 15) >> 4);
   }
-  // DeleteSet pass over the item buffer (IdSet::decode, id_set.rs:412-426).  The buffer is
-  // a pure varint stream, so it is decoded wave-parallel: lane j takes bytes [8j, 8j + 8),
-  // its terminating bytes (bit 7 clear) get varint indices by a prefix sum, and each lane
-  // decodes the varints ending in its bytes into dsv.  Then one lane per item assigns the
-  // roles (nds, then per entry client, nr, nr x (start, len)) reading dsv at computable
-  // indices: entry clients -> buckets (unknown clients inserted between steps, uniform
-  // loop), ranges -> arena records (slots by an LDS atomic per entry: the union does not
-  // depend on their order), window per client, first-occurrence keys with the update's
-  // table position (ds_pos4) for multi-entry updates.
-  uint32_t dsn = 0, dsused = 0;
-  auto ds_pass = [&]() {
-    const uint64_t tp0 = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
-    if (STAMPS) tst[14]++;
-    // 1 terminators and varint indices
-    const uint32_t b0 = 8 * lane;
-    const uint32_t vmask = b0 >= dsused ? 0u : (b0 + 8 <= dsused ? 0xFFu : (1u << (dsused - b0)) - 1);
-    const uint32_t wl = L.dsb[2 * lane], wh = L.dsb[2 * lane + 1];
-    const uint32_t tl = ~wl & 0x80808080u, th = ~wh & 0x80808080u;
-    const uint32_t tm = (((tl >> 7) & 1) | ((tl >> 14) & 2) | ((tl >> 21) & 4) | ((tl >> 28) & 8) |
-                         (((th >> 7) & 1) << 4) | (((th >> 14) & 2) << 4) | (((th >> 21) & 4) << 4) |
-                         (((th >> 28) & 8) << 4)) & vmask;
-    const uint32_t ns = (uint32_t)__builtin_popcount(tm);
-    const uint32_t ginc = wincl(ns, lane), gbase = ginc - ns;
-    // 2 decode: a varint starts at byte 0 and after every terminator; its index = the
-    // terminators before it
-    const uint32_t tprev = shfl(tm, lane ? (int)lane - 1 : 0);
-    uint32_t sm = ((tm << 1) | (lane == 0 ? 1u : (tprev >> 7) & 1)) & vmask;
-    bool vok = true;
-    while (sm) {
-      const uint32_t kb = (uint32_t)__builtin_ctz(sm);
-      const VarR r = var_at(L.dsb, b0 + kb, dsused);
-      vok = vok && r.fine;
-      L.dsv[gbase + (uint32_t)__builtin_popcount(tm & ((1u << kb) - 1))] = r.v;
-      sm &= sm - 1;
-    }
-    if (__ballot(!vok)) {
-      bad = 3;
-      return;
-    }
-    wsync();
-    // 3 roles, one lane per item, entries in lockstep (uniform loop over the entry index)
-    const bool it = lane < dsn;
-    const uint32_t io = it ? L.dsi[lane] : 0, iu = io >> 17;
-    const uint32_t st0 = io & 0x1FF, iend = st0 + ((io >> 9) & 0xFF);
-    const uint32_t ja = st0 >> 3, jz = (iend - 1) >> 3;
-    const uint32_t gba = shfl(gbase, (int)(ja & 63)), tma = shfl(tm, (int)(ja & 63));
-    const uint32_t gbz = shfl(gbase, (int)(jz & 63)), tmz = shfl(tm, (int)(jz & 63));
-    const uint32_t g0 = gba + (uint32_t)__builtin_popcount(tma & ((1u << (st0 & 7)) - 1));
-    const uint32_t zb = (iend - 1) & 7;
-    const uint32_t gend = gbz + (uint32_t)__builtin_popcount(tmz & ((2u << zb) - 1)); // one past the item's varints
-    bool ok = !it || ((tmz >> zb) & 1); // the item's last byte ends a varint
-    const uint32_t nds = it ? L.dsv[g0] : 0;
-    ok = ok && (!it || (nds >= 1 && nds <= 4 && g0 < gend));
-    const uint32_t nent = it && ok ? nds : 0;
-    uint32_t g = g0 + 1;
-    uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
-    int b0k = 0, b1k = 0, b2k = 0, b3k = 0;
-#pragma unroll
-    for (uint32_t e = 0; e < 4; e++) {
-      bool ae = ok && e < nent;
-      if (!__ballot(ae)) break;
-      uint32_t cv = 0, nr = 0;
-      if (ae) {
-        ae = g + 2 <= gend;
-        if (ae) {
-          cv = L.dsv[g];
-          nr = L.dsv[g + 1];
-          ae = nr >= 1 && nr <= iend - st0 && g + 2 + 2 * nr <= gend && !(e > 0 && c0 == cv) &&
-               !(e > 1 && c1 == cv) && !(e > 2 && c2 == cv);
-        }
-        ok = ae;
-      }
-      int bq;
-      if (!bucket_of(lane, tabc, cv, ae, nbk, bq)) {
-        bad = 4;
-        return;
-      }
-      if (e == 0) { c0 = cv; b0k = bq; }
-      else if (e == 1) { c1 = cv; b1k = bq; }
-      else if (e == 2) { c2 = cv; b2k = bq; }
-      else { c3 = cv; b3k = bq; }
-      // records relative to the client's first block clock: a deleted range lies in the
-      // client's block window (a delete follows the insert it removes), else not lean
-      const uint32_t fq = shfl(bfirst, bq & 63);
-      const uint32_t f0 = ((blkmask >> (bq & 31)) & 1) ? fq : LN_NONE;
-      uint32_t nrec = 0, mn = LN_NONE, mx = 0;
-      if (ae) {
-        for (uint32_t t = 0; t < nr; t++) {
-          const uint32_t a = L.dsv[g + 2 + 2 * t], l = L.dsv[g + 3 + 2 * t];
-          ae = ae && l != 0 && a >= f0 && a - f0 + l <= (1u << 20) && (uint64_t)a + l <= 0xFFFFFFFFull;
-          nrec += (l + 254) / 255;
-          mn = a < mn ? a : mn;
-          mx = a + l > mx ? a + l : mx;
-        }
-        ok = ae;
-      }
-      const uint32_t rin = wincl(ae ? nrec : 0u, lane), rt = rdlane(rin, 63);
-      if (NBk + NR + rt > LN_AW) {
-        bad = 5;
-        return;
-      }
-      if (ae) {
-        uint32_t sl = NR + rin - nrec;
-        for (uint32_t t = 0; t < nr; t++) {
-          const uint32_t a = L.dsv[g + 2 + 2 * t], l = L.dsv[g + 3 + 2 * t];
-          for (uint32_t q = 0; 255 * q < l; q++) {
-            const uint32_t ln = l - 255 * q < 255 ? l - 255 * q : 255;
-            L.buf[LN_BUF - 1 - sl++] = (a - f0 + 255 * q) | (ln << 20) | ((uint32_t)bq << 28);
-          }
-        }
-        atomicMin(&L.dsmin[bq], mn);
-        atomicMax(&L.dsmax[bq], mx);
-        g += 2 + 2 * nr;
-      }
-      NR += rt;
-    }
-    ok = ok && (!it || g == gend); // no varints after the DeleteSet (trailing bytes: not lean)
-    if (__ballot(it && !ok)) {
-      bad = 3;
-      return;
-    }
-    if (it) {
-      uint32_t p0 = 0, p1 = 1, p2 = 2, p3 = 3;
-      if (nent >= 2) ds_pos4(nent, c0, c1, c2, c3, p0, p1, p2, p3);
-      atomicMin(&L.dsfirst[b0k], (iu << 8) | p0);
-      if (nent > 1) atomicMin(&L.dsfirst[b1k], (iu << 8) | p1);
-      if (nent > 2) atomicMin(&L.dsfirst[b2k], (iu << 8) | p2);
-      if (nent > 3) atomicMin(&L.dsfirst[b3k], (iu << 8) | p3);
-    }
-    wsync();
-    dsn = 0;
-    dsused = 0;
-    acc(13, tp0);
-  };
   uint4 v0, v1;
   stage_load(b.bytes, al, n16, lane, v0, v1);
   stamp(1);
@@ -676,7 +544,7 @@ template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB, 4) k
     }
     const uint64_t mall = __ballot(hb);
     const uint32_t nbr = (uint32_t)__builtin_popcountll(mall);
-    if (NBk + nbr + NR > LN_AW) { // arena full: not lean
+    if (NBk + nbr + NI > LN_AW) { // arena full: not lean
       bad = 5;
       break;
     }
@@ -721,7 +589,8 @@ template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB, 4) k
     }
     acc(10, tr2);
     const uint64_t tr3 = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
-    // DeleteSets: copied byte-packed into the item buffer, decoded by ds_pass
+    // DeleteSets: item bytes verbatim to the HBM scratch (input order), end offsets to the
+    // arena top; decoded in a few large batches by phase 4
     {
       const bool hd = act && r.nent > 0;
       const uint32_t ilen = hd ? (uint32_t)(e - al) - r.dspos : 0;
@@ -729,21 +598,20 @@ template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB, 4) k
       if (hm) {
         const uint32_t binc = wincl(ilen, lane), btot = rdlane(binc, 63);
         const uint32_t nit = (uint32_t)__builtin_popcountll(hm);
-        if (__ballot(ilen > LN_DSMAXI) || btot > LN_DSB) {
+        if (__ballot(ilen > LN_DSMAXI)) {
           bad = 3;
           break;
         }
-        if (dsn + nit > LN_DSI || dsused + btot > LN_DSB) {
-          ds_pass();
-          if (bad) break;
+        if (NBk + NI + nit > LN_AW) {
+          bad = 5;
+          break;
         }
         if (hd) {
-          const uint32_t idx = dsn + lanes_below(hm), off = dsused + binc - ilen;
-          copy_lds(L.buf, r.dspos, L.dsb, off, ilen);
-          L.dsi[idx] = off | (ilen << 9) | (i << 17);
+          copy_out(L.buf, r.dspos, dscr + DSB + binc - ilen, ilen);
+          L.buf[LN_BUF - 1 - (NI + lanes_below(hm))] = DSB + binc;
         }
-        dsn += nit;
-        dsused += btot;
+        NI += nit;
+        DSB += btot;
       }
     }
     acc(11, tr3);
@@ -764,7 +632,6 @@ template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB, 4) k
     v1 = w1;
     wsync();
   }
-  if (!bad && dsn) ds_pass();
   if (bad) {
     reject(bad - 1);
     return;
@@ -775,10 +642,6 @@ template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB, 4) k
   // ---------------------------------------------------------------- 2 layout
   const bool lb = lane < nbk;
   const uint32_t cnt = lb ? bcnt : 0, cl = lb ? tabc : 0, fst = lb ? bfirst : 0, byt = lb ? L.bytes[lane] : 0;
-  if (lb) {
-    L.client[lane] = cl;
-    L.first[lane] = fst;
-  }
   const bool hasb = cnt > 0;
   const uint64_t hbm = __ballot(hasb);
   const uint32_t NC = (uint32_t)__builtin_popcountll(hbm);
@@ -795,14 +658,17 @@ template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB, 4) k
     blocks_size += sq;
     if (((hbm >> q) & 1) && rq < rank) sst += sq;
   }
-  // DeleteSet windows: bitmap words per client, checked before anything is written
-  const uint32_t dsf = lb ? L.dsfirst[lane] : LN_NONE;
-  const bool hasd = dsf != LN_NONE;
-  const uint32_t dmn = hasd ? L.dsmin[lane] : 0, dmx = hasd ? L.dsmax[lane] : 0;
-  const uint32_t words = hasd ? ((dmx - 1) >> 5) - (dmn >> 5) + 1 : 0;
+  // DeleteSet bitmap: one window per client with blocks, [first clock & ~31, next clock) — a
+  // lean DeleteSet deletes clocks of the document's own blocks (else: handed over)
+  const uint32_t bnx = hasb ? bnext : 0;
+  const uint32_t dbase = hasb ? fst & ~31u : 0;
+  const uint32_t words = hasb ? ((bnx - 1) >> 5) - (dbase >> 5) + 1 : 0;
   const uint32_t win = wincl(words, lane), W = rdlane(win, 63), woff = win - words;
-  const uint32_t D = (uint32_t)__builtin_popcountll(__ballot(hasd));
-  if (W + 2 * NR + LN_ORD > LN_BUF) { // bitmap, component starts / ends, order scratch
+  const uint32_t Wr = (W + 3) & ~3u; // staging after the bitmap, 16-byte aligned
+  // DS batches need the bitmap, a staging window and its decoded varints below the item ends
+  const uint32_t dsavail = LN_BUF - NI > Wr + LN_DSW / 4 + 8 ? LN_BUF - NI - (Wr + LN_DSW / 4 + 8) : 0;
+  const uint32_t dslim = dsavail < LN_DSW - 16 ? dsavail : LN_DSW - 16; // batch bytes (<= varints)
+  if (NI && dslim < LN_DSMAXI) {
     reject(6);
     return;
   }
@@ -811,12 +677,12 @@ template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB, 4) k
     Writer wr{out, 0};
     w_var(wr, NC);
   }
+  uint32_t curr = sst + hdr; // copy cursor of bucket `lane`
   if (hasb) {
     Writer wr{out, sst};
     w_var(wr, cnt);
     w_var(wr, cl);
     w_var(wr, fst);
-    L.cur[lane] = sst + hdr;
   }
   wsync();
 
@@ -861,9 +727,9 @@ template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB, 4) k
         const bool mine = act && bq == bb;
         rem &= ~__ballot(mine);
         const uint32_t inc = wincl(mine ? bl : 0u, lane), tot = rdlane(inc, 63);
-        const uint32_t base = L.cur[bb]; // (LDS operations of one wave complete in order)
+        const uint32_t base = rdlane(curr, bb);
         if (mine) off = base + inc - bl;
-        if (lane == 0) L.cur[bb] = base + tot;
+        if (lane == bb) curr = base + tot;
       }
       if (act) copy_out(L.buf, (uint32_t)(B0 + src - al1), out + off, bl);
       wsync();
@@ -873,30 +739,164 @@ template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB, 4) k
 
   stamp(4);
   // ---------------------------------------------------------------- 4 DeleteSet
-  // bitmap over each client's window [dbase, dmax) (stage + arena bottom; ranges stay at the
-  // arena top until they are scattered)
+  // IdSet::decode of every item (id_set.rs:412-426) in batches of whole items staged from the
+  // HBM scratch; ranges go straight into the bitmap (IdSet::merge + squash = union,
+  // id_set.rs:129-164, 385-395); first-occurrence keys give the union's client order.
   uint32_t *bmp = L.buf;
-  const uint32_t dbase = dmn & ~31u;
   for (uint32_t q = lane; q < W; q += 64) bmp[q] = 0;
-  if (hasd) {
-    L.cur[lane] = woff;   // cursors are free after the copy
-    L.eoff[lane] = dbase; // entry offsets are computed after the scatter
-  }
+  // the wave's scratch stores must be visible to its own loads below
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
   wsync();
-  for (uint32_t j = lane; j < NR; j += 64) {
-    const uint32_t lw = L.buf[LN_BUF - 1 - j];
-    const uint32_t bq = lw >> 28, ln = (lw >> 20) & 0xFF;
-    const uint32_t wo = L.cur[bq], bs = L.eoff[bq];
-    uint32_t a = L.first[bq] + (lw & 0xFFFFF) - bs;
-    const uint32_t z = a + ln;
-    while (a < z) {
-      const uint32_t wi = a >> 5, bo = a & 31, nb = (z - a < 32 - bo) ? z - a : 32 - bo;
-      const uint32_t mask = (nb == 32 ? 0xFFFFFFFFu : ((1u << nb) - 1)) << bo;
-      atomicOr(&bmp[wo + wi], mask);
-      a += nb;
+  uint32_t *stg = L.buf + Wr, *dsv = stg + LN_DSW / 4 + 8;
+  uint32_t NR = 0; // ranges (bound the components)
+  {
+    const uint64_t tp0 = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+    uint32_t i0 = 0, s0 = 0;
+    uint32_t dbad = 0; // why + 1
+    while (i0 < NI && !dbad) {
+      if (STAMPS) tst[14]++;
+      // items [i0, i1) with their bytes [s0, s1) <= dslim (item ends are ascending)
+      uint32_t i1 = i0;
+      for (;;) {
+        const uint32_t j = i1 + lane;
+        const uint64_t fm = __ballot(j < NI && L.buf[LN_BUF - 1 - j] - s0 <= dslim);
+        const uint32_t kf = lead_ones(fm);
+        i1 += kf;
+        if (kf < 64) break;
+      }
+      const uint32_t s1 = L.buf[LN_BUF - i1];
+      const uint64_t ga = (uint64_t)(uintptr_t)(dscr + s0), ga16 = ga & ~15ull;
+      const uint32_t so = (uint32_t)(ga - ga16), send = so + (s1 - s0);
+      {
+        uint4 d0 = make_uint4(0, 0, 0, 0), d1 = d0;
+        const uint32_t n16 = (send + 15) >> 4;
+        stage_load((const uint8_t *)(uintptr_t)ga16, 0, n16, lane, d0, d1);
+        stage_store(stg, n16, lane, d0, d1);
+      }
+      wsync();
+      // 1 terminators (bit 7 clear) of bytes [16 lane, 16 lane + 16) within [so, send); a
+      // varint starts at so and after every terminator; its index = terminators before it
+      const uint32_t b0 = 16 * lane;
+      const uint32_t lo = so > b0 ? so - b0 : 0, hi = send > b0 ? send - b0 : 0;
+      const uint32_t vmask = (hi >= 16 ? 0xFFFFu : (1u << hi) - 1) & ~(lo >= 16 ? 0xFFFFu : (1u << lo) - 1);
+      uint32_t tm = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++) {
+        const uint32_t t = ~stg[4 * lane + q] & 0x80808080u;
+        tm |= (((t >> 7) & 1) | ((t >> 14) & 2) | ((t >> 21) & 4) | ((t >> 28) & 8)) << (4 * q);
+      }
+      tm &= vmask;
+      const uint32_t ns = (uint32_t)__builtin_popcount(tm);
+      const uint32_t ginc = wincl(ns, lane), gbase = ginc - ns;
+      const uint32_t tprev = shfl(tm, lane ? (int)lane - 1 : 0);
+      uint32_t sm = ((tm << 1) | (lane == 0 ? 1u << so : (tprev >> 15) & 1)) & vmask; // lane 0: the batch's first byte
+      bool vok = true;
+      while (sm) {
+        const uint32_t kb = (uint32_t)__builtin_ctz(sm);
+        const VarR r = var_at(stg, b0 + kb, send);
+        vok = vok && r.fine;
+        dsv[gbase + (uint32_t)__builtin_popcount(tm & ((1u << kb) - 1))] = r.v;
+        sm &= sm - 1;
+      }
+      if (__ballot(!vok)) {
+        dbad = 4;
+        break;
+      }
+      wsync();
+      // 2 one lane per item, groups of 64; entries in lockstep (uniform loop)
+      for (uint32_t g0i = i0; g0i < i1 && !dbad; g0i += 64) {
+        const uint32_t it = g0i + lane;
+        const bool iv = it < i1;
+        const uint32_t ist = iv ? (it ? L.buf[LN_BUF - it] : 0) - s0 + so : so;
+        const uint32_t ien = iv ? L.buf[LN_BUF - 1 - it] - s0 + so : so + 1;
+        const uint32_t ja = ist >> 4, jz = (ien - 1) >> 4;
+        const uint32_t gba = shfl(gbase, (int)(ja & 63)), tma = shfl(tm, (int)(ja & 63));
+        const uint32_t gbz = shfl(gbase, (int)(jz & 63)), tmz = shfl(tm, (int)(jz & 63));
+        const uint32_t g0 = gba + (uint32_t)__builtin_popcount(tma & ((1u << (ist & 15)) - 1));
+        const uint32_t zb = (ien - 1) & 15;
+        const uint32_t gend = gbz + (uint32_t)__builtin_popcount(tmz & ((2u << zb) - 1));
+        bool ok = !iv || ((tmz >> zb) & 1); // the item's last byte ends a varint
+        const uint32_t nds = iv ? dsv[g0] : 0;
+        ok = ok && (!iv || (nds >= 1 && nds <= 4 && g0 < gend));
+        const uint32_t nent = iv && ok ? nds : 0;
+        uint32_t g = g0 + 1, nrec = 0;
+        uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+        int b0k = 0, b1k = 0, b2k = 0, b3k = 0;
+#pragma unroll
+        for (uint32_t e = 0; e < 4; e++) {
+          bool ae = ok && e < nent;
+          if (!__ballot(ae)) break;
+          uint32_t cv = 0, nr = 0;
+          if (ae) {
+            ae = g + 2 <= gend;
+            if (ae) {
+              cv = dsv[g];
+              nr = dsv[g + 1];
+              ae = nr >= 1 && nr <= ien - ist && g + 2 + 2 * nr <= gend && !(e > 0 && c0 == cv) &&
+                   !(e > 1 && c1 == cv) && !(e > 2 && c2 == cv);
+            }
+          }
+          // the entry's client must own blocks here (its window): else not lean
+          const int bq = ae ? tab_find(tabc, nbk, cv) : 0;
+          ae = ae && bq >= 0 && ((blkmask >> (bq & 31)) & 1);
+          const uint32_t bqq = (uint32_t)(bq < 0 ? 0 : bq) & 63;
+          const uint32_t f0 = shfl(fst, (int)bqq), bn = shfl(bnx, (int)bqq);
+          const uint32_t wo = shfl(woff, (int)bqq), bs = shfl(dbase, (int)bqq);
+          if (e == 0) { c0 = cv; b0k = bq; }
+          else if (e == 1) { c1 = cv; b1k = bq; }
+          else if (e == 2) { c2 = cv; b2k = bq; }
+          else { c3 = cv; b3k = bq; }
+          if (ae) {
+            for (uint32_t t = 0; t < nr && ae; t++) {
+              const uint32_t a = dsv[g + 2 + 2 * t], l = dsv[g + 3 + 2 * t];
+              ae = l != 0 && a >= f0 && (uint64_t)a + l <= bn;
+              if (!ae) break;
+              uint32_t x = a - bs;
+              const uint32_t z = x + l;
+              while (x < z) {
+                const uint32_t wi = x >> 5, bo = x & 31, nb = (z - x < 32 - bo) ? z - x : 32 - bo;
+                const uint32_t mask = (nb == 32 ? 0xFFFFFFFFu : ((1u << nb) - 1)) << bo;
+                atomicOr(&bmp[wo + wi], mask);
+                x += nb;
+              }
+            }
+            nrec += nr;
+            g += 2 + 2 * nr;
+          }
+          if (e < nent) ok = ae;
+        }
+        ok = ok && (!iv || g == gend); // no varints after the DeleteSet (trailing bytes: not lean)
+        if (__ballot(iv && !ok)) {
+          dbad = 7; // window (a range outside its client's blocks) or malformed: hand over
+          break;
+        }
+        if (iv) {
+          uint32_t p0 = 0, p1 = 1, p2 = 2, p3 = 3;
+          if (nent >= 2) ds_pos4(nent, c0, c1, c2, c3, p0, p1, p2, p3);
+          atomicMin(&L.dsfirst[b0k], (it << 8) | p0);
+          if (nent > 1) atomicMin(&L.dsfirst[b1k], (it << 8) | p1);
+          if (nent > 2) atomicMin(&L.dsfirst[b2k], (it << 8) | p2);
+          if (nent > 3) atomicMin(&L.dsfirst[b3k], (it << 8) | p3);
+        }
+        NR += rdlane(wincl(nrec, lane), 63);
+      }
+      wsync();
+      i0 = i1;
+      s0 = s1;
+    }
+    acc(13, tp0);
+    if (dbad) {
+      reject(dbad - 1);
+      return;
     }
   }
-  wsync();
+  const uint32_t dsf = lb ? L.dsfirst[lane] : LN_NONE;
+  const bool hasd = dsf != LN_NONE;
+  const uint32_t D = (uint32_t)__builtin_popcountll(__ballot(hasd));
+  if (W + 2 * NR + LN_ORD > LN_BUF) { // bitmap, component starts / ends, order scratch
+    reject(6);
+    return;
+  }
   // runs -> components: cst[c] / cen[c] per bucket in bucket-index order
   uint32_t *cst = L.buf + W, *cen = L.buf + W + NR;
   uint32_t ncomp = 0, cbase = 0, NCD = 0;
@@ -950,7 +950,12 @@ template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB, 4) k
     if (lane == q) dsb = acc;
   }
   // client order and entry offsets (one lane, D <= 16)
+  // scratch at the end of buf (free once the ranges are scattered): order [16], hash slots
+  // [64], clients [16], entry offsets [16]
+  uint32_t *ord = L.buf + LN_BUF - LN_ORD, *slots = ord + LN_NBK, *clients = slots + 4 * LN_NBK,
+           *eoff = clients + LN_NBK;
   const uint32_t ds_start = blocks_size;
+  if (lb) clients[lane] = cl;
   if (hasd) {
     L.dsfirst[lane] = dsf;
     L.bytes[lane] = varlen(cl) + varlen(ncomp) + dsb; // entry size (bytes[] is free after the copy)
@@ -958,11 +963,11 @@ template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB, 4) k
   wsync();
   uint32_t total = 0;
   if (lane == 0) {
-    lean_ds_order(nbk, L.client, L.dsfirst, L.buf + LN_BUF - LN_ORD, L.buf + LN_BUF - 4 * LN_NBK);
+    lean_ds_order(nbk, clients, L.dsfirst, ord, slots);
     uint32_t pos = ds_start + varlen(D);
     for (uint32_t i2 = 0; i2 < D; i2++) {
-      const uint32_t bq = L.buf[LN_BUF - LN_ORD + i2];
-      L.eoff[bq] = pos;
+      const uint32_t bq = ord[i2];
+      eoff[bq] = pos;
       pos += L.bytes[bq];
     }
     total = pos;
@@ -971,15 +976,16 @@ template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB, 4) k
   }
   total = rdlane(total, 0);
   wsync();
+  const uint32_t myeo = hasd ? eoff[lane] : 0;
   if (hasd) {
-    Writer wr{out, L.eoff[lane]};
+    Writer wr{out, myeo};
     w_var(wr, cl);
     w_var(wr, ncomp);
   }
   for (uint32_t q = 0; q < nbk; q++) {
     const uint32_t nq = rdlane(ncomp, q), cq = rdlane(cbase, q);
     if (!nq) continue;
-    const uint32_t eo = L.eoff[q] + varlen(rdlane(cl, q)) + varlen(nq);
+    const uint32_t eo = rdlane(myeo, q) + varlen(rdlane(cl, q)) + varlen(nq);
     uint32_t acc = 0;
     for (uint32_t c0 = 0; c0 < nq; c0 += 64) {
       const uint32_t c = cq + c0 + lane;
@@ -1011,10 +1017,19 @@ template <int WPB, bool STAMPS> __global__ void __launch_bounds__(64 * WPB, 4) k
 void launch_lean(const BatchIn &b, const FastOut &o, hipStream_t s) {
   if (!b.n_docs) return;
   constexpr int WPB = 1;
-  if (o.stamps)
-    hipLaunchKernelGGL((k_lean<WPB, true>), dim3((b.n_docs + WPB - 1) / WPB), dim3(64 * WPB), 0, s, b, o);
-  else
-    hipLaunchKernelGGL((k_lean<WPB, false>), dim3((b.n_docs + WPB - 1) / WPB), dim3(64 * WPB), 0, s, b, o);
+  // waves per SIMD the register budget is compiled for (LDS allows 6 at 6.8 KB per wave);
+  // env YMERGE_LEAN_OCC=4/6 selects the 4- / 6-wave build (A/B)
+  static const int occ = getenv("YMERGE_LEAN_OCC") ? atoi(getenv("YMERGE_LEAN_OCC")) : 5;
+  const dim3 g((b.n_docs + WPB - 1) / WPB), t(64 * WPB);
+  if (o.stamps) {
+    if (occ == 4) hipLaunchKernelGGL((k_lean<WPB, 4, true>), g, t, 0, s, b, o);
+    else if (occ == 6) hipLaunchKernelGGL((k_lean<WPB, 6, true>), g, t, 0, s, b, o);
+    else hipLaunchKernelGGL((k_lean<WPB, 5, true>), g, t, 0, s, b, o);
+  } else {
+    if (occ == 4) hipLaunchKernelGGL((k_lean<WPB, 4, false>), g, t, 0, s, b, o);
+    else if (occ == 6) hipLaunchKernelGGL((k_lean<WPB, 6, false>), g, t, 0, s, b, o);
+    else hipLaunchKernelGGL((k_lean<WPB, 5, false>), g, t, 0, s, b, o);
+  }
 }
 
 } // namespace ym
