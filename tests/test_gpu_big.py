@@ -13,8 +13,10 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module")
 def engine():
-    import ymerge
-    e = ymerge.Engine(0)
+    # k_lean off: every document here reaches the tiled kernel (or the exact engine) as it
+    # would for shapes k_lean hands over (tests/test_gpu_lean.py covers k_lean's BIG mode)
+    from test_gpu_parity import engine_with
+    e = engine_with(YMERGE_LEAN=0)
     yield e
     e.close()
 
@@ -28,8 +30,7 @@ def test_c3_zipf_tail_on_tiled_kernel(engine, oracle):
     st = engine.stats()
     assert st["docs_exact"] == 0, st
     assert st["docs_big"] >= big, st
-    # documents of <= 4 updates: k_lean (wave per document) or, without it, lane per document
-    assert st["docs_tiny"] + st["docs_lean"] > 0, st
+    assert st["docs_tiny"] > 0, st  # documents of <= 4 updates: lane per document
 
 
 def test_tiny_docs_on_fast_path(oracle):

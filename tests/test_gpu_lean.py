@@ -191,3 +191,40 @@ def test_lean_matches_fast_path(oracle):
         finally:
             e1.close()
         assert o0.tobytes() == o1.tobytes() and np.array_equal(f0, f1) and np.array_equal(s0, s1)
+
+
+def test_lean_big_documents(engine, oracle):
+    """k_lean's BIG mode (documents above the LDS arena: > 1280 updates or >= 64 KB; tables
+    in HBM scratch): multi-client editing logs of 1,281 - 12,000 updates, ~100 B updates
+    past 64 KB, DeleteSet-heavy logs; all written by k_lean, byte-exact."""
+    rng = np.random.default_rng(0xB1C)
+    docs = []
+    for n in (1281, 2000, 5000, 12000):
+        cl = [int(x) for x in rng.integers(0, 2 ** 32, int(rng.integers(1, 6)))]
+        docs.append(text_log(rng, cl, n))
+    docs.append(text_log(rng, [7], 3000, del_frac=0.6))
+    ups, clock = [], 0
+    for i in range(700):  # ~100 B per update: ~70 KB with 700 updates
+        t = "".join(chr(97 + int(x)) for x in rng.integers(0, 26, 90))
+        ups.append(upd(1, clock, item(t, origin=(1, clock - 1) if clock else None)))
+        clock += len(t)
+    docs.append(ups)
+    ups = [upd(1, 0, item("x" * 500))]
+    for i in range(400):  # 400 updates x 2 ranges
+        ups.append(upd(ds=[(1, [(i, 1), (i + 100, 1)])]))
+    docs.append(ups)
+    docs.append([upd(3, 0, item("a" * 600)), upd(3, 600, item("b" * 300))] +
+                [upd(ds=[(3, [(2 * (i % 450), 1)])]) for i in range(1500)])  # 450 components
+    st = run(engine, oracle, docs)
+    assert st["docs_lean"] == len(docs), st
+
+
+def test_lean_c3_zipf(engine, oracle):
+    """C3-shaped batch (Zipf update counts up to 10^4): every document lean, byte-exact."""
+    import workloads
+    b = workloads.zipf_docs(4000, seed=0x5EED)
+    assert int((np.diff(b.doc_upd) > 1280).sum()) > 10
+    check_batch(engine, oracle, b)
+    st = engine.stats()
+    assert st["docs_lean"] == b.n_docs and st["docs_exact"] == 0 and st["docs_big"] == 0, st
+

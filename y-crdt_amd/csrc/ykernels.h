@@ -51,8 +51,13 @@ struct FastOut {
 };
 size_t fast_lds_bytes(const FastCaps &c);
 // one wavefront per document for the common editor shape (ymerge_lean.hip): writes the
-// document (path 0) or hands it to k_decode + k_fast_merge (path 3, counted in npath[6])
-void launch_lean(const BatchIn &b, const FastOut &o, hipStream_t s);
+// document (path 0) or hands it to k_decode + k_fast_merge (path 3, counted in npath[6]).
+// scr: HBM scratch of lean_scratch_words(...) u32 for documents above the LDS arena (null:
+// those are handed over)
+void launch_lean(const BatchIn &b, const FastOut &o, uint32_t *scr, hipStream_t s);
+inline uint64_t lean_scratch_words(uint64_t n_updates, uint64_t n_docs, uint64_t n_bytes) {
+  return 4 * n_updates + 64 * n_docs + n_bytes;
+}
 void launch_fast_merge(const BatchIn &b, const FastCaps &caps, const FastOut &o, int nt, hipStream_t s);
 
 // documents over the fast path's LDS capacities (path == 2): tiled, HBM scratch

@@ -54,7 +54,7 @@ struct ymerge_ctx {
   hipStream_t s = nullptr;
   DevBuf in_bytes, in_upd_off, in_doc_upd, in_sv, in_sv_off, sync_off, sync_end, sync_st;
   DevBuf status, path, out_start, out_len, pack_off, counts, need, scr_off, scratch, sizes, spill_off, scan_tmp;
-  DevBuf arena, packed, counter, stamps, plan_small, plan_big, rec, ovf, big_scratch;
+  DevBuf arena, packed, counter, stamps, plan_small, plan_big, rec, ovf, big_scratch, lean_scr;
   // lib0 v2: v1x arena + offsets + per-update status, v2 output arena + sizes + offsets,
   // state-vector rest offsets + pre-status
   DevBuf v2x, v2x_sz, v2x_off, v2_ust, v2_out, v2_osz, v2_ooff, v2_svoff, v2_svend, v2_pre;
@@ -112,7 +112,7 @@ extern "C" void ymerge_ctx_destroy(ymerge_ctx *c) {
                     &c->sync_end, &c->sync_st, &c->rec, &c->ovf, &c->status, &c->path,
                     &c->out_start, &c->out_len, &c->pack_off, &c->counts, &c->need, &c->scr_off, &c->scratch,
                     &c->sizes, &c->spill_off, &c->scan_tmp, &c->arena, &c->packed, &c->counter, &c->stamps,
-                    &c->plan_small, &c->plan_big, &c->big_scratch, &c->v2x, &c->v2x_sz, &c->v2x_off, &c->v2_ust,
+                    &c->plan_small, &c->plan_big, &c->big_scratch, &c->lean_scr, &c->v2x, &c->v2x_sz, &c->v2x_off, &c->v2_ust,
                     &c->v2_out, &c->v2_osz, &c->v2_ooff, &c->v2_svoff, &c->v2_svend, &c->v2_pre})
     b->release();
   if (c->h_pinned) hipHostFree(c->h_pinned);
@@ -184,7 +184,10 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   uint32_t n_rej = n;
   hipEventRecord(c->ev[7], c->s);
   if (lean) {
-    ym::launch_lean(b, fo, c->s);
+    // BIG k_lean documents keep their size-proportional tables in HBM (untouched otherwise)
+    const uint64_t lw = ym::lean_scratch_words(n_updates, n_docs, n_bytes);
+    uint32_t *lscr = c->lean_scr.ensure(lw * 4 + 64) ? c->lean_scr.as<uint32_t>() : nullptr;
+    ym::launch_lean(b, fo, lscr, c->s);
     if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
     hipMemcpyAsync(c->h_pinned + 16, c->counter.as<uint32_t>() + 10, 4, hipMemcpyDeviceToHost, c->s);
     if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;

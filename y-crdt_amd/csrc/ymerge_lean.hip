@@ -47,6 +47,7 @@ constexpr uint32_t LN_DSW = 1024;            // DeleteSet batch window: 16 stage
 constexpr uint32_t LN_ORD = 7 * LN_NBK;      // DeleteSet client order scratch (end of buf, after the scatter):
                                              // order, hash slots (2x) + copy, clients, entry offsets
 constexpr uint32_t LN_NONE = 0xFFFFFFFFu;
+constexpr uint32_t LN_UMAX = 32768;          // BIG documents: above, the tiled kernel is faster per document
 
 // buf = [stage | arena]: block records (src | blen << 16 | bucket << 27) from the arena
 // bottom; from the top, one word per DeleteSet item: its end offset in the document's DS
@@ -416,15 +417,14 @@ __device__ __noinline__ uint32_t lean_ds_order(uint32_t nbk, const uint32_t *cli
 // Diagnostic build only (STAMPS, env YMERGE_STAMPS): lane 0 records s_memtime at phase
 // boundaries into o.stamps[doc * 16 + k] (k 0..6), per-round sub-phase cycle sums (8..11),
 // rounds (12), marker 0x1EA4 (15); never part of a timed run.
-template <int WPB, int OCC, bool STAMPS>
-__global__ void __launch_bounds__(64 * WPB, OCC) k_lean(BatchIn b, FastOut o) {
-  __shared__ LeanLds lds[WPB];
-  ym_set_grammar(b.v1x);
-  const uint32_t lane = __lane_id();
-  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t d = blockIdx.x * WPB + w;
-  if (d >= b.n_docs) return;
-  LeanLds &L = lds[w];
+// BIG (documents above the LDS arena: > LN_AW updates or >= 64 KB): the same algorithm
+// with the size-proportional tables in the document's HBM scratch `scr` (word offset
+// 4 * u0 + 64 * d + B0, capacity 4 U + 64 + bytes words): block records (2 words) at
+// [0, 2U), DeleteSet item ends at [2U, 3U), the DeleteSet bitmap from 3U, component starts /
+// ends after it.  LDS then holds only the stage and the DeleteSet batch.
+template <bool BIG, bool STAMPS>
+__device__ __forceinline__ void lean_doc(const BatchIn &b, const FastOut &o, LeanLds &L, const uint32_t d,
+                                         const uint32_t lane, uint32_t *const scr) {
   uint64_t tst[16];
   auto stamp = [&](int k) {
     if (STAMPS) tst[k] = __builtin_amdgcn_s_memtime();
@@ -449,10 +449,14 @@ __global__ void __launch_bounds__(64 * WPB, OCC) k_lean(BatchIn b, FastOut o) {
       atomicAdd(&o.npath[7 + (why < 7 ? why : 0)], 1u);
     }
   };
-  if (U == 0 || B1 - B0 >= 65536 || U >= 16384) {
+  if (U == 0 || (!BIG && (B1 - B0 >= 65536 || U > LN_AW))) {
     reject(0);
     return;
   }
+  // this document's HBM scratch (every document has one when scr is set; BIG documents
+  // keep all their tables there, the others only component lists that outgrow LDS)
+  uint32_t *const hs = scr ? scr + 4 * u0 + 64ull * d + B0 : nullptr;
+  auto item_end = [&](uint32_t j) -> uint32_t { return BIG ? hs[2 * U + j] : L.buf[LN_BUF - 1 - j]; };
   if (lane < LN_NBK) {
     L.bytes[lane] = 0;
     L.dsfirst[lane] = LN_NONE;
@@ -544,7 +548,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC) k_lean(BatchIn b, FastOut o) {
     }
     const uint64_t mall = __ballot(hb);
     const uint32_t nbr = (uint32_t)__builtin_popcountll(mall);
-    if (NBk + nbr + NI > LN_AW) { // arena full: not lean
+    if (!BIG && NBk + nbr + NI > LN_AW) { // arena full: not lean
       bad = 5;
       break;
     }
@@ -582,8 +586,13 @@ __global__ void __launch_bounds__(64 * WPB, OCC) k_lean(BatchIn b, FastOut o) {
       }
       if (hb) {
         atomicAdd(&L.bytes[bk], r.blen);
-        const uint32_t src = (uint32_t)(al + r.bpos - B0);
-        L.buf[LN_SW + NBk + lanes_below(mall)] = src | (r.blen << 16) | ((uint32_t)bk << 27);
+        const uint32_t src = (uint32_t)(al + r.bpos - B0), ri = NBk + lanes_below(mall);
+        if (BIG) {
+          hs[2 * ri] = src;
+          hs[2 * ri + 1] = r.blen | ((uint32_t)bk << 27);
+        } else {
+          L.buf[LN_SW + ri] = src | (r.blen << 16) | ((uint32_t)bk << 27);
+        }
       }
       NBk += nbr;
     }
@@ -602,13 +611,15 @@ __global__ void __launch_bounds__(64 * WPB, OCC) k_lean(BatchIn b, FastOut o) {
           bad = 3;
           break;
         }
-        if (NBk + NI + nit > LN_AW) {
+        if (!BIG && NBk + NI + nit > LN_AW) {
           bad = 5;
           break;
         }
         if (hd) {
           copy_out(L.buf, r.dspos, dscr + DSB + binc - ilen, ilen);
-          L.buf[LN_BUF - 1 - (NI + lanes_below(hm))] = DSB + binc;
+          const uint32_t ii = NI + lanes_below(hm);
+          if (BIG) hs[2 * U + ii] = DSB + binc;
+          else L.buf[LN_BUF - 1 - ii] = DSB + binc;
         }
         NI += nit;
         DSB += btot;
@@ -665,10 +676,15 @@ __global__ void __launch_bounds__(64 * WPB, OCC) k_lean(BatchIn b, FastOut o) {
   const uint32_t words = hasb ? ((bnx - 1) >> 5) - (dbase >> 5) + 1 : 0;
   const uint32_t win = wincl(words, lane), W = rdlane(win, 63), woff = win - words;
   const uint32_t Wr = (W + 3) & ~3u; // staging after the bitmap, 16-byte aligned
-  // DS batches need the bitmap, a staging window and its decoded varints below the item ends
-  const uint32_t dsavail = LN_BUF - NI > Wr + LN_DSW / 4 + 8 ? LN_BUF - NI - (Wr + LN_DSW / 4 + 8) : 0;
+  // DS batches need the bitmap, a staging window and its decoded varints below the item ends.
+  // The bitmap goes to the HBM scratch ([3U, 3U + Wr), then the component lists: 2 NR <= DSB
+  // words, within the scratch's last U + 64 + bytes words) for BIG documents and whenever
+  // it would leave no room for one batch of the largest item.
+  const bool bmg = BIG || Wr + LN_DSW / 4 + 8 + LN_DSMAXI + NI > LN_BUF;
+  const uint32_t lds_used = (BIG ? 0 : NI) + (bmg ? 0 : Wr);
+  const uint32_t dsavail = LN_BUF - lds_used > LN_DSW / 4 + 8 ? LN_BUF - lds_used - (LN_DSW / 4 + 8) : 0;
   const uint32_t dslim = dsavail < LN_DSW - 16 ? dsavail : LN_DSW - 16; // batch bytes (<= varints)
-  if (NI && dslim < LN_DSMAXI) {
+  if ((NI && dslim < LN_DSMAXI) || (bmg && (!hs || (uint64_t)Wr + DSB > U + 64 + (B1 - B0)))) {
     reject(6);
     return;
   }
@@ -691,13 +707,20 @@ __global__ void __launch_bounds__(64 * WPB, OCC) k_lean(BatchIn b, FastOut o) {
   {
     uint32_t r0 = 0;
     uint4 c0 = make_uint4(0, 0, 0, 0), c1 = c0;
-    uint32_t rec = 0, kk = 0, cn16 = 0;
+    uint32_t rsrc = 0, rmeta = 0, kk = 0, cn16 = 0; // record: source offset, blen | bucket << 27
     uint64_t cal = 0;
     auto plan = [&](uint32_t base) {
       const uint32_t j = base + lane;
       const bool v = j < NBk;
-      rec = v ? L.buf[LN_SW + j] : 0;
-      const uint32_t src = rec & 0xFFFF, bl = (rec >> 16) & 0x7FF;
+      if (BIG) {
+        rsrc = v ? hs[2 * j] : 0;
+        rmeta = v ? hs[2 * j + 1] : 0;
+      } else {
+        const uint32_t rec = v ? L.buf[LN_SW + j] : 0;
+        rsrc = rec & 0xFFFF;
+        rmeta = ((rec >> 16) & 0x7FF) | (rec & 0x78000000u);
+      }
+      const uint32_t src = rsrc, bl = rmeta & 0x7FF;
       cal = (B0 + rdlane(src, 0)) & ~15ull;
       const uint64_t ae = B0 + src + bl;
       kk = lead_ones(__ballot(v && ae - cal <= LN_STAGE));
@@ -709,7 +732,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC) k_lean(BatchIn b, FastOut o) {
       stage_load(b.bytes, cal, cn16, lane, c0, c1);
     }
     while (r0 < NBk) {
-      const uint32_t myrec = rec, k1 = kk, n1 = cn16;
+      const uint32_t mysrc = rsrc, mymeta = rmeta, k1 = kk, n1 = cn16;
       const uint64_t al1 = cal;
       stage_store(L.buf, n1, lane, c0, c1);
       const uint32_t r1 = r0 + k1;
@@ -719,7 +742,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC) k_lean(BatchIn b, FastOut o) {
       }
       wsync();
       const bool act = lane < k1;
-      const uint32_t src = myrec & 0xFFFF, bl = (myrec >> 16) & 0x7FF, bq = (myrec >> 27) & 15;
+      const uint32_t src = mysrc, bl = mymeta & 0x7FF, bq = (mymeta >> 27) & 15;
       uint32_t off = 0;
       uint64_t rem = __ballot(act);
       while (rem) {
@@ -742,12 +765,12 @@ __global__ void __launch_bounds__(64 * WPB, OCC) k_lean(BatchIn b, FastOut o) {
   // IdSet::decode of every item (id_set.rs:412-426) in batches of whole items staged from the
   // HBM scratch; ranges go straight into the bitmap (IdSet::merge + squash = union,
   // id_set.rs:129-164, 385-395); first-occurrence keys give the union's client order.
-  uint32_t *bmp = L.buf;
+  uint32_t *const bmp = bmg ? hs + 3 * U : L.buf;
   for (uint32_t q = lane; q < W; q += 64) bmp[q] = 0;
   // the wave's scratch stores must be visible to its own loads below
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
   wsync();
-  uint32_t *stg = L.buf + Wr, *dsv = stg + LN_DSW / 4 + 8;
+  uint32_t *const stg = bmg ? L.buf : L.buf + Wr, *const dsv = stg + LN_DSW / 4 + 8;
   uint32_t NR = 0; // ranges (bound the components)
   {
     const uint64_t tp0 = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
@@ -759,12 +782,12 @@ __global__ void __launch_bounds__(64 * WPB, OCC) k_lean(BatchIn b, FastOut o) {
       uint32_t i1 = i0;
       for (;;) {
         const uint32_t j = i1 + lane;
-        const uint64_t fm = __ballot(j < NI && L.buf[LN_BUF - 1 - j] - s0 <= dslim);
+        const uint64_t fm = __ballot(j < NI && item_end(j) - s0 <= dslim);
         const uint32_t kf = lead_ones(fm);
         i1 += kf;
         if (kf < 64) break;
       }
-      const uint32_t s1 = L.buf[LN_BUF - i1];
+      const uint32_t s1 = item_end(i1 - 1);
       const uint64_t ga = (uint64_t)(uintptr_t)(dscr + s0), ga16 = ga & ~15ull;
       const uint32_t so = (uint32_t)(ga - ga16), send = so + (s1 - s0);
       {
@@ -807,8 +830,8 @@ __global__ void __launch_bounds__(64 * WPB, OCC) k_lean(BatchIn b, FastOut o) {
       for (uint32_t g0i = i0; g0i < i1 && !dbad; g0i += 64) {
         const uint32_t it = g0i + lane;
         const bool iv = it < i1;
-        const uint32_t ist = iv ? (it ? L.buf[LN_BUF - it] : 0) - s0 + so : so;
-        const uint32_t ien = iv ? L.buf[LN_BUF - 1 - it] - s0 + so : so + 1;
+        const uint32_t ist = iv ? (it ? item_end(it - 1) : 0) - s0 + so : so;
+        const uint32_t ien = iv ? item_end(it) - s0 + so : so + 1;
         const uint32_t ja = ist >> 4, jz = (ien - 1) >> 4;
         const uint32_t gba = shfl(gbase, (int)(ja & 63)), tma = shfl(tm, (int)(ja & 63));
         const uint32_t gbz = shfl(gbase, (int)(jz & 63)), tmz = shfl(tm, (int)(jz & 63));
@@ -893,12 +916,19 @@ __global__ void __launch_bounds__(64 * WPB, OCC) k_lean(BatchIn b, FastOut o) {
   const uint32_t dsf = lb ? L.dsfirst[lane] : LN_NONE;
   const bool hasd = dsf != LN_NONE;
   const uint32_t D = (uint32_t)__builtin_popcountll(__ballot(hasd));
-  if (W + 2 * NR + LN_ORD > LN_BUF) { // bitmap, component starts / ends, order scratch
+  // component starts / ends: LDS after the bitmap when they fit below the order scratch,
+  // else the scratch after the bitmap's region (2 NR <= DeleteSet bytes <= input)
+  const bool cg = bmg || W + 2 * NR + LN_ORD > LN_BUF;
+  if (cg && !hs) {
     reject(6);
     return;
   }
+  if (bmg) { // the bitmap's global atomics complete before the component scan reads it
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    wsync();
+  }
   // runs -> components: cst[c] / cen[c] per bucket in bucket-index order
-  uint32_t *cst = L.buf + W, *cen = L.buf + W + NR;
+  uint32_t *const cst = cg ? hs + 3 * U + (bmg ? Wr : 0) : L.buf + W, *const cen = cst + NR;
   uint32_t ncomp = 0, cbase = 0, NCD = 0;
   for (uint32_t q = 0; q < nbk; q++) {
     const uint32_t wc = rdlane(words, q);
@@ -1014,7 +1044,23 @@ __global__ void __launch_bounds__(64 * WPB, OCC) k_lean(BatchIn b, FastOut o) {
   }
 }
 
-void launch_lean(const BatchIn &b, const FastOut &o, hipStream_t s) {
+template <int WPB, int OCC, bool STAMPS>
+__global__ void __launch_bounds__(64 * WPB, OCC) k_lean(BatchIn b, FastOut o, uint32_t *scr) {
+  __shared__ LeanLds lds[WPB];
+  ym_set_grammar(b.v1x);
+  const uint32_t lane = __lane_id();
+  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t d = blockIdx.x * WPB + w;
+  if (d >= b.n_docs) return;
+  const uint64_t u0 = b.doc_upd[d], u1 = b.doc_upd[d + 1];
+  const uint64_t nb = b.upd_off[u1] - b.upd_off[u0];
+  if (scr && (u1 - u0 > LN_AW || nb >= 65536) && u1 - u0 <= LN_UMAX && nb < (1ull << 31))
+    lean_doc<true, STAMPS>(b, o, lds[w], d, lane, scr);
+  else
+    lean_doc<false, STAMPS>(b, o, lds[w], d, lane, scr);
+}
+
+void launch_lean(const BatchIn &b, const FastOut &o, uint32_t *scr, hipStream_t s) {
   if (!b.n_docs) return;
   constexpr int WPB = 1;
   // waves per SIMD the register budget is compiled for (LDS allows 6 at 6.8 KB per wave);
@@ -1022,13 +1068,13 @@ void launch_lean(const BatchIn &b, const FastOut &o, hipStream_t s) {
   static const int occ = getenv("YMERGE_LEAN_OCC") ? atoi(getenv("YMERGE_LEAN_OCC")) : 5;
   const dim3 g((b.n_docs + WPB - 1) / WPB), t(64 * WPB);
   if (o.stamps) {
-    if (occ == 4) hipLaunchKernelGGL((k_lean<WPB, 4, true>), g, t, 0, s, b, o);
-    else if (occ == 6) hipLaunchKernelGGL((k_lean<WPB, 6, true>), g, t, 0, s, b, o);
-    else hipLaunchKernelGGL((k_lean<WPB, 5, true>), g, t, 0, s, b, o);
+    if (occ == 4) hipLaunchKernelGGL((k_lean<WPB, 4, true>), g, t, 0, s, b, o, scr);
+    else if (occ == 6) hipLaunchKernelGGL((k_lean<WPB, 6, true>), g, t, 0, s, b, o, scr);
+    else hipLaunchKernelGGL((k_lean<WPB, 5, true>), g, t, 0, s, b, o, scr);
   } else {
-    if (occ == 4) hipLaunchKernelGGL((k_lean<WPB, 4, false>), g, t, 0, s, b, o);
-    else if (occ == 6) hipLaunchKernelGGL((k_lean<WPB, 6, false>), g, t, 0, s, b, o);
-    else hipLaunchKernelGGL((k_lean<WPB, 5, false>), g, t, 0, s, b, o);
+    if (occ == 4) hipLaunchKernelGGL((k_lean<WPB, 4, false>), g, t, 0, s, b, o, scr);
+    else if (occ == 6) hipLaunchKernelGGL((k_lean<WPB, 6, false>), g, t, 0, s, b, o, scr);
+    else hipLaunchKernelGGL((k_lean<WPB, 5, false>), g, t, 0, s, b, o, scr);
   }
 }
 
