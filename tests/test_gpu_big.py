@@ -134,3 +134,27 @@ def test_big_doc_handovers(engine, oracle):
     rng = np.random.default_rng(2)
     docs.append([_ds_update([(int(c), [(0, 1)])]) for c in rng.integers(0, 2 ** 32, 1100)])
     check_batch(engine, oracle, batch_of(docs))
+
+
+def test_update_with_2p21_gc_blocks(engine, oracle):
+    """One update of 2^21 + 5 GC blocks (4.2 MB), alone and twice (duplicate): above the
+    decode record's 21-bit block count, through the lane clamp of the fast path's decode
+    and on to the tiled kernel (ymerge_fast.hip hand-over); GPU == oracle."""
+    from test_gpu_lean import var
+    n = (1 << 21) + 5
+    u = bytes([1]) + var(n) + var(77) + var(0) + bytes([0, 1]) * n + bytes([0])
+    check_batch(engine, oracle, batch_of([[u], [u, u]]))
+
+
+def test_document_of_2p23_updates(engine, oracle):
+    """One document of 2^23 + 4 updates (2^23 + 3 empty ones around one insert): past the
+    fast path's 23-bit update index (hand-over at U >= 2^23); GPU == oracle."""
+    n = (1 << 23) + 3
+    ins = np.frombuffer(bytes([1, 1, 5, 0, 4, 1, 1, ord("t"), 1, ord("a"), 0]), np.uint8)
+    data = np.concatenate([np.tile(np.array([0, 0], np.uint8), n // 2), ins,
+                           np.tile(np.array([0, 0], np.uint8), n - n // 2)])
+    lens = np.full(n + 1, 2, np.uint64)
+    lens[n // 2] = len(ins)
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    b = workloads.Batch(data, off, np.array([0, n + 1], np.uint64))
+    check_batch(engine, oracle, b)

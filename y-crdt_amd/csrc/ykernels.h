@@ -47,7 +47,9 @@ struct FastOut {
   uint32_t *dbg = nullptr; // k_lean diagnostics (env YMERGE_LEAN_DEBUG): 8 words per document
   uint32_t *npath;  // npath[p]: documents handed to path p (1 exact engine, 2 tiled kernel); [3] tiled
                     // kernel in overlap mode, [4] tiled kernel -> exact engine, [5] of [1]:
-                    // tiny documents (FastCaps.in_cap / u_cap), [6] k_lean -> fast path
+                    // tiny documents (FastCaps.in_cap / u_cap), [6] k_lean -> fast path,
+                    // [7..13] k_lean hand-over reasons
+  unsigned long long *lean_total = nullptr; // k_lean output bytes: 64 partial sums, 8 words apart
 };
 size_t fast_lds_bytes(const FastCaps &c);
 // one wavefront per document for the common editor shape (ymerge_lean.hip): writes the

@@ -54,7 +54,7 @@ struct ymerge_ctx {
   hipStream_t s = nullptr;
   DevBuf in_bytes, in_upd_off, in_doc_upd, in_sv, in_sv_off, sync_off, sync_end, sync_st;
   DevBuf status, path, out_start, out_len, pack_off, counts, need, scr_off, scratch, sizes, spill_off, scan_tmp;
-  DevBuf arena, packed, counter, stamps, plan_small, plan_big, rec, ovf, big_scratch, lean_scr;
+  DevBuf arena, packed, counter, stamps, plan_small, plan_big, rec, ovf, big_scratch, lean_scr, lean_tot;
   // lib0 v2: v1x arena + offsets + per-update status, v2 output arena + sizes + offsets,
   // state-vector rest offsets + pre-status
   DevBuf v2x, v2x_sz, v2x_off, v2_ust, v2_out, v2_osz, v2_ooff, v2_svoff, v2_svend, v2_pre;
@@ -67,6 +67,7 @@ struct ymerge_ctx {
   ym::FastCaps caps{4, 4096, 1024, 512, 512};
   int fast_threads = 256;
   bool lean = true; // k_lean first (env YMERGE_LEAN=0: every document through k_decode + k_fast_merge)
+  bool pack_stale = false; // pack_off not computed for the last merge (all documents on k_lean)
   std::mutex mu;
 };
 
@@ -76,7 +77,7 @@ static bool ctx_init(ymerge_ctx *c, int device) {
   c->device = device;
   if (hipSetDevice(device) != hipSuccess) return false;
   if (hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking) != hipSuccess) return false;
-  if (hipHostMalloc((void **)&c->h_pinned, 64 * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess) return false;
+  if (hipHostMalloc((void **)&c->h_pinned, 1024 * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess) return false;
   for (auto &e : c->ev)
     if (hipEventCreate(&e) != hipSuccess) return false;
   // YMERGE_FAST_THREADS: workgroup size of the fast path (256/512/1024); 0 routes every
@@ -112,7 +113,7 @@ extern "C" void ymerge_ctx_destroy(ymerge_ctx *c) {
                     &c->sync_end, &c->sync_st, &c->rec, &c->ovf, &c->status, &c->path,
                     &c->out_start, &c->out_len, &c->pack_off, &c->counts, &c->need, &c->scr_off, &c->scratch,
                     &c->sizes, &c->spill_off, &c->scan_tmp, &c->arena, &c->packed, &c->counter, &c->stamps,
-                    &c->plan_small, &c->plan_big, &c->big_scratch, &c->lean_scr, &c->v2x, &c->v2x_sz, &c->v2x_off, &c->v2_ust,
+                    &c->plan_small, &c->plan_big, &c->big_scratch, &c->lean_scr, &c->lean_tot, &c->v2x, &c->v2x_sz, &c->v2x_off, &c->v2_ust,
                     &c->v2_out, &c->v2_osz, &c->v2_ooff, &c->v2_svoff, &c->v2_svend, &c->v2_pre})
     b->release();
   if (c->h_pinned) hipHostFree(c->h_pinned);
@@ -187,9 +188,14 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     // BIG k_lean documents keep their size-proportional tables in HBM (untouched otherwise)
     const uint64_t lw = ym::lean_scratch_words(n_updates, n_docs, n_bytes);
     uint32_t *lscr = c->lean_scr.ensure(lw * 4 + 64) ? c->lean_scr.as<uint32_t>() : nullptr;
+    if (!c->lean_tot.ensure(64 * 64)) return YMERGE_ERR_DEVICE;
+    hipMemsetAsync(c->lean_tot.p, 0, 64 * 64, c->s);
+    fo.lean_total = c->lean_tot.as<unsigned long long>();
     ym::launch_lean(b, fo, lscr, c->s);
     if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
+    // hand-over count and k_lean's output bytes (npath[6], the 64 partial sums) in one sync
     hipMemcpyAsync(c->h_pinned + 16, c->counter.as<uint32_t>() + 10, 4, hipMemcpyDeviceToHost, c->s);
+    hipMemcpyAsync(c->h_pinned + 512, c->lean_tot.p, 64 * 64, hipMemcpyDeviceToHost, c->s);
     if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
     n_rej = (uint32_t)(c->h_pinned[16] & 0xFFFFFFFFu);
     b.only_path3 = 1;
@@ -282,11 +288,19 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
   }
   hipEventRecord(c->ev[2], c->s);
-  // total output bytes (and packed offsets for host copies)
-  ym::launch_scan_u64(olen, c->pack_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
-  hipEventRecord(c->ev[3], c->s);
+  // total output bytes (and packed offsets for host copies); when k_lean wrote every
+  // document its byte counter is the total and the scan waits for a host copy (pack_to_host)
   uint64_t total = 0;
-  if (!read_words(c, c->pack_off.as<uint64_t>() + n, 8, &total)) return YMERGE_ERR_DEVICE;
+  c->pack_stale = lean && n_rej == 0;
+  if (c->pack_stale) {
+    for (int q = 0; q < 64; q++) total += c->h_pinned[512 + 8 * q];
+    hipEventRecord(c->ev[3], c->s);
+    if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
+  } else {
+    ym::launch_scan_u64(olen, c->pack_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
+    hipEventRecord(c->ev[3], c->s);
+    if (!read_words(c, c->pack_off.as<uint64_t>() + n, 8, &total)) return YMERGE_ERR_DEVICE;
+  }
   if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
   float t01 = 0, t12 = 0, t23 = 0, t03 = 0, t05 = 0, t61 = 0, t70 = 0;
   hipEventElapsedTime(&t70, c->ev[7], c->ev[0]);
@@ -343,6 +357,7 @@ static int plan_exec(ymerge_ctx *c, bool diff, const uint8_t *d_bytes, const uin
   if (n_docs > 0xFFFFFFFFull) return YMERGE_ERR_OTHER;
   const uint32_t n = (uint32_t)n_docs;
   ym::DiffBatch b{d_bytes, d_upd_off, d_sv, d_sv_off, n};
+  c->pack_stale = false; // pack_off = this batch's output offsets (set below)
   b.v1x = d_bytes == c->v2x.as<uint8_t>(); // the lib0 v2 path's transcoded arena
   b.frame = frame;
   if (frame == 1) {
@@ -480,6 +495,7 @@ static int v2_encode(ymerge_ctx *c, ymerge_device_result *res, uint32_t n, int m
   ym::launch_v2_encode(true, res->d_out, res->d_out_start, res->d_out_len, res->d_status, n,
                        c->v2_ooff.as<uint64_t>(), c->v2_out.as<uint8_t>(), mode, c->s);
   // packed offsets of the result (pack_to_host copies the arena in their order)
+  c->pack_stale = false;
   if (hipMemcpyAsync(c->pack_off.p, c->v2_ooff.p, nn * 8, hipMemcpyDeviceToDevice, c->s) != hipSuccess)
     return YMERGE_ERR_DEVICE;
   if (hipStreamSynchronize(c->s) != hipSuccess || hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
@@ -552,6 +568,10 @@ static int pack_to_host(ymerge_ctx *c, const ymerge_device_result *res, uint64_t
                         uint64_t *out_off, uint8_t *status) {
   const uint32_t n = (uint32_t)n_docs;
   if (!c->packed.ensure(res->out_bytes + 64)) return YMERGE_ERR_DEVICE;
+  if (c->pack_stale) { // packed offsets of a merge whose documents were all written by k_lean
+    ym::launch_scan_u64(res->d_out_len, c->pack_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
+    c->pack_stale = false;
+  }
   ym::launch_pack(res->d_out, res->d_out_start, res->d_out_len, c->pack_off.as<uint64_t>(),
                   c->packed.as<uint8_t>(), n, c->s);
   if (out && res->out_bytes &&

@@ -1036,6 +1036,9 @@ __device__ __forceinline__ void lean_doc(const BatchIn &b, const FastOut &o, Lea
     o.status[d] = 0;
     o.out_len[d] = total;
     o.out_start[d] = slot;
+    // batch output bytes: 64 counters 64 B apart (one address for a million documents
+    // serialises the L2 atomics: +7 ms on C3)
+    if (o.lean_total) atomicAdd(o.lean_total + 8 * (d & 63), (unsigned long long)total);
   }
   stamp(6);
   if (STAMPS && lane == 0) {
