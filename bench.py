@@ -197,7 +197,7 @@ def run_merge(a, rank, world, dev):
     docs_exact, docs_big = int(kstats[-1]["docs_exact"]), int(kstats[-1]["docs_big"])
     docs_tiny = int(kstats[-1]["docs_tiny"])
 
-    e2e = None
+    e2e = e2e_abi = pcie = None
     if not a.no_e2e:  # end-to-end: pinned host arena -> H2D -> pipeline -> pack -> D2H
         h_b = torch.from_numpy(ymerge.padded(batch.data)).pin_memory()
         h_u = torch.from_numpy(batch.upd_off.view(np.int64)).pin_memory()
@@ -211,6 +211,24 @@ def run_merge(a, rank, world, dev):
         r.to_host()
         e2e = time.perf_counter() - t
         del g_b, g_u, g_d
+        # the server-facing C-ABI host entry (ymerge_updates_v1_batch): pageable host arrays
+        # in, a library-owned host result out (pinned double-buffered staging inside)
+        for _ in range(2):  # warm: the pinned result pool, the staging ring
+            eng.host_batch("ymerge_updates_v1_batch", batch.data, batch.upd_off, batch.n_updates, batch.doc_upd)
+        t = time.perf_counter()
+        eng.host_batch("ymerge_updates_v1_batch", batch.data, batch.upd_off, batch.n_updates, batch.doc_upd)
+        e2e_abi = time.perf_counter() - t  # (includes the wrapper's copy of the result into numpy)
+        # PCIe lower bound for the same bytes: pinned H2D of the input + D2H of the output
+        h_o = torch.empty(out_bytes, dtype=torch.uint8).pin_memory()
+        g = torch.empty(max(batch.n_bytes, out_bytes), dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        g[:batch.n_bytes].copy_(h_b[:batch.n_bytes], non_blocking=True)
+        torch.cuda.synchronize(dev)
+        h_o.copy_(g[:out_bytes], non_blocking=True)
+        torch.cuda.synchronize(dev)
+        pcie = time.perf_counter() - t
+        del g, h_o
 
     allst = dist.gather_stats([batch.n_docs, batch.n_bytes, out_bytes, n_err, elapsed, ms_pipe,
                                e2e or 0.0], device=dev)
@@ -247,7 +265,11 @@ def run_merge(a, rank, world, dev):
                      "alg_bytes_per_launch": alg_bytes},
         "end_to_end": None if e2e is None else {
             "value": float(allst[:, 1].sum()) / float(allst[:, 6].max()) / 1e9, "unit": "GB/s",
-            "note": "pinned host arena -> H2D -> merge -> pack -> D2H, one batch"},
+            "note": "pinned host arena -> H2D -> merge -> pack -> D2H (pageable numpy), one batch",
+            "c_abi_host_entry": batch.n_bytes / e2e_abi / 1e9 if e2e_abi else None,
+            "c_abi_note": "ymerge_updates_v1_batch from pageable host arrays to a host result, rank 0",
+            "pcie_bound": batch.n_bytes / pcie / 1e9 if pcie else None,
+            "pcie_note": "input GB/s if only the pinned H2D of the input and D2H of the output ran"},
         "cpu_baseline": cpu,
     }
     return line

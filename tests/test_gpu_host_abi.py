@@ -154,3 +154,12 @@ def test_multi_context_merge_and_diff(oracle, n_ctx):
     finally:
         for e in engines:
             e.close()
+
+
+def test_pipelined_host_entry(engine, oracle):
+    """A host batch above 96 MB takes the pipelined path (document groups of ~48 MB: H2D,
+    merge and D2H overlapped); GPU == oracle, documents in input order."""
+    b = workloads.text_docs(4000, 1000, seed=21)
+    assert b.n_bytes >= 96 << 20
+    got = engine.host_batch("ymerge_updates_v1_batch", b.data, b.upd_off, len(b.upd_off) - 1, b.doc_upd)
+    _same(got, oracle.merge_batch(b.data, b.upd_off, b.doc_upd, mode=1, threads=8))
