@@ -81,6 +81,21 @@ def merge_updates_v1(updates, mode=0):
     return _take(out, olen)
 
 
+def compact_updates_v1(updates):
+    """Store-based compaction (yrs_oracle_store.c): a Doc (GC on) applies the updates in order,
+    one transaction each, then encode_state_as_update_v1 (yrs/src/transaction.rs:73-85)."""
+    bufs = [_buf(u) for u in updates]
+    n = len(bufs)
+    ptrs = (ctypes.POINTER(ctypes.c_uint8) * max(1, n))(*[ctypes.cast(b[0], ctypes.POINTER(ctypes.c_uint8)) for b in bufs])
+    lens = (ctypes.c_size_t * max(1, n))(*[b[1] for b in bufs])
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    st = lib().yo_compact_updates_v1(ptrs, lens, n, ctypes.byref(out), ctypes.byref(olen))
+    if st:
+        raise OracleError(st)
+    return _take(out, olen)
+
+
 def diff_updates_v1(update, sv):
     a, an = _buf(update)
     b, bn = _buf(sv)
@@ -217,6 +232,11 @@ def merge_batch(data, upd_off, doc_upd, mode=0, threads=1, version=1):
     arena = ctypes.string_at(out, total) if total else b""
     lib().yo_free(out)
     return arena, out_off, status[:n_docs]
+
+
+def compact_batch(data, upd_off, doc_upd, threads=1):
+    """compact_updates_v1 per document of an arena batch: (arena, offsets, status)."""
+    return merge_batch(data, upd_off, doc_upd, mode=8, threads=threads)
 
 
 def diff_batch(ubytes, u_off, svbytes, sv_off, threads=1, version=1):

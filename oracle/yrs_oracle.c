@@ -2374,6 +2374,7 @@ int yo_encode_state_vector_from_update_v1(const uint8_t *update, size_t len, uin
 void yo_free(void *p) { free(p); }
 
 #include "yrs_oracle_v2.c"
+#include "yrs_oracle_store.c"
 
 /* ------------------------------------------------------------------ y-sync framing
  * Message::encode / SyncMessage::encode (yrs/src/sync/protocol.rs:219-233, 245-258):
@@ -2460,8 +2461,11 @@ static void *worker(void *arg) {
           ptrs[u - u0] = j->bytes + j->upd_off[u];
           lens[u - u0] = j->upd_off[u + 1] - j->upd_off[u];
         }
-        st = (v2 ? yo_merge_updates_v2 : yo_merge_updates_v1)(ptrs, lens, u1 - u0, j->mode & 3, &j->outs[d],
-                                                              &j->lens[d]);
+        if (j->mode & 8) /* store-based compaction (yrs_oracle_store.c) */
+          st = yo_compact_updates_v1(ptrs, lens, u1 - u0, &j->outs[d], &j->lens[d]);
+        else
+          st = (v2 ? yo_merge_updates_v2 : yo_merge_updates_v1)(ptrs, lens, u1 - u0, j->mode & 3, &j->outs[d],
+                                                                &j->lens[d]);
       }
       j->status[d] = (uint8_t)st;
     }

@@ -37,6 +37,10 @@ enum {
 /* mode for merge: 0 = literal reference loop (per-iteration stable insertion
  * sort of all live decoders, DS re-squash after every input — same complexity
  * as yrs), 1 = equivalent fast form (decoder heap, single final squash). */
+/* store-based compaction: a Doc (GC on) applies the updates in order, one transaction each, then
+ * encode_state_as_update_v1 (yrs_oracle_store.c) */
+int yo_compact_updates_v1(const uint8_t *const *updates, const size_t *lens, size_t n, uint8_t **out,
+                          size_t *out_len);
 int yo_merge_updates_v1(const uint8_t *const *updates, const size_t *lens, size_t n,
                         int mode, uint8_t **out, size_t *out_len);
 int yo_diff_updates_v1(const uint8_t *update, size_t update_len, const uint8_t *sv,
