@@ -150,6 +150,16 @@ int ydiff_updates_v2_batch_device(ymerge_ctx *ctx, const uint8_t *d_bytes, const
 int yencode_state_vector_from_update_v2_batch_device(ymerge_ctx *ctx, const uint8_t *d_bytes,
                                                      const uint64_t *d_upd_off, uint64_t n_docs,
                                                      ymerge_device_result *res);
+/* Store-based compaction: document d's updates applied in order to a fresh
+ * yrs Doc with GC on, one transaction each (yffi ytransaction_apply, yffi/src/lib.rs:1078;
+ * TransactionMut::apply_update, yrs/src/transaction.rs:675-730), then the whole state encoded
+ * (ytransaction_state_diff_v1 with no state vector, yffi/src/lib.rs:802; Doc
+ * encode_state_as_update_v1, yrs/src/transaction.rs:73-85): squashed Items, GC'd content.
+ * Device shape (ycompact.hip header); documents outside it get status YMERGE_ERR_UNSUPPORTED
+ * (21), decode errors their yrs code. */
+int ycompact_updates_v1_batch_device(ymerge_ctx *ctx, const uint8_t *d_bytes, uint64_t n_bytes,
+                                     const uint64_t *d_upd_off, uint64_t n_updates, const uint64_t *d_doc_upd,
+                                     uint64_t n_docs, ymerge_device_result *res);
 /* pack the last device result into host buffers: out (res->out_bytes), out_off (n_docs + 1,
  * document d at out[out_off[d] .. out_off[d+1])), status (n_docs) */
 int ymerge_result_to_host(ymerge_ctx *ctx, const ymerge_device_result *res, uint64_t n_docs, uint8_t *out,
@@ -184,6 +194,8 @@ int ydiff_updates_v2_batch(ymerge_ctx *ctx, const uint8_t *bytes, const uint64_t
                            const uint64_t *sv_off, uint64_t n_docs, ymerge_batch_result **res);
 int yencode_state_vector_from_update_v2_batch(ymerge_ctx *ctx, const uint8_t *bytes, const uint64_t *upd_off,
                                               uint64_t n_docs, ymerge_batch_result **res);
+int ycompact_updates_v1_batch(ymerge_ctx *ctx, const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_updates,
+                              const uint64_t *doc_upd, uint64_t n_docs, ymerge_batch_result **res);
 void ymerge_batch_result_destroy(ymerge_batch_result *res);
 
 /* ---------------------------------------------------------------- multi-device (one node)

@@ -1,0 +1,76 @@
+"""GPU parity of store-based compaction (ycompact_updates_v1_batch[_device]: k_compact_count +
+k_compact on gfx950) against the oracle (oracle/yrs_oracle_store.c) and against the same
+kernel source built for the CPU (tools/hostemu): statuses equal the CPU build's for every
+document, bytes equal the oracle's for every document the device writes."""
+import numpy as np
+import pytest
+
+import workloads
+from compact_cases import edge_docs, fixtures, regrouped
+from test_compact_emu import emu  # noqa: F401 (fixture)
+from test_gpu_parity import engine  # noqa: F401 (fixture)
+
+pytestmark = pytest.mark.gpu
+
+
+def check_gpu(engine, emu, oracle, b, min_device=1.0, host_entry=False):
+    if host_entry:  # the C-ABI host-memory entry
+        out, off, st = engine.host_batch("ycompact_updates_v1_batch", b.data, b.upd_off, b.n_updates, b.doc_upd)
+    else:
+        out, off, st = engine.compact_host(b.data, b.upd_off, b.doc_upd)
+    eouts, est, ewhy = emu(b)
+    arena, aoff, ost = oracle.compact_batch(b.data, b.upd_off, b.doc_upd, threads=8)
+    bad = np.nonzero(st != est)[0]
+    assert len(bad) == 0, f"status differs from the CPU build at docs {bad[:10]}: gpu {st[bad[:10]]} cpu {est[bad[:10]]}"
+    done = 0
+    for d in range(b.n_docs):
+        g = out[int(off[d]):int(off[d + 1])].tobytes()
+        if st[d] == 21 and ost[d] != 21:
+            assert not g
+            continue
+        assert st[d] == ost[d], f"doc {d}: status {st[d]} oracle {ost[d]}"
+        e = arena[int(aoff[d]):int(aoff[d + 1])]
+        if g != e:
+            k = next((i for i in range(min(len(g), len(e))) if g[i] != e[i]), min(len(g), len(e)))
+            pytest.fail(f"doc {d}: first byte diff at {k} (gpu len {len(g)}, oracle len {len(e)})")
+        done += 1
+    assert done >= min_device * b.n_docs - 1e-9, f"{done}/{b.n_docs} documents on the device"
+    return st
+
+
+def test_text_docs(engine, emu, oracle):
+    for seed, mc, df in ((1, 4, 0.2), (2, 8, 0.4)):
+        check_gpu(engine, emu, oracle, workloads.text_docs(300, 300, seed=seed, max_clients=mc, del_frac=df))
+
+
+def test_zipf_docs(engine, emu, oracle):
+    check_gpu(engine, emu, oracle, workloads.zipf_docs(1000))
+
+
+def test_editing_traces(engine, emu, oracle):
+    for name in workloads.TRACES:
+        b, _ = workloads.trace_updates(name)
+        check_gpu(engine, emu, oracle, b)
+
+
+def test_merged_and_snapshot(engine, emu, oracle):
+    b = workloads.text_docs(60, 300, seed=23)
+    check_gpu(engine, emu, oracle, regrouped(oracle, b, k=7))
+    check_gpu(engine, emu, oracle, regrouped(oracle, b, head=200))
+
+
+def test_fixtures_and_edges(engine, emu, oracle):
+    _, b = fixtures()
+    check_gpu(engine, emu, oracle, b, min_device=0.6)
+    b, _ = edge_docs()
+    check_gpu(engine, emu, oracle, b, min_device=0.5)
+
+
+def test_mixed_shapes_and_pending(engine, emu, oracle):
+    """Nine-plus clients and withheld updates interleaved with ordinary documents."""
+    check_gpu(engine, emu, oracle, workloads.text_docs(100, 300, seed=5, max_clients=12), min_device=0.3)
+    check_gpu(engine, emu, oracle, workloads.delete_heavy_docs(16, 1000), min_device=0.0)
+
+
+def test_host_entry(engine, emu, oracle):
+    check_gpu(engine, emu, oracle, workloads.text_docs(200, 200, seed=9), host_entry=True)

@@ -61,6 +61,14 @@ inline uint64_t lean_scratch_words(uint64_t n_updates, uint64_t n_docs, uint64_t
   return 4 * n_updates + 64 * n_docs + n_bytes;
 }
 void launch_fast_merge(const BatchIn &b, const FastCaps &caps, const FastOut &o, int nt, hipStream_t s);
+// store-based compaction (ycompact.hip): one lane per document applies its updates to a
+// device block store; documents outside the device shape get status E_UNSUPPORTED.
+// k_compact_count fills a 32-word header per document and its scratch words (need[d]);
+// scr_off = exclusive scan of need (n_docs + 1 entries)
+constexpr uint32_t COMPACT_HDR_WORDS = 32;
+void launch_compact_count(const BatchIn &b, uint32_t *hdr, uint64_t *need, hipStream_t s);
+void launch_compact(const BatchIn &b, const FastOut &o, uint32_t *hdr, const uint64_t *scr_off, uint32_t *scr,
+                    hipStream_t s);
 
 // documents over the fast path's LDS capacities (path == 2): tiled, HBM scratch
 void launch_big_count(const BatchIn &b, const FastOut &o, uint32_t *counts, uint64_t *need, uint32_t *n_big,

@@ -56,7 +56,7 @@ struct ymerge_ctx {
   hipStream_t s = nullptr;
   DevBuf in_bytes, in_upd_off, in_doc_upd, in_sv, in_sv_off, sync_off, sync_end, sync_st;
   DevBuf status, path, out_start, out_len, pack_off, counts, need, scr_off, scratch, sizes, spill_off, scan_tmp;
-  DevBuf arena, packed, counter, stamps, plan_small, plan_big, rec, ovf, big_scratch, lean_scr, lean_tot;
+  DevBuf arena, packed, counter, stamps, plan_small, plan_big, rec, ovf, big_scratch, lean_scr, lean_tot, cscr;
   // lib0 v2: v1x arena + offsets + per-update status, v2 output arena + sizes + offsets,
   // state-vector rest offsets + pre-status
   DevBuf v2x, v2x_sz, v2x_off, v2_ust, v2_out, v2_osz, v2_ooff, v2_svoff, v2_svend, v2_pre;
@@ -122,7 +122,7 @@ extern "C" void ymerge_ctx_destroy(ymerge_ctx *c) {
                     &c->sync_end, &c->sync_st, &c->rec, &c->ovf, &c->status, &c->path,
                     &c->out_start, &c->out_len, &c->pack_off, &c->counts, &c->need, &c->scr_off, &c->scratch,
                     &c->sizes, &c->spill_off, &c->scan_tmp, &c->arena, &c->packed, &c->counter, &c->stamps,
-                    &c->plan_small, &c->plan_big, &c->big_scratch, &c->lean_scr, &c->lean_tot, &c->v2x, &c->v2x_sz, &c->v2x_off, &c->v2_ust,
+                    &c->plan_small, &c->plan_big, &c->big_scratch, &c->lean_scr, &c->lean_tot, &c->cscr, &c->v2x, &c->v2x_sz, &c->v2x_off, &c->v2_ust,
                     &c->v2_out, &c->v2_osz, &c->v2_ooff, &c->v2_svoff, &c->v2_svend, &c->v2_pre})
     b->release();
   if (c->h_pinned) hipHostFree(c->h_pinned);
@@ -566,6 +566,66 @@ extern "C" int ydiff_updates_v1_batch_device(ymerge_ctx *c, const uint8_t *d_byt
   return plan_exec(c, true, d_bytes, d_upd_off, d_sv, d_sv_off, n_docs, res);
 }
 
+// ---------------------------------------------------------------- store-based compaction
+// Each document's updates applied in order to a fresh yrs Doc (GC on), one transaction each,
+// then encode_state_as_update_v1 (ycompact.hip).  Output slots as for the merge; packed
+// offsets by a scan of the lengths.
+static int compact_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes, const uint64_t *d_upd_off,
+                          uint64_t n_updates, const uint64_t *d_doc_upd, uint64_t n_docs, ymerge_device_result *res) {
+  if (hipSetDevice(c->device) != hipSuccess) return YMERGE_ERR_DEVICE;
+  if (n_docs > 0xFFFFFFFFull) return YMERGE_ERR_OTHER;
+  const uint32_t n = (uint32_t)n_docs;
+  const size_t nn = (size_t)n + 1;
+  const uint64_t slots = 2 * n_bytes + 64 * (uint64_t)n_docs;
+  if (!c->status.ensure(nn) || !c->path.ensure(nn) || !c->out_start.ensure(nn * 8) || !c->out_len.ensure(nn * 8) ||
+      !c->pack_off.ensure(nn * 8) || !c->scan_tmp.ensure(ym::scan_tmp_elems(n) * 8 + 64) ||
+      !ensure_keep(c, c->arena, slots + 4096, 0) || !c->need.ensure(nn * 8) || !c->scr_off.ensure(nn * 8) ||
+      !c->counts.ensure(nn * ym::COMPACT_HDR_WORDS * 4))
+    return YMERGE_ERR_DEVICE;
+  ym::BatchIn b{d_bytes, d_upd_off, d_doc_upd, n, nullptr, nullptr};
+  ym::FastOut fo{c->arena.as<uint8_t>(), c->out_start.as<uint64_t>(), c->out_len.as<uint64_t>(),
+                 c->status.as<uint8_t>(), c->path.as<uint8_t>(), nullptr, nullptr, nullptr};
+  hipEventRecord(c->ev[0], c->s);
+  // per-document scratch from the counts (blocks, ranges, clients), then the store pass
+  ym::launch_compact_count(b, c->counts.as<uint32_t>(), c->need.as<uint64_t>(), c->s);
+  ym::launch_scan_u64(c->need.as<uint64_t>(), c->scr_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
+  uint64_t words = 0;
+  if (!read_words(c, c->scr_off.as<uint64_t>() + n, 8, &words)) return YMERGE_ERR_DEVICE;
+  if (!c->cscr.ensure(words * 4 + 64)) return YMERGE_ERR_DEVICE;
+  hipEventRecord(c->ev[2], c->s);
+  ym::launch_compact(b, fo, c->counts.as<uint32_t>(), c->scr_off.as<uint64_t>(), c->cscr.as<uint32_t>(), c->s);
+  if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
+  hipEventRecord(c->ev[1], c->s);
+  ym::launch_scan_u64(c->out_len.as<uint64_t>(), c->pack_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
+  c->pack_stale = false;
+  uint64_t total = 0;
+  if (!read_words(c, c->pack_off.as<uint64_t>() + n, 8, &total)) return YMERGE_ERR_DEVICE;
+  float t01 = 0, t21 = 0;
+  hipEventElapsedTime(&t01, c->ev[0], c->ev[1]);
+  hipEventElapsedTime(&t21, c->ev[2], c->ev[1]);
+  c->stats = ymerge_stats{};
+  c->stats.n_docs = n_docs;
+  c->stats.bytes_in = n_bytes;
+  c->stats.bytes_out = total;
+  c->stats.ms_total = t01;     // counts + scan + store pass
+  c->stats.ms_exact = t21;     // k_compact
+  c->stats.ms_decode = t01 - t21;
+  res->d_out = c->arena.as<uint8_t>();
+  res->d_out_start = c->out_start.as<uint64_t>();
+  res->d_out_len = c->out_len.as<uint64_t>();
+  res->d_status = c->status.as<uint8_t>();
+  res->arena_bytes = c->arena.cap;
+  res->out_bytes = total;
+  return 0;
+}
+extern "C" int ycompact_updates_v1_batch_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
+                                                const uint64_t *d_upd_off, uint64_t n_updates,
+                                                const uint64_t *d_doc_upd, uint64_t n_docs, ymerge_device_result *res) {
+  if (!c || !res) return YMERGE_ERR_OTHER;
+  std::lock_guard<std::mutex> g(c->mu);
+  return compact_device(c, d_bytes, n_bytes, d_upd_off, n_updates, d_doc_upd, n_docs, res);
+}
+
 // ---------------------------------------------------------------- lib0 v2 (yv2.hip)
 // v2 updates -> v1x arena (c->v2x, offsets c->v2x_off[n_upd + 1], status c->v2_ust)
 static int v2_transcode(ymerge_ctx *c, const uint8_t *d_bytes, const uint64_t *d_upd_off, uint64_t n_upd,
@@ -719,6 +779,11 @@ extern "C" int ymerge_updates_v1_batch(ymerge_ctx *c, const uint8_t *bytes, cons
                                        uint64_t n_updates, const uint64_t *doc_upd, uint64_t n_docs,
                                        ymerge_batch_result **out) {
   return host_merge(c, 1, bytes, upd_off, n_updates, doc_upd, n_docs, out);
+}
+extern "C" int ycompact_updates_v1_batch(ymerge_ctx *c, const uint8_t *bytes, const uint64_t *upd_off,
+                                         uint64_t n_updates, const uint64_t *doc_upd, uint64_t n_docs,
+                                         ymerge_batch_result **out) {
+  return host_merge(c, 3, bytes, upd_off, n_updates, doc_upd, n_docs, out);
 }
 extern "C" int ymerge_updates_v2_batch(ymerge_ctx *c, const uint8_t *bytes, const uint64_t *upd_off,
                                        uint64_t n_updates, const uint64_t *doc_upd, uint64_t n_docs,
@@ -876,7 +941,7 @@ static int host_merge(ymerge_ctx *c, int version, const uint8_t *bytes, const ui
       hipMemcpyAsync(c->in_doc_upd.p, doc_upd, (n_docs + 1) * 8, hipMemcpyHostToDevice, c->s) != hipSuccess)
     return YMERGE_ERR_DEVICE;
   ymerge_device_result dr{};
-  int st = (version == 2 ? merge_v2_device : merge_device)(c, c->in_bytes.as<uint8_t>(), nbytes,
+  int st = (version == 3 ? compact_device : version == 2 ? merge_v2_device : merge_device)(c, c->in_bytes.as<uint8_t>(), nbytes,
                                                            c->in_upd_off.as<uint64_t>(), n_updates,
                                                            c->in_doc_upd.as<uint64_t>(), n_docs, &dr);
   if (st) return st;

@@ -59,6 +59,7 @@ HOST_BATCH = {
     "ydiff_updates_v1_batch": "bobo", "ydiff_updates_v2_batch": "bobo",
     "yencode_state_vector_from_update_v1_batch": "bo", "yencode_state_vector_from_update_v2_batch": "bo",
     "ysync_step1_v1_batch": "bo", "ysync_step2_v1_batch": "bobo",
+    "ycompact_updates_v1_batch": "bono",
 }
 
 _lib = None
@@ -101,6 +102,7 @@ def lib():
         getattr(L, f"yencode_state_vector_from_update_{v}").restype = vp
         getattr(L, f"yencode_state_vector_from_update_{v}").argtypes = [c.c_char_p, u32, c.POINTER(u32)]
     L.ymerge_updates_v2_batch_device.argtypes = [vp, vp, u64, vp, u64, vp, u64, c.POINTER(_DevRes)]
+    L.ycompact_updates_v1_batch_device.argtypes = [vp, vp, u64, vp, u64, vp, u64, c.POINTER(_DevRes)]
     L.ydiff_updates_v2_batch_device.argtypes = [vp, vp, vp, vp, vp, u64, c.POINTER(_DevRes)]
     L.yencode_state_vector_from_update_v2_batch_device.argtypes = [vp, vp, vp, u64, c.POINTER(_DevRes)]
     L.ymerge_binary_destroy.argtypes = [vp, u32]
@@ -280,6 +282,17 @@ class Engine:
             raise DeviceError(f"merge batch failed ({rc})")
         return DeviceResult(self, res, n_docs)
 
+    def compact_device(self, d_bytes, n_bytes, d_upd_off, n_updates, d_doc_upd, n_docs):
+        """Store-based compaction (ycompact_updates_v1_batch_device): each document's updates
+        applied in order to a fresh Doc, then encode_state_as_update_v1.  Same argument
+        layout as merge_device; documents outside the device shape get status 21."""
+        res = _DevRes()
+        rc = lib().ycompact_updates_v1_batch_device(self._ctx, d_bytes, n_bytes, d_upd_off, n_updates, d_doc_upd,
+                                                     n_docs, ctypes.byref(res))
+        if rc:
+            raise DeviceError(f"compaction batch failed ({rc})")
+        return DeviceResult(self, res, n_docs)
+
     def diff_device(self, d_bytes, d_upd_off, d_sv, d_sv_off, n_docs, version=1):
         """Device pointers in, DeviceResult out; the update arena must stay readable 16 bytes
         past its end (`padded`), as for merge_device."""
@@ -397,3 +410,11 @@ class Engine:
         r = self.merge_device(t_b.data_ptr(), int(upd_off[-1]), t_u.data_ptr(), len(upd_off) - 1, t_d.data_ptr(),
                               len(doc_upd) - 1, version)
         return r.to_host()
+
+    def compact_host(self, data, upd_off, doc_upd):
+        """compact_device over host arrays (torch for HBM residency)."""
+        ub = np.ascontiguousarray(data, dtype=np.uint8)
+        args = [ub if len(ub) else np.zeros(1, np.uint8), np.asarray(upd_off, np.uint64).view(np.int64),
+                np.asarray(doc_upd, np.uint64).view(np.int64)]
+        return self._host_batch(args, lambda a, b, c: self.compact_device(a, int(upd_off[-1]), b, len(upd_off) - 1,
+                                                                          c, len(doc_upd) - 1))
