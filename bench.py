@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="target wall time of one CPU-baseline run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-compact", action="store_true", help="skip the store-based compaction line (c2)")
     return ap.parse_args()
 
 
@@ -232,6 +233,10 @@ def run_merge(a, rank, world, dev):
         pcie = time.perf_counter() - t
         del g, h_o
 
+    compact = None
+    if a.workload == "c2" and not a.no_compact and rank == 0:
+        compact = run_compact(a, eng, batch, (t_b, t_u, t_d), dev, world)
+
     allst = dist.gather_stats([batch.n_docs, batch.n_bytes, out_bytes, n_err, elapsed, ms_pipe,
                                e2e or 0.0], device=dev)
     if rank != 0:
@@ -273,8 +278,44 @@ def run_merge(a, rank, world, dev):
             "pcie_bound": batch.n_bytes / pcie / 1e9 if pcie else None,
             "pcie_note": "input GB/s if only the pinned H2D of the input and D2H of the output ran"},
         "cpu_baseline": cpu,
+        "store_compaction": compact,
     }
     return line
+
+
+def run_compact(a, eng, batch, tensors, dev, world):
+    """Store-based compaction (ycompact_updates_v1_batch_device) of the same
+    resident batch: every document's updates applied in order to a fresh Doc, then
+    encode_state_as_update_v1.  Rank 0's shard; the CPU oracle on a bounded sample beside it."""
+    import oracle
+    t_b, t_u, t_d = tensors
+    args = (t_b.data_ptr(), batch.n_bytes, t_u.data_ptr(), batch.n_updates, t_d.data_ptr(), batch.n_docs)
+    eng.compact_device(*args)  # warm-up: scratch allocation
+    runs = []
+    for _ in range(2):
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        r = eng.compact_device(*args)
+        torch.cuda.synchronize(dev)
+        runs.append(time.perf_counter() - t)
+    st_k = eng.stats()
+    _, _, st = r.to_host()
+    dt = min(runs)
+    cpu = None
+    if not a.no_cpu_baseline and world == 1:
+        k = min(batch.n_docs, 1000)
+        s = batch.prefix(k)
+        threads = min(8, os.cpu_count() or 1)
+        t = time.perf_counter()
+        oracle.compact_batch(s.data, s.upd_off, s.doc_upd, threads=threads)
+        ct = time.perf_counter() - t
+        cpu = {"value": s.n_bytes / ct / 1e9, "unit": "GB/s", "docs_per_s": k / ct, "cores": threads, "kind": "port",
+               "sample": f"oracle/yrs_oracle_store.c compact_updates_v1 on the first {k} documents"}
+    return {"value": batch.n_bytes / dt / 1e9, "unit": "GB/s", "docs_per_s": batch.n_docs / dt, "ms": dt * 1e3,
+            "k_compact_ms": st_k["ms_exact"], "count_scan_ms": st_k["ms_decode"],
+            "out_bytes": int(r.out_bytes), "docs_device": int((st == 0).sum()),
+            "docs_unsupported": int((st == 21).sum()),
+            "kernel": "k_compact_count + k_compact (lane per document)", "cpu_baseline": cpu}
 
 
 def run_diff(a, rank, world, dev):

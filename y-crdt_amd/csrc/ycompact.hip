@@ -1008,11 +1008,13 @@ __device__ void compact_doc(const BatchIn &b, const FastOut &o, uint32_t *hdr, c
   o.out_len[d] = status ? 0 : olen;
 }
 
+// lpw documents per wavefront (lanes >= lpw idle): fewer lanes per wave trade SIMD width for
+// less divergence and more waves in flight on a latency-bound, branchy lane body
 __global__ void __launch_bounds__(64) k_compact(BatchIn b, FastOut o, uint32_t *hdr, const uint64_t *scr_off,
-                                                 uint32_t *scr) {
+                                                 uint32_t *scr, uint32_t lpw) {
   ym_set_grammar(0);
-  const uint32_t d = blockIdx.x * 64 + threadIdx.x;
-  if (d < b.n_docs) compact_doc(b, o, hdr, scr_off, scr, d);
+  const uint32_t d = blockIdx.x * lpw + threadIdx.x;
+  if (threadIdx.x < lpw && d < b.n_docs) compact_doc(b, o, hdr, scr_off, scr, d);
 }
 
 // ------------------------------------------------------------------ counts (scratch sizing)
@@ -1076,9 +1078,10 @@ void launch_compact_count(const BatchIn &b, uint32_t *hdr, uint64_t *need, hipSt
   hipLaunchKernelGGL(k_compact_count, dim3((b.n_docs + 63) / 64), dim3(64), 0, s, b, hdr, need);
 }
 void launch_compact(const BatchIn &b, const FastOut &o, uint32_t *hdr, const uint64_t *scr_off, uint32_t *scr,
-                    hipStream_t s) {
+                    uint32_t lpw, hipStream_t s) {
   if (!b.n_docs) return;
-  hipLaunchKernelGGL(k_compact, dim3((b.n_docs + 63) / 64), dim3(64), 0, s, b, o, hdr, scr_off, scr);
+  if (lpw < 1 || lpw > 64) lpw = 64;
+  hipLaunchKernelGGL(k_compact, dim3((b.n_docs + lpw - 1) / lpw), dim3(64), 0, s, b, o, hdr, scr_off, scr, lpw);
 }
 
 } // namespace ym

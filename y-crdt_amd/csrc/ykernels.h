@@ -68,7 +68,7 @@ void launch_fast_merge(const BatchIn &b, const FastCaps &caps, const FastOut &o,
 constexpr uint32_t COMPACT_HDR_WORDS = 32;
 void launch_compact_count(const BatchIn &b, uint32_t *hdr, uint64_t *need, hipStream_t s);
 void launch_compact(const BatchIn &b, const FastOut &o, uint32_t *hdr, const uint64_t *scr_off, uint32_t *scr,
-                    hipStream_t s);
+                    uint32_t lpw, hipStream_t s);
 
 // documents over the fast path's LDS capacities (path == 2): tiled, HBM scratch
 void launch_big_count(const BatchIn &b, const FastOut &o, uint32_t *counts, uint64_t *need, uint32_t *n_big,

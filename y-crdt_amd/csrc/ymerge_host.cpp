@@ -70,6 +70,7 @@ struct ymerge_ctx {
   int fast_threads = 256;
   bool lean = true; // k_lean first (env YMERGE_LEAN=0: every document through k_decode + k_fast_merge)
   bool pack_stale = false; // pack_off not computed for the last merge (all documents on k_lean)
+  uint32_t compact_lpw = 64; // k_compact documents per wavefront (env YMERGE_COMPACT_LPW)
   // host staging: two pinned buffers (double-buffered H2D / D2H of caller memory)
   uint8_t *stage[2] = {nullptr, nullptr};
   hipEvent_t stage_ev[2] = {nullptr, nullptr};
@@ -95,6 +96,7 @@ static bool ctx_init(ymerge_ctx *c, int device) {
   if (const char *v = getenv("YMERGE_STAMPS")) c->want_stamps = atoi(v) != 0;
   if (const char *v = getenv("YMERGE_TINY")) c->caps.in_cap = (uint32_t)atoi(v); // 0: no tiny path
   if (const char *v = getenv("YMERGE_LEAN")) c->lean = atoi(v) != 0;
+  if (const char *v = getenv("YMERGE_COMPACT_LPW")) c->compact_lpw = (uint32_t)atoi(v);
   // the fast kernel's LDS layout must fit one workgroup (160 KB on gfx950)
   int lds_max = 0;
   if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess) return false;
@@ -593,7 +595,8 @@ static int compact_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_byte
   if (!read_words(c, c->scr_off.as<uint64_t>() + n, 8, &words)) return YMERGE_ERR_DEVICE;
   if (!c->cscr.ensure(words * 4 + 64)) return YMERGE_ERR_DEVICE;
   hipEventRecord(c->ev[2], c->s);
-  ym::launch_compact(b, fo, c->counts.as<uint32_t>(), c->scr_off.as<uint64_t>(), c->cscr.as<uint32_t>(), c->s);
+  ym::launch_compact(b, fo, c->counts.as<uint32_t>(), c->scr_off.as<uint64_t>(), c->cscr.as<uint32_t>(),
+                     c->compact_lpw, c->s);
   if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
   hipEventRecord(c->ev[1], c->s);
   ym::launch_scan_u64(c->out_len.as<uint64_t>(), c->pack_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
