@@ -14,5 +14,7 @@ extern "C" void emu_compact_batch(const uint8_t *bytes, const uint64_t *upd_off,
   for (uint32_t d = 0; d < n_docs; d++) ym::compact_count_doc(b, hdr.data(), need.data(), d);
   for (uint32_t d = 0; d < n_docs; d++) off[d + 1] = off[d] + need[d];
   std::vector<uint32_t> scr(off[n_docs] + 16);
-  for (uint32_t d = 0; d < n_docs; d++) ym::compact_doc(b, o, hdr.data(), off.data(), scr.data(), d);
+  alignas(16) uint8_t stage[ym::CP_STAGE];
+  uint32_t misc[ym::M_END];
+  for (uint32_t d = 0; d < n_docs; d++) ym::compact_doc(b, o, hdr.data(), off.data(), scr.data(), d, stage, misc);
 }

@@ -10,6 +10,7 @@
 #define __global__
 #define __forceinline__ inline
 #define __noinline__ __attribute__((noinline))
+#define __align__(n) alignas(n)
 #define __shared__
 #define __constant__
 #define __launch_bounds__(...)
@@ -23,6 +24,7 @@ struct emu_idx {
 };
 static emu_idx blockIdx, threadIdx;
 #define hipLaunchKernelGGL(...) ((void)0)
+#define __builtin_amdgcn_s_memtime() 0ull
 static inline int __clz(int x) { return x ? __builtin_clz((unsigned)x) : 32; }
 static inline int __clzll(long long x) { return x ? __builtin_clzll((unsigned long long)x) : 64; }
 static inline long long __double_as_longlong(double d) {

@@ -18,9 +18,9 @@ NAMES = ["decode", "-", "sort", "classify", "sizes", "write", "ds_clients", "ds_
 BIG_NAMES = ["gather", "sort", "classify", "write", "deleteset"]
 
 
-def main_big(n):
-    """Tiled-kernel documents (k_big_merge, marker 0xB16 in slot 7) of a C3-style batch."""
-    b = workloads.zipf_docs(n, seed=0x5EED)
+def main_big(n, kind="c3"):
+    """Tiled-kernel documents (k_big_merge, marker 0xB16 in slot 7) of a C3-style (or C4) batch."""
+    b = workloads.zipf_docs(n, seed=0x5EED) if kind == "c3" else workloads.delete_heavy_docs(n)
     e = ymerge.Engine(0)
     e.merge_host(b.data, b.upd_off, b.doc_upd)
     L = ymerge.lib()
@@ -40,6 +40,40 @@ def main_big(n):
         if sel.any():
             print(f"  U in ({lo},{hi}]: {sel.sum()} docs, cycles/doc {tot[sel].mean():.0f}, "
                   + ", ".join(f"{nm} {d[sel, i].mean():.0f}" for i, nm in enumerate(BIG_NAMES)))
+
+
+def main_c1():
+    """The automerge-paper trace as one document (C1): tiled-kernel phase split."""
+    b, _ = workloads.trace_updates("automerge-paper")
+    e = ymerge.Engine(0)
+    e.merge_host(b.data, b.upd_off, b.doc_upd)
+    L = ymerge.lib()
+    L.ymerge_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+    st = np.zeros((1, 16), np.uint64)
+    assert L.ymerge_debug_stamps(e._ctx, 1, st.ctypes.data) == 0
+    d = np.diff(st[0, :6].astype(np.int64))
+    print("marker", hex(int(st[0, 7])), "stats", e.stats())
+    for i, nm in enumerate(BIG_NAMES):
+        print(f"  {nm:10s} {d[i]:10d} cycles ({d[i] / 100e3:.3f} ms at 100 MHz)  {100 * d[i] / d.sum():5.1f}%")
+
+
+def main_compact(n, lpw):
+    """k_compact (store-based compaction) of C2 documents: per-document phase cycle sums."""
+    os.environ["YMERGE_COMPACT_LPW"] = str(lpw)
+    b = workloads.text_docs(n, 1000)
+    e = ymerge.Engine(0)
+    e.compact_host(b.data, b.upd_off, b.doc_upd)
+    L = ymerge.lib()
+    L.ymerge_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+    st = np.zeros((n, 16), np.uint64)
+    assert L.ymerge_debug_stamps(e._ctx, n, st.ctypes.data) == 0
+    print(f"compact docs {n}, lpw {lpw}: {e.stats()['ms_exact']:.2f} ms k_compact")
+    tot = st[:, :5].sum(axis=1).astype(np.float64)
+    upd = np.maximum(st[:, 5].astype(np.float64), 1)
+    print(f"  cycles/doc {tot.mean():.0f}, cycles/update {(tot / upd).mean():.0f}")
+    for i, nm in enumerate(["decode", "integrate", "apply_delete", "commit", "encode"]):
+        v = st[:, i].astype(np.float64)
+        print(f"  {nm:12s} {v.mean():12.0f} cycles/doc {(v / upd).mean():8.0f} /update {100 * v.mean() / tot.mean():5.1f}%")
 
 
 def main_zipf(n):
@@ -101,6 +135,12 @@ def main():
         return main_zipf(int(sys.argv[2]) if len(sys.argv) > 2 else 20000)
     if len(sys.argv) > 1 and sys.argv[1] == "big":
         return main_big(int(sys.argv[2]) if len(sys.argv) > 2 else 20000)
+    if len(sys.argv) > 1 and sys.argv[1] == "c4":
+        return main_big(int(sys.argv[2]) if len(sys.argv) > 2 else 2000, "c4")
+    if len(sys.argv) > 1 and sys.argv[1] == "c1":
+        return main_c1()
+    if len(sys.argv) > 1 and sys.argv[1] == "compact":
+        return main_compact(int(sys.argv[2]) if len(sys.argv) > 2 else 10000, int(sys.argv[3]) if len(sys.argv) > 3 else 16)
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
     threads = os.environ.get("YMERGE_FAST_THREADS", "256")
     b = workloads.text_docs(n, 1000)

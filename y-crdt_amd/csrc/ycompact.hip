@@ -30,6 +30,7 @@
 namespace ym {
 
 constexpr uint32_t CP_MAXCL = 8, CP_MAXROOT = 4;
+constexpr uint32_t CP_STAGE = 256; // per-lane LDS copy of the current update (bytes)
 constexpr uint32_t CNIL = 0xFFFFFFFFu;
 // item words
 enum : uint32_t {
@@ -65,7 +66,11 @@ enum : uint32_t {
   M_CBK = M_ROOTSTART + CP_MAXROOT, // client -> its arrival array (index into the count header)
   M_UE = M_CBK + CP_MAXCL,          // update DS entry clients [16] (table order)
   M_UEN = M_UE + 16,               // ranges per entry [16]
-  M_END = M_UEN + 16
+  M_HCL = M_UEN + 16,               // the count header's block clients [8]
+  M_HCN = M_HCL + CP_MAXCL,         // their block counts (arrival capacities) [8]
+  M_HCO = M_HCN + CP_MAXCL,         // their arrival arrays' offsets (pairs) [8]
+  M_HNCL = M_HCO + CP_MAXCL,        // header clients
+  M_END = M_HNCL + 1
 };
 static_assert(M_END <= 1024, "misc area");
 // per-document counts from k_compact_count (CP_HDR words per document): blocks, deleted
@@ -94,7 +99,9 @@ enum : uint32_t {
 };
 
 struct CDoc {
-  const uint8_t *p; // the document's bytes
+  const uint8_t *p;  // the document's bytes
+  const uint8_t *up; // the current update's bytes (an LDS copy when it fits the lane's stage)
+  uint32_t uoff;     // its offset in the document
   uint32_t *it, *sg, *cb, *m;
   uint32_t *ubr, *ub, *stk, *ur, *mb; // update blocks (stream order, integration order), stack,
                                       // DS ranges, merge blocks
@@ -128,8 +135,8 @@ __device__ int cp_cl_add(CDoc &D, uint32_t client) { // BlockStore::get_client_b
     return -1;
   }
   uint32_t k = 0;
-  while (k < D.h[H_NCL] && D.h[H_CL + k] != client) k++;
-  if (k == D.h[H_NCL]) {
+  while (k < D.m[M_HNCL] && D.m[M_HCL + k] != client) k++;
+  if (k == D.m[M_HNCL]) {
     cp_unsup(D, CU_ARRIVALS);
     return -1;
   }
@@ -154,7 +161,7 @@ __device__ uint32_t cp_clock(CDoc &D, int c) { // ClientBlockList::clock
 __device__ uint32_t cp_cell(CDoc &D, int c, uint32_t clock) {
   if (c < 0) return CNIL;
   const uint32_t n = D.m[M_NBLK + c];
-  const uint32_t *a = D.cb + 2ull * D.h[H_CO + D.m[M_CBK + c]];
+  const uint32_t *a = D.cb + 2ull * D.m[M_HCO + D.m[M_CBK + c]];
   if (!n || a[0] > clock) return CNIL;
   uint32_t lo = 0, hi = n - 1; // last arrived block starting <= clock
   while (lo < hi) {
@@ -185,6 +192,9 @@ __device__ uint32_t cp_new_item(CDoc &D) {
   D.I(x, I_SEG0) = D.I(x, I_SEG1) = CNIL;
   return x;
 }
+// segment words: byte offset in the document, length | SEG_ASCII (every char one byte: UTF-16
+// offsets are byte offsets), next
+constexpr uint32_t SEG_ASCII = 0x80000000u, SEG_LEN = 0x7FFFFFFFu;
 __device__ uint32_t cp_new_seg(CDoc &D, uint32_t off, uint32_t n) {
   if (D.ns == D.cap_s) {
     cp_unsup(D, CU_ITEMS);
@@ -199,16 +209,22 @@ __device__ uint32_t cp_new_seg(CDoc &D, uint32_t off, uint32_t n) {
 // ItemContent::splice(off, Utf16) of a String (block.rs:1837-1879, split_str :1483-1502): the
 // item keeps [0, off) (a char is never cut: the UTF-16 offset maps to the next char boundary;
 // landing inside a surrogate pair is outside the device shape); returns the right part's
-// first segment and its UTF-16 length
-__device__ uint32_t cp_str_split(CDoc &D, uint32_t x, uint32_t off, uint32_t &rlen) {
-  uint32_t u = 0, s = D.I(x, I_SEG0), prev = CNIL;
+// first segment.  Its UTF-16 length is the item's minus off: an item's length equals its
+// content's UTF-16 length on the device (the surrogate case above is the only exception).
+__device__ uint32_t cp_str_split(CDoc &D, uint32_t x, uint32_t off) {
+  uint32_t u = 0, s = D.I(x, I_SEG0);
   while (s != CNIL) {
-    const uint8_t *b = D.p + D.sg[3 * s];
-    const uint32_t n = D.sg[3 * s + 1];
+    const uint32_t lw = D.sg[3 * s + 1], n = lw & SEG_LEN;
     uint32_t i = 0;
-    while (i < n && u < off) {
-      const uint32_t ch = utf8_next(b, n, i);
-      u += ch_len16(ch);
+    if (lw & SEG_ASCII) {
+      i = off - u < n ? off - u : n;
+      u += i;
+    } else {
+      const uint8_t *b = D.p + D.sg[3 * s];
+      while (i < n && u < off) {
+        const uint32_t ch = utf8_next(b, n, i);
+        u += ch_len16(ch);
+      }
     }
     if (u >= off) {
       if (u != off) {
@@ -221,28 +237,17 @@ __device__ uint32_t cp_str_split(CDoc &D, uint32_t x, uint32_t off, uint32_t &rl
         D.sg[3 * s + 2] = CNIL;
         D.I(x, I_SEG1) = s;
       } else {
-        r = cp_new_seg(D, D.sg[3 * s] + i, n - i);
+        r = cp_new_seg(D, D.sg[3 * s] + i, (n - i) | (lw & SEG_ASCII));
         if (r == CNIL) return CNIL;
         D.sg[3 * r + 2] = D.sg[3 * s + 2];
-        D.sg[3 * s + 1] = i;
+        D.sg[3 * s + 1] = i | (lw & SEG_ASCII);
         D.sg[3 * s + 2] = CNIL;
         D.I(x, I_SEG1) = s;
       }
-      // UTF-16 length of the right part
-      uint32_t rl = 0, tb = 0;
-      for (uint32_t q = r; q != CNIL; q = D.sg[3 * q + 2]) {
-        const uint8_t *bb = D.p + D.sg[3 * q];
-        const uint32_t nn = D.sg[3 * q + 1];
-        tb += nn;
-        for (uint32_t k = 0; k < nn;) rl += ch_len16(utf8_next(bb, nn, k));
-      }
-      rlen = tb == 1 ? 1 : rl;
       return r;
     }
-    prev = s;
     s = D.sg[3 * s + 2];
   }
-  (void)prev;
   D.st = E_PANIC; // offset past the content: yrs' splice unwraps None
   return CNIL;
 }
@@ -255,14 +260,13 @@ __device__ uint32_t cp_split(CDoc &D, uint32_t x, uint32_t off) {
   if (fl & F_DELC) {
     D.I(r, I_LEN) = D.I(x, I_LEN) - off;
   } else {
-    uint32_t rl = 0;
-    const uint32_t rs = cp_str_split(D, x, off, rl);
+    const uint32_t seg1 = D.I(x, I_SEG1); // the right part ends where the item did
+    const uint32_t rs = cp_str_split(D, x, off);
     if (D.st) return CNIL;
     D.I(r, I_SEG0) = rs;
-    uint32_t t = rs;
-    while (t != CNIL && D.sg[3 * t + 2] != CNIL) t = D.sg[3 * t + 2];
-    D.I(r, I_SEG1) = t;
-    D.I(r, I_LEN) = rl;
+    // the split segment was the last one: the new right segment is the last; else the old last
+    D.I(r, I_SEG1) = rs == CNIL ? CNIL : D.I(x, I_SEG1) == seg1 ? rs : seg1;
+    D.I(r, I_LEN) = D.I(x, I_LEN) - off;
   }
   const uint32_t c = fl >> 24;
   D.I(r, I_CLOCK) = D.I(x, I_CLOCK) + off;
@@ -406,11 +410,11 @@ __device__ void cp_push(CDoc &D, int c, uint32_t x) {
   D.m[M_TAIL + c] = x;
   const uint32_t n = D.m[M_NBLK + c];
   const uint32_t k = D.m[M_CBK + c];
-  if (n == D.h[H_CN + k]) {
+  if (n == D.m[M_HCN + k]) {
     cp_unsup(D, CU_ARRIVALS);
     return;
   }
-  uint32_t *a = D.cb + 2ull * D.h[H_CO + k];
+  uint32_t *a = D.cb + 2ull * D.m[M_HCO + k];
   a[2 * n] = D.I(x, I_CLOCK);
   a[2 * n + 1] = x;
   D.m[M_NBLK + c] = n + 1;
@@ -595,14 +599,14 @@ struct CpSink {
 // (integrated or skipped), 1 = a dependency on client `dep` is missing, -1 = stop (D.st)
 __device__ int cp_block(CDoc &D, const uint32_t *ub, uint32_t &dep) {
   const uint32_t client = ub[0], clock = ub[1], bpos = ub[2], len = ub[3];
-  const uint8_t info = D.p[bpos];
+  const uint8_t info = D.up[bpos]; // bpos: within the current update
   if (info == 10) return 0; // Skip
   const uint32_t lc = cp_clock(D, cp_cl_find(D, client));
   if (clock > lc) { // a gap: pending (not on the device)
     cp_unsup(D, CU_GAP);
     return -1;
   }
-  Cur r{D.p, 0xFFFFFFFFu, bpos + 1u}; // validated by walk_update
+  Cur r{D.up, 0xFFFFFFFFu, bpos + 1u}; // validated by walk_update
   bool cn;
   uint32_t fl = 0, oc = 0, ok = 0, rc = 0, rk = 0;
   if (info != 0) {
@@ -659,14 +663,14 @@ __device__ int cp_block(CDoc &D, const uint32_t *ub, uint32_t &dep) {
     uint32_t nl;
     rd_var_u32(r, nl, cn);
     for (uint32_t q = 0; q < D.nroot && root < 0; q++)
-      if (D.m[M_ROOTLEN + q] == nl && bytes_eq(D.p + D.m[M_ROOTOFF + q], D.p + r.i, nl)) root = (int)q;
+      if (D.m[M_ROOTLEN + q] == nl && bytes_eq(D.p + D.m[M_ROOTOFF + q], D.up + r.i, nl)) root = (int)q;
     if (root < 0) { // Store::get_or_create_type
       if (D.nroot == CP_MAXROOT) {
         cp_unsup(D, CU_ROOTS);
         return -1;
       }
       root = (int)D.nroot++;
-      D.m[M_ROOTOFF + root] = r.i;
+      D.m[M_ROOTOFF + root] = D.uoff + r.i;
       D.m[M_ROOTLEN + root] = nl;
       D.m[M_ROOTSTART + root] = CNIL;
     }
@@ -681,7 +685,7 @@ __device__ int cp_block(CDoc &D, const uint32_t *ub, uint32_t &dep) {
   } else { // String: one segment over the update's bytes
     uint32_t sl;
     rd_var_u32(r, sl, cn);
-    const uint32_t s = cp_new_seg(D, r.i, sl);
+    const uint32_t s = cp_new_seg(D, D.uoff + r.i, sl | (sl == len ? SEG_ASCII : 0u));
     if (s == CNIL) return -1;
     D.I(x, I_SEG0) = D.I(x, I_SEG1) = s;
   }
@@ -755,6 +759,33 @@ __device__ void cp_apply_delete(CDoc &D, uint32_t nent) {
 }
 
 // ------------------------------------------------------------------ encode (store.rs:204-232)
+// Output writer bounded by the document's slot; string bytes move 16 at a time (the loads of a
+// group issue together instead of one load-store round trip per byte)
+struct CpWriter {
+  uint8_t *p;
+  uint64_t n, cap;
+  __device__ __forceinline__ void u8(uint8_t b) {
+    if (n < cap) p[n] = b;
+    n++;
+  }
+  __device__ void bytes(const uint8_t *s, uint32_t k) {
+    if (n + k > cap) {
+      n += k;
+      return;
+    }
+    uint8_t *d = p + n;
+    uint32_t i = 0;
+    for (; i + 16 <= k; i += 16) {
+      uint8_t t[16];
+#pragma unroll
+      for (int j = 0; j < 16; j++) t[j] = s[i + j];
+#pragma unroll
+      for (int j = 0; j < 16; j++) d[i + j] = t[j];
+    }
+    for (; i < k; i++) d[i] = s[i];
+    n += k;
+  }
+};
 template <class W> __device__ void cp_encode(CDoc &D, W &w) {
   // clients with blocks, descending
   uint32_t ord[CP_MAXCL], n = 0;
@@ -800,9 +831,10 @@ template <class W> __device__ void cp_encode(CDoc &D, W &w) {
         w_var(w, D.I(x, I_LEN));
       } else {
         uint32_t tb = 0;
-        for (uint32_t s = D.I(x, I_SEG0); s != CNIL; s = D.sg[3 * s + 2]) tb += D.sg[3 * s + 1];
+        for (uint32_t s = D.I(x, I_SEG0); s != CNIL; s = D.sg[3 * s + 2]) tb += D.sg[3 * s + 1] & SEG_LEN;
         w_var(w, tb);
-        for (uint32_t s = D.I(x, I_SEG0); s != CNIL; s = D.sg[3 * s + 2]) w.bytes(D.p + D.sg[3 * s], D.sg[3 * s + 1]);
+        for (uint32_t s = D.I(x, I_SEG0); s != CNIL; s = D.sg[3 * s + 2])
+          w.bytes(D.p + D.sg[3 * s], D.sg[3 * s + 1] & SEG_LEN);
       }
     }
   }
@@ -856,7 +888,7 @@ template <class W> __device__ void cp_encode(CDoc &D, W &w) {
 // ------------------------------------------------------------------ the kernel
 // document d of the batch (the kernel's lane body; tools/hostemu runs it on the CPU too)
 __device__ void compact_doc(const BatchIn &b, const FastOut &o, uint32_t *hdr, const uint64_t *scr_off,
-                            uint32_t *scr, uint32_t d) {
+                            uint32_t *scr, uint32_t d, uint8_t *stage, uint32_t *misc) {
   uint64_t u0 = b.doc_upd[d], u1 = b.doc_upd[d + 1];
   const uint64_t B0 = b.upd_off[u0], B1 = b.upd_off[u1];
   const uint64_t slot = 2 * B0 + 64ull * d, cap = 2 * (B1 - B0) + 64;
@@ -869,6 +901,16 @@ __device__ void compact_doc(const BatchIn &b, const FastOut &o, uint32_t *hdr, c
   D.st = 0;
   D.why = 0;
   int status = 0;
+  // diagnostic (env YMERGE_STAMPS): s_memtime sums per phase -> o.stamps[16 d + k]:
+  // 0 decode, 1 integrate, 2 apply_delete, 3 commit, 4 encode, 5 updates
+  uint64_t tph[6] = {0, 0, 0, 0, 0, 0}, tq = o.stamps ? __builtin_amdgcn_s_memtime() : 0;
+  auto lap = [&](int k) {
+    if (o.stamps) {
+      const uint64_t now = __builtin_amdgcn_s_memtime();
+      tph[k] += now - tq;
+      tq = now;
+    }
+  };
   if (h[H_OVER]) { // more than 8 block clients / document bytes over 2^31
     status = E_UNSUPPORTED;
     D.why = h[H_OVER];
@@ -880,14 +922,18 @@ __device__ void compact_doc(const BatchIn &b, const FastOut &o, uint32_t *hdr, c
   D.cap_i = D.cap_s = 3 * h[H_NB] + 2 * h[H_NR] + 64;
   D.mB = h[H_MB];
   D.mR = h[H_MR];
-  D.m = base;
+  D.m = misc ? misc : base; // the client table etc. in the lane's LDS words when given
   D.it = base + 1024;
   D.sg = D.it + (size_t)D.cap_i * I_W;
   D.cb = D.sg + (size_t)D.cap_s * 3;
   {
     uint32_t acc = 0; // arrival array offsets (pairs) after the counts
-    for (uint32_t k = 0; k < h[H_NCL]; k++) {
-      h[H_CO + k] = acc;
+    const uint32_t hn = h[H_NCL];
+    D.m[M_HNCL] = hn;
+    for (uint32_t k = 0; k < hn; k++) {
+      D.m[M_HCL + k] = h[H_CL + k];
+      D.m[M_HCN + k] = h[H_CN + k];
+      D.m[M_HCO + k] = acc;
       acc += h[H_CN + k];
     }
     D.ubr = D.cb + 2ull * (acc + 8);
@@ -902,8 +948,25 @@ __device__ void compact_doc(const BatchIn &b, const FastOut &o, uint32_t *hdr, c
     for (uint32_t c = 0; c < D.ncl; c++) D.m[M_BEFORE + c] = cp_clock(D, (int)c);
     D.nub = D.nur = D.nt = D.nm = 0;
     const uint64_t a = b.upd_off[u], z = b.upd_off[u + 1];
-    CpSink sk{&D, D.p, 0, 0, 0, false};
-    const int e = walk_update(b.bytes + a, (uint32_t)(z - a), sk);
+    const uint32_t ulen = (uint32_t)(z - a);
+    D.uoff = (uint32_t)(a - B0);
+    D.up = b.bytes + a;
+    if (stage && ulen + 4 <= CP_STAGE) { // the update into this lane's LDS stage, aligned dwords
+      const uint64_t a4 = a & ~3ull;
+      const uint32_t *src = (const uint32_t *)(b.bytes + a4), nd = (uint32_t)((a - a4) + ulen + 3) >> 2;
+      uint32_t *dst = (uint32_t *)stage;
+      for (uint32_t k = 0; k < nd; k += 8) {
+        uint32_t t[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) t[j] = k + j < nd ? src[k + j] : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++)
+          if (k + j < nd) dst[k + j] = t[j];
+      }
+      D.up = stage + (a - a4);
+    }
+    CpSink sk{&D, D.up, 0, 0, 0, false};
+    const int e = walk_update(D.up, ulen, sk);
     if (e) {
       status = e;
       break;
@@ -912,6 +975,8 @@ __device__ void compact_doc(const BatchIn &b, const FastOut &o, uint32_t *hdr, c
       status = E_UNSUPPORTED, D.why = CU_UPDATE_SHAPE;
       break;
     }
+    lap(0);
+    tph[5]++;
     // Update::integrate order (update.rs:169-262): per-client queues by client descending
     // (a client's sections keep their stream order), blocks in order; a block whose
     // dependency on another client is missing waits on a stack while that client's queue runs
@@ -957,7 +1022,7 @@ __device__ void compact_doc(const BatchIn &b, const FastOut &o, uint32_t *hdr, c
       uint32_t *t = D.ub + 4 * qe[q]++;
       t[0] = D.ubr[4 * i];
       t[1] = D.ubr[4 * i + 1];
-      t[2] = D.ubr[4 * i + 2] + (uint32_t)(a - B0);
+      t[2] = D.ubr[4 * i + 2];
       t[3] = D.ubr[4 * i + 3];
     }
     if (D.nub) {
@@ -987,21 +1052,23 @@ __device__ void compact_doc(const BatchIn &b, const FastOut &o, uint32_t *hdr, c
         }
       }
     }
+    lap(1);
     if (!D.st) cp_apply_delete(D, sk.nent);
+    lap(2);
     if (!D.st) cp_commit(D);
+    lap(3);
     status = D.st;
   }
   uint64_t olen = 0;
-  if (!status) {
-    Counter cnt;
-    cp_encode(D, cnt);
-    if (cnt.n > cap) status = E_UNSUPPORTED, D.why = CU_OUTPUT;
-    else {
-      Writer w{o.out + slot, 0};
-      cp_encode(D, w);
-      olen = w.n;
-    }
+  if (!status) { // one pass into the slot, bounded by its capacity
+    CpWriter w{o.out + slot, 0, cap};
+    cp_encode(D, w);
+    if (w.n > cap) status = E_UNSUPPORTED, D.why = CU_OUTPUT;
+    olen = w.n;
   }
+  lap(4);
+  if (o.stamps)
+    for (int k = 0; k < 6; k++) o.stamps[(size_t)d * 16 + k] = tph[k];
   o.status[d] = (uint8_t)status;
   if (o.path) o.path[d] = (uint8_t)(status == E_UNSUPPORTED ? D.why : 0);
   o.out_start[d] = slot;
@@ -1012,9 +1079,12 @@ __device__ void compact_doc(const BatchIn &b, const FastOut &o, uint32_t *hdr, c
 // less divergence and more waves in flight on a latency-bound, branchy lane body
 __global__ void __launch_bounds__(64) k_compact(BatchIn b, FastOut o, uint32_t *hdr, const uint64_t *scr_off,
                                                  uint32_t *scr, uint32_t lpw) {
+  __shared__ __align__(16) uint8_t stage[64 * CP_STAGE];
+  __shared__ uint32_t misc[64 * M_END];
   ym_set_grammar(0);
   const uint32_t d = blockIdx.x * lpw + threadIdx.x;
-  if (threadIdx.x < lpw && d < b.n_docs) compact_doc(b, o, hdr, scr_off, scr, d);
+  if (threadIdx.x < lpw && d < b.n_docs)
+    compact_doc(b, o, hdr, scr_off, scr, d, stage + threadIdx.x * CP_STAGE, misc + threadIdx.x * M_END);
 }
 
 // ------------------------------------------------------------------ counts (scratch sizing)

@@ -70,7 +70,7 @@ struct ymerge_ctx {
   int fast_threads = 256;
   bool lean = true; // k_lean first (env YMERGE_LEAN=0: every document through k_decode + k_fast_merge)
   bool pack_stale = false; // pack_off not computed for the last merge (all documents on k_lean)
-  uint32_t compact_lpw = 64; // k_compact documents per wavefront (env YMERGE_COMPACT_LPW)
+  uint32_t compact_lpw = 16; // k_compact documents per wavefront (env YMERGE_COMPACT_LPW; C2: 16 best)
   // host staging: two pinned buffers (double-buffered H2D / D2H of caller memory)
   uint8_t *stage[2] = {nullptr, nullptr};
   hipEvent_t stage_ev[2] = {nullptr, nullptr};
@@ -587,6 +587,12 @@ static int compact_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_byte
   ym::BatchIn b{d_bytes, d_upd_off, d_doc_upd, n, nullptr, nullptr};
   ym::FastOut fo{c->arena.as<uint8_t>(), c->out_start.as<uint64_t>(), c->out_len.as<uint64_t>(),
                  c->status.as<uint8_t>(), c->path.as<uint8_t>(), nullptr, nullptr, nullptr};
+  if (c->want_stamps) { // diagnostic: per-document phase cycles (ycompact.hip)
+    if (!c->stamps.ensure(nn * 16 * 8)) return YMERGE_ERR_DEVICE;
+    hipMemsetAsync(c->stamps.p, 0, nn * 16 * 8, c->s);
+    fo.stamps = c->stamps.as<uint64_t>();
+    c->stamps_docs = n_docs;
+  }
   hipEventRecord(c->ev[0], c->s);
   // per-document scratch from the counts (blocks, ranges, clients), then the store pass
   ym::launch_compact_count(b, c->counts.as<uint32_t>(), c->need.as<uint64_t>(), c->s);
