@@ -91,6 +91,8 @@ typedef struct {
   float ms_tiny;      /* merge: exact-engine stage time when it ran tiny documents only */
   uint64_t docs_lean; /* merge: documents written by k_lean (one wavefront each; not in docs_fast) */
   float ms_lean;      /* merge: k_lean (ms_decode / ms_fast then time the documents it handed over) */
+  uint64_t docs_giant; /* merge: of docs_big, long single-client documents merged by the grid-wide
+                          kernels of ygiant.hip instead of one tiled workgroup */
 } ymerge_stats;
 
 /* Device-resident result, owned by the context, valid until the next batch.

@@ -1,0 +1,253 @@
+// ygiant.hip — merge_updates_v1 of one very long single-client document across the whole GPU.
+//
+// A document of ~10^5 updates (the automerge-paper trace: 259,778 per-op updates) is a
+// single unit of work for every per-document kernel: the tiled kernel runs it on one CU.  When
+// the document is the shape of one author's log — every block and every DeleteSet entry of one
+// client, the blocks contiguous in clock in update order, each block canonical — yrs' merge
+// (update.rs:537-704) writes that client's blocks in update order behind one section header,
+// and the DeleteSet union of one client's ranges (id_set.rs:129-164).  That output is built
+// here by grid-wide kernels over the k_decode records, with no per-document serial phase:
+//   k_gs_pre    lane per update: blocks / ranges / bytes / clock lengths, shape checks
+//   (scans)     block and range counts, block bytes, clock lengths (k_scan)
+//   k_gs_write  lane per update: the clock-contiguity check, block bytes copied to their
+//               scanned offsets, deleted ranges set in a bitmap over the clock space
+//   k_gs_runs   lane per bitmap word: run starts (a run = one squashed DeleteSet range:
+//               union of overlapping and adjacent ranges, as IdRange::squash merges them)
+//   (scan)      run offsets
+//   k_gs_comp   lane per word: each run's start and length, its varint bytes
+//   (scan)      range byte offsets
+//   k_gs_ds     lane per run: the (start, length) varints
+//   k_gs_final  section header, DeleteSet header, length / status / path of the document.
+// Documents outside the shape keep path 2 and go to the tiled kernel as before.
+#include "ycodec.h"
+#include "ykernels.h"
+
+namespace ym {
+
+enum : uint32_t { GS_BAD = 0, GS_CMIN, GS_CMAX, GS_MAXEND, GS_FIRST = 4 /* u64 at words 4-5 */, GS_WORDS = 8 };
+enum : uint32_t {
+  GSB_SLOW = 1,      // an update k_decode did not decode (exact walk needed)
+  GSB_BLOCK = 2,     // a block that is not copied verbatim (re-encoded / panics)
+  GSB_DS = 4,        // a DeleteSet shape outside the path (several entries, empty range)
+  GSB_GAP = 8,       // blocks not contiguous in clock in update order
+  GSB_RANGE = 16     // a deleted range beyond the bitmap
+};
+
+__device__ __forceinline__ void gs_rec(const GsArgs &a, uint32_t i, uint32_t w[6]) {
+  const uint2 *rp = (const uint2 *)(a.rec + (size_t)(a.u0 + i) * REC_WORDS);
+  const uint2 x0 = rp[0], x1 = rp[1], x2 = rp[2];
+  w[0] = x0.x;
+  w[1] = x0.y;
+  w[2] = x1.x;
+  w[3] = x1.y;
+  w[4] = x2.x;
+  w[5] = x2.y;
+}
+
+// per-update blocks / ranges; calls blk(client, clock, len, pos, meta) and rng(client, s, e)
+template <class FB, class FR>
+__device__ __forceinline__ uint32_t gs_visit(const GsArgs &a, uint32_t i, FB blk, FR rng) {
+  uint32_t w[6];
+  gs_rec(a, i, w);
+  if (w[0] & (REC_SLOW | 0xFF)) return GSB_SLOW;
+  const uint32_t shape = (w[0] >> 10) & 3;
+  if (shape == REC_BLOCK) {
+    blk(w[1], w[2], w[3], w[4], w[5]);
+  } else if (shape == REC_DS) {
+    const uint32_t nr = (w[0] >> 12) & 3;
+    if (nr > 0) rng(w[1], w[2], w[3]);
+    if (nr > 1) rng(w[1], w[4], w[5]);
+  } else if (shape == REC_COMPLEX) {
+    if (!(w[0] & REC_OVF)) return GSB_SLOW;
+    const uint32_t nb = w[1], ne = w[2], nr = w[3];
+    if (ne > 1) return GSB_DS;
+    const uint32_t *ov = a.ovf + w[4];
+    for (uint32_t k = 0; k < nb; k++) blk(ov[5 * k], ov[5 * k + 1], ov[5 * k + 2], ov[5 * k + 3], ov[5 * k + 4]);
+    const uint32_t *rv = ov + 5 * nb + 2 * ne;
+    for (uint32_t k = 0; k < nr; k++) rng(ov[5 * nb], rv[3 * k], rv[3 * k + 1]);
+  }
+  return 0;
+}
+
+__global__ void __launch_bounds__(256) k_gs_pre(GsArgs a) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.U) return;
+  uint32_t nb = 0, nr = 0, bad = 0, cmin = 0xFFFFFFFFu, cmax = 0, maxend = 0;
+  uint64_t bytes = 0, lens = 0, first = ~0ull;
+  bad |= gs_visit(
+      a, i,
+      [&](uint32_t c, uint32_t k, uint32_t len, uint32_t, uint32_t meta) {
+        if (meta & 12) bad |= GSB_BLOCK;
+        if (nb == 0) first = ((uint64_t)i << 32) | k;
+        nb++;
+        bytes += meta >> 8;
+        lens += len;
+        cmin = c < cmin ? c : cmin;
+        cmax = c > cmax ? c : cmax;
+      },
+      [&](uint32_t c, uint32_t s, uint32_t e) {
+        if (e <= s) bad |= GSB_DS;
+        nr++;
+        maxend = e > maxend ? e : maxend;
+        cmin = c < cmin ? c : cmin;
+        cmax = c > cmax ? c : cmax;
+      });
+  a.cnt[i] = nb | ((uint64_t)nr << 32);
+  a.bytes_[i] = bytes;
+  a.lens[i] = lens;
+  if (bad) atomicOr(&a.g[GS_BAD], bad);
+  if (nb || nr) {
+    atomicMin(&a.g[GS_CMIN], cmin);
+    atomicMax(&a.g[GS_CMAX], cmax);
+  }
+  if (nr) atomicMax(&a.g[GS_MAXEND], maxend);
+  if (nb) atomicMin((unsigned long long *)(a.g + GS_FIRST), (unsigned long long)first);
+}
+
+__device__ __forceinline__ uint32_t gs_hdr(const GsArgs &a) { // bytes of the one-section header
+  const uint32_t nbt = (uint32_t)a.s_cnt[a.U];
+  return varlen(1) + varlen(nbt) + varlen(a.g[GS_CMIN]) + varlen((uint32_t)*(const uint64_t *)(a.g + GS_FIRST));
+}
+
+__global__ void __launch_bounds__(256) k_gs_write(GsArgs a) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.U) return;
+  const uint32_t clock0 = (uint32_t)*(const uint64_t *)(a.g + GS_FIRST);
+  uint64_t expect = clock0 + a.s_lens[i];
+  uint8_t *dst = a.out + gs_hdr(a) + a.s_bytes[i];
+  const uint8_t *src = a.bytes + a.upd_off[a.u0 + i];
+  uint32_t bad = 0;
+  gs_visit(
+      a, i,
+      [&](uint32_t, uint32_t k, uint32_t len, uint32_t pos, uint32_t meta) {
+        if (k != expect) bad |= GSB_GAP;
+        expect += len;
+        const uint32_t n = meta >> 8;
+        for (uint32_t q = 0; q < n; q++) dst[q] = src[pos + q];
+        dst += n;
+      },
+      [&](uint32_t, uint32_t s, uint32_t e) {
+        if (e > a.nbits) {
+          bad |= GSB_RANGE;
+          return;
+        }
+        // bits [s, e): the partial end words and the whole words between them
+        const uint32_t w0 = s >> 5, w1 = (e - 1) >> 5;
+        const uint32_t m0 = 0xFFFFFFFFu << (s & 31), m1 = 0xFFFFFFFFu >> (31 - ((e - 1) & 31));
+        if (w0 == w1) {
+          atomicOr(&a.bm[w0], m0 & m1);
+        } else {
+          atomicOr(&a.bm[w0], m0);
+          for (uint32_t q = w0 + 1; q < w1; q++) atomicOr(&a.bm[q], 0xFFFFFFFFu);
+          atomicOr(&a.bm[w1], m1);
+        }
+      });
+  if (bad) atomicOr(&a.g[GS_BAD], bad);
+}
+
+__device__ __forceinline__ uint32_t gs_starts(const GsArgs &a, uint32_t j) {
+  const uint32_t w = a.bm[j], prev = j ? a.bm[j - 1] >> 31 : 0u;
+  return w & ~((w << 1) | prev);
+}
+
+__global__ void __launch_bounds__(256) k_gs_runs(GsArgs a) {
+  const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= a.nwords) return;
+  a.w_cnt[j] = a.g[GS_BAD] ? 0 : __popc(gs_starts(a, j));
+}
+
+__global__ void __launch_bounds__(256) k_gs_comp(GsArgs a) {
+  const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= a.nwords || a.g[GS_BAD]) return;
+  uint32_t st = gs_starts(a, j);
+  uint64_t k = a.w_scan[j];
+  while (st) {
+    const uint32_t b = __builtin_ctz(st);
+    st &= st - 1;
+    const uint32_t s = 32 * j + b;
+    // end: the first clear bit after s (the bitmap's last word is always clear)
+    uint32_t q = j, inv = ~a.bm[j] & (b == 31 ? 0u : 0xFFFFFFFFu << (b + 1));
+    while (!inv) inv = ~a.bm[++q];
+    const uint32_t e = 32 * q + __builtin_ctz(inv);
+    a.k_start[k] = s;
+    a.k_len[k] = e - s;
+    a.k_size[k] = varlen(s) + varlen(e - s);
+    k++;
+  }
+}
+
+__device__ __forceinline__ uint64_t gs_ds_base(const GsArgs &a) {
+  const uint32_t K = (uint32_t)a.w_scan[a.nwords];
+  return gs_hdr(a) + a.s_bytes[a.U] + (K ? varlen(1) + varlen(a.g[GS_CMIN]) + varlen(K) : varlen(0));
+}
+
+__global__ void __launch_bounds__(256) k_gs_ds(GsArgs a) {
+  const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+  if (a.g[GS_BAD] || k >= a.w_scan[a.nwords]) return;
+  Writer w{a.out + gs_ds_base(a) + a.k_off[k], 0};
+  w_var(w, a.k_start[k]);
+  w_var(w, a.k_len[k]);
+}
+
+__global__ void k_gs_final(GsArgs a, FastOut o) {
+  if (threadIdx.x || a.g[GS_BAD]) return;
+  const uint32_t K = (uint32_t)a.w_scan[a.nwords];
+  const uint64_t total = gs_ds_base(a) + a.k_off[K];
+  if (total > a.cap) return; // (cannot happen: verbatim blocks + squashed ranges) tiled kernel
+  Writer w{a.out, 0};
+  w_var(w, 1);
+  w_var(w, (uint32_t)a.s_cnt[a.U]);
+  w_var(w, a.g[GS_CMIN]);
+  w_var(w, (uint32_t)*(const uint64_t *)(a.g + GS_FIRST));
+  Writer v{a.out + gs_hdr(a) + a.s_bytes[a.U], 0};
+  if (K) {
+    w_var(v, 1);
+    w_var(v, a.g[GS_CMIN]);
+    w_var(v, K);
+  } else {
+    w_var(v, 0);
+  }
+  o.out_len[a.d] = total;
+  o.status[a.d] = 0;
+  o.path[a.d] = 0; // written: the tiled kernel skips it
+  atomicAdd(&o.npath[14], 1u);
+}
+
+// documents the tiled kernel would take (path 2) with at least min_u updates: list[0] =
+// count, then (document, updates, ranges, first update, first byte, bytes) for up to GS_LIST
+__global__ void k_gs_find(BatchIn b, const uint8_t *path, const uint32_t *counts, uint32_t min_u, uint64_t *list) {
+  const uint32_t d = blockIdx.x * 256 + threadIdx.x;
+  if (d >= b.n_docs || path[d] != 2) return;
+  const uint64_t u0 = b.doc_upd[d], u1 = b.doc_upd[d + 1];
+  if (u1 - u0 < min_u || u1 - u0 >= (1ull << 31)) return;
+  const uint64_t k = atomicAdd((unsigned long long *)&list[0], 1ull);
+  if (k < GS_LIST) {
+    uint64_t *e = list + 1 + 6 * k;
+    e[0] = d;
+    e[1] = u1 - u0;
+    e[2] = counts[4 * d + 3];
+    e[3] = u0;
+    e[4] = b.upd_off[u0];
+    e[5] = b.upd_off[u1] - b.upd_off[u0];
+  }
+}
+
+void launch_gs_find(const BatchIn &b, const uint8_t *path, const uint32_t *counts, uint32_t min_u, uint64_t *list,
+                    hipStream_t s) {
+  if (!b.n_docs) return;
+  hipLaunchKernelGGL(k_gs_find, dim3((b.n_docs + 255) / 256), dim3(256), 0, s, b, path, counts, min_u, list);
+}
+void launch_gs_pre(const GsArgs &a, hipStream_t s) {
+  hipLaunchKernelGGL(k_gs_pre, dim3((a.U + 255) / 256), dim3(256), 0, s, a);
+}
+void launch_gs_rest(const GsArgs &a, const FastOut &o, uint32_t n_ranges, uint64_t *scan_tmp, hipStream_t s) {
+  hipLaunchKernelGGL(k_gs_write, dim3((a.U + 255) / 256), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_gs_runs, dim3((a.nwords + 255) / 256), dim3(256), 0, s, a);
+  launch_scan_u64(a.w_cnt, a.w_scan, a.nwords, scan_tmp, s);
+  hipLaunchKernelGGL(k_gs_comp, dim3((a.nwords + 255) / 256), dim3(256), 0, s, a);
+  launch_scan_u64(a.k_size, a.k_off, n_ranges + 1, scan_tmp, s);
+  hipLaunchKernelGGL(k_gs_ds, dim3((n_ranges + 256) / 256), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_gs_final, dim3(1), dim3(64), 0, s, a, o);
+}
+
+} // namespace ym

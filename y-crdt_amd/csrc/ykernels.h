@@ -61,6 +61,31 @@ inline uint64_t lean_scratch_words(uint64_t n_updates, uint64_t n_docs, uint64_t
   return 4 * n_updates + 64 * n_docs + n_bytes;
 }
 void launch_fast_merge(const BatchIn &b, const FastCaps &caps, const FastOut &o, int nt, hipStream_t s);
+// one long single-client document merged by grid-wide kernels (ygiant.hip)
+constexpr uint32_t GS_LIST = 16;     // such documents per batch (the rest: tiled kernel)
+constexpr uint32_t GS_MIN_U = 65536; // updates (env YMERGE_GIANT_MIN)
+struct GsArgs {
+  const uint8_t *bytes;
+  const uint64_t *upd_off;
+  const uint32_t *rec, *ovf;
+  uint64_t u0;
+  uint32_t U, d;
+  uint8_t *out; // the document's slot
+  uint64_t cap;
+  uint64_t *cnt, *bytes_, *lens;       // [U]: blocks | ranges << 32, block bytes, clock lengths
+  uint64_t *s_cnt, *s_bytes, *s_lens; // [U + 1] exclusive scans
+  uint32_t *g;                         // flags / client min, max / max range end / first block key
+  uint32_t *bm;                        // deleted-clock bitmap [nwords]
+  uint32_t nbits, nwords;
+  uint64_t *w_cnt, *w_scan;            // run starts per word, scan [nwords + 1]
+  uint32_t *k_start, *k_len;           // runs = squashed ranges
+  uint64_t *k_size, *k_off;
+};
+void launch_gs_find(const BatchIn &b, const uint8_t *path, const uint32_t *counts, uint32_t min_u, uint64_t *list,
+                    hipStream_t s);
+void launch_gs_pre(const GsArgs &a, hipStream_t s);
+void launch_gs_rest(const GsArgs &a, const FastOut &o, uint32_t n_ranges, uint64_t *scan_tmp, hipStream_t s);
+
 // store-based compaction (ycompact.hip): one lane per document applies its updates to a
 // device block store; documents outside the device shape get status E_UNSUPPORTED.
 // k_compact_count fills a 32-word header per document and its scratch words (need[d]);

@@ -57,6 +57,7 @@ struct ymerge_ctx {
   DevBuf in_bytes, in_upd_off, in_doc_upd, in_sv, in_sv_off, sync_off, sync_end, sync_st;
   DevBuf status, path, out_start, out_len, pack_off, counts, need, scr_off, scratch, sizes, spill_off, scan_tmp;
   DevBuf arena, packed, counter, stamps, plan_small, plan_big, rec, ovf, big_scratch, lean_scr, lean_tot, cscr;
+  DevBuf gs_list, gs1, gs2; // long single-client documents (ygiant.hip)
   // lib0 v2: v1x arena + offsets + per-update status, v2 output arena + sizes + offsets,
   // state-vector rest offsets + pre-status
   DevBuf v2x, v2x_sz, v2x_off, v2_ust, v2_out, v2_osz, v2_ooff, v2_svoff, v2_svend, v2_pre;
@@ -70,6 +71,7 @@ struct ymerge_ctx {
   int fast_threads = 256;
   bool lean = true; // k_lean first (env YMERGE_LEAN=0: every document through k_decode + k_fast_merge)
   bool pack_stale = false; // pack_off not computed for the last merge (all documents on k_lean)
+  uint32_t giant_min = ym::GS_MIN_U; // updates of a document for the grid-wide path (env YMERGE_GIANT_MIN, 0: off)
   uint32_t compact_lpw = 16; // k_compact documents per wavefront (env YMERGE_COMPACT_LPW; C2: 16 best)
   // host staging: two pinned buffers (double-buffered H2D / D2H of caller memory)
   uint8_t *stage[2] = {nullptr, nullptr};
@@ -97,6 +99,7 @@ static bool ctx_init(ymerge_ctx *c, int device) {
   if (const char *v = getenv("YMERGE_TINY")) c->caps.in_cap = (uint32_t)atoi(v); // 0: no tiny path
   if (const char *v = getenv("YMERGE_LEAN")) c->lean = atoi(v) != 0;
   if (const char *v = getenv("YMERGE_COMPACT_LPW")) c->compact_lpw = (uint32_t)atoi(v);
+  if (const char *v = getenv("YMERGE_GIANT_MIN")) c->giant_min = (uint32_t)atoi(v);
   // the fast kernel's LDS layout must fit one workgroup (160 KB on gfx950)
   int lds_max = 0;
   if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess) return false;
@@ -124,7 +127,7 @@ extern "C" void ymerge_ctx_destroy(ymerge_ctx *c) {
                     &c->sync_end, &c->sync_st, &c->rec, &c->ovf, &c->status, &c->path,
                     &c->out_start, &c->out_len, &c->pack_off, &c->counts, &c->need, &c->scr_off, &c->scratch,
                     &c->sizes, &c->spill_off, &c->scan_tmp, &c->arena, &c->packed, &c->counter, &c->stamps,
-                    &c->plan_small, &c->plan_big, &c->big_scratch, &c->lean_scr, &c->lean_tot, &c->cscr, &c->v2x, &c->v2x_sz, &c->v2x_off, &c->v2_ust,
+                    &c->plan_small, &c->plan_big, &c->big_scratch, &c->lean_scr, &c->lean_tot, &c->cscr, &c->gs_list, &c->gs1, &c->gs2, &c->v2x, &c->v2x_sz, &c->v2x_off, &c->v2_ust,
                     &c->v2_out, &c->v2_osz, &c->v2_ooff, &c->v2_svoff, &c->v2_svend, &c->v2_pre})
     b->release();
   if (c->h_pinned) hipHostFree(c->h_pinned);
@@ -249,6 +252,66 @@ static bool ensure_keep(ymerge_ctx *c, DevBuf &b, size_t bytes, size_t keep) {
   return true;
 }
 
+// One long single-client document over the whole GPU (ygiant.hip); leaves it on path 2 (tiled
+// kernel) when it is not that shape.  e = (document, updates, ranges, first update, first
+// byte, bytes) from k_gs_find.
+static int run_giant(ymerge_ctx *c, const ym::BatchIn &b, const ym::FastOut &fo, const uint64_t *e) {
+  const uint32_t d = (uint32_t)e[0], U = (uint32_t)e[1], NR = (uint32_t)e[2];
+  ym::GsArgs a{};
+  a.bytes = b.bytes;
+  a.upd_off = b.upd_off;
+  a.rec = b.rec;
+  a.ovf = b.ovf;
+  a.u0 = e[3];
+  a.U = U;
+  a.d = d;
+  a.out = fo.out + 2 * e[4] + 64ull * d;
+  a.cap = 2 * e[5] + 64;
+  const size_t nu = (size_t)U + 1;
+  if (!c->gs1.ensure((6 * nu + 4) * 8) ||
+      !c->scan_tmp.ensure(ym::scan_tmp_elems((uint32_t)std::max<size_t>(nu, NR + 2)) * 8 + 64))
+    return YMERGE_ERR_DEVICE;
+  uint64_t *w = c->gs1.as<uint64_t>();
+  a.cnt = w;
+  a.bytes_ = w + nu;
+  a.lens = w + 2 * nu;
+  a.s_cnt = w + 3 * nu;
+  a.s_bytes = w + 4 * nu;
+  a.s_lens = w + 5 * nu;
+  a.g = (uint32_t *)(w + 6 * nu);
+  hipMemsetAsync(a.g, 0, 32, c->s);
+  hipMemsetAsync(a.g + 1, 0xFF, 4, c->s);  // client min
+  hipMemsetAsync(a.g + 4, 0xFF, 8, c->s);  // first block key
+  ym::launch_gs_pre(a, c->s);
+  ym::launch_scan_u64(a.cnt, a.s_cnt, U, c->scan_tmp.as<uint64_t>(), c->s);
+  ym::launch_scan_u64(a.bytes_, a.s_bytes, U, c->scan_tmp.as<uint64_t>(), c->s);
+  ym::launch_scan_u64(a.lens, a.s_lens, U, c->scan_tmp.as<uint64_t>(), c->s);
+  uint64_t *hp = c->h_pinned + 64; // flags, client min / max, max range end, first key, block count
+  hipMemcpyAsync(hp, a.g, 32, hipMemcpyDeviceToHost, c->s);
+  hipMemcpyAsync(hp + 4, a.s_cnt + U, 8, hipMemcpyDeviceToHost, c->s);
+  if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
+  const uint32_t *g = (const uint32_t *)hp;
+  const uint32_t nb_total = (uint32_t)(hp[4] & 0xFFFFFFFFu);
+  if (g[0] || g[1] != g[2] || nb_total == 0) return 0; // not the shape: tiled kernel
+  a.nbits = g[3];
+  a.nwords = a.nbits / 32 + 2; // the last word stays clear (run ends)
+  const size_t nw = a.nwords;
+  if (!c->gs2.ensure(nw * 4 + (2 * nw + 1) * 8 + 2 * ((size_t)NR + 2) * 4 + 2 * ((size_t)NR + 2) * 8 + 64) ||
+      !c->scan_tmp.ensure(ym::scan_tmp_elems((uint32_t)std::max<size_t>(nw, NR + 2)) * 8 + 64))
+    return YMERGE_ERR_DEVICE;
+  uint8_t *q = c->gs2.as<uint8_t>();
+  a.w_cnt = (uint64_t *)q;
+  a.w_scan = a.w_cnt + nw;
+  a.k_size = a.w_scan + nw + 1;
+  a.k_off = a.k_size + NR + 2;
+  a.bm = (uint32_t *)(a.k_off + NR + 2);
+  a.k_start = a.bm + nw;
+  a.k_len = a.k_start + NR + 2;
+  hipMemsetAsync(a.bm, 0, nw * 4, c->s);
+  ym::launch_gs_rest(a, fo, NR, c->scan_tmp.as<uint64_t>(), c->s);
+  return hipGetLastError() == hipSuccess ? 0 : YMERGE_ERR_DEVICE;
+}
+
 // One batch: fast path for every document, exact engine for the documents it hands over.
 static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes, const uint64_t *d_upd_off,
                         uint64_t n_updates, const uint64_t *d_doc_upd, uint64_t n_docs, ymerge_device_result *res) {
@@ -352,8 +415,26 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     ym::launch_scan_u64(c->need.as<uint64_t>(), c->scr_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
     hipMemcpyAsync(c->h_pinned + 10, c->scr_off.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, c->s);
     hipMemcpyAsync(c->h_pinned + 11, c->counter.as<uint32_t>() + 2, 4, hipMemcpyDeviceToHost, c->s);
+    // long documents for the grid-wide single-client path, listed in the same sync
+    const bool giant = c->giant_min && n_updates >= c->giant_min && !c->want_stamps;
+    constexpr size_t GSL = 1 + 6 * ym::GS_LIST;
+    if (giant) {
+      if (!c->gs_list.ensure(GSL * 8)) return YMERGE_ERR_DEVICE;
+      hipMemsetAsync(c->gs_list.p, 0, 8, c->s);
+      ym::launch_gs_find(b, path, c->counts.as<uint32_t>(), c->giant_min, c->gs_list.as<uint64_t>(), c->s);
+      hipMemcpyAsync(c->h_pinned + 128, c->gs_list.p, GSL * 8, hipMemcpyDeviceToHost, c->s);
+    }
     if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
     n_big = (uint32_t)(c->h_pinned[11] & 0xFFFFFFFFu);
+    if (giant) {
+      uint64_t ent[GSL];
+      memcpy(ent, c->h_pinned + 128, sizeof ent);
+      const uint64_t ng = std::min<uint64_t>(ent[0], ym::GS_LIST);
+      for (uint64_t k = 0; k < ng; k++) {
+        const int rc = run_giant(c, b, fo, ent + 1 + 6 * k);
+        if (rc) return rc;
+      }
+    }
     if (n_big) {
       if (!c->big_scratch.ensure((size_t)c->h_pinned[10] * 4 + 64)) return YMERGE_ERR_DEVICE;
       ym::launch_big_merge(b, c->counts.as<uint32_t>(), c->scr_off.as<uint64_t>(), c->big_scratch.as<uint32_t>(), fo,
@@ -364,7 +445,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   hipEventRecord(c->ev[1], c->s);
   // exact engine for documents the fast or tiled path handed over (path == 1)
   uint64_t words = 0;
-  uint32_t n_exact = 0, n_overlap = 0, n_tiny = 0;
+  uint32_t n_exact = 0, n_overlap = 0, n_tiny = 0, n_giant = 0;
   if (n_p1 || n_p2) {
     ym::launch_seq_count(b, path, status, c->counts.as<uint32_t>(), c->need.as<uint64_t>(), c->counter.as<uint32_t>(),
                          c->s);
@@ -372,12 +453,14 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     hipMemcpyAsync(c->h_pinned + 8, c->scr_off.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, c->s);
     hipMemcpyAsync(c->h_pinned + 9, c->counter.p, 4, hipMemcpyDeviceToHost, c->s);
     hipMemcpyAsync(c->h_pinned + 14, c->counter.as<uint32_t>() + 7, 12, hipMemcpyDeviceToHost, c->s);
+    hipMemcpyAsync(c->h_pinned + 17, c->counter.as<uint32_t>() + 18, 4, hipMemcpyDeviceToHost, c->s); // npath[14]
     if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
     words = c->h_pinned[8];
     n_exact = (uint32_t)(c->h_pinned[9] & 0xFFFFFFFFu);
     n_overlap = (uint32_t)(c->h_pinned[14] & 0xFFFFFFFFu);
     n_big -= (uint32_t)(c->h_pinned[14] >> 32); // tiled-kernel documents handed to the exact engine
     n_tiny = (uint32_t)(c->h_pinned[15] & 0xFFFFFFFFu);
+    n_giant = (uint32_t)(c->h_pinned[17] & 0xFFFFFFFFu);
   }
   if (n_exact) {
     if (!c->scratch.ensure((size_t)words * 4 + 64)) return YMERGE_ERR_DEVICE;
@@ -428,6 +511,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   c->stats.ms_tiny = n_exact == n_tiny ? t12 : 0.0f;
   c->stats.docs_big = n_big;
   c->stats.docs_overlap = n_overlap;
+  c->stats.docs_giant = n_giant;
   c->stats.docs_fast = n_docs - n_exact - n_big - c->stats.docs_lean;
   c->stats.ms_big = t61;
   c->stats.ms_fast = t01;
