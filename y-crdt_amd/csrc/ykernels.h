@@ -16,6 +16,7 @@ struct BatchIn {
   const uint32_t *ovf; // their overflow words (DEC_OVF per decode workgroup)
   uint32_t v1x = 0;    // bytes are the internal v1x grammar (lib0 v2 path), not lib0 v1
   uint32_t only_path3 = 0; // k_fast_merge: only the documents k_lean handed over (path == 3)
+  const uint32_t *order = nullptr; // k_lean: wavefront -> document (long documents first), or identity
 };
 
 // Per-update decode record written by k_decode (one lane per update over the whole
@@ -57,6 +58,10 @@ size_t fast_lds_bytes(const FastCaps &c);
 // scr: HBM scratch of lean_scratch_words(...) u32 for documents above the LDS arena (null:
 // those are handed over)
 void launch_lean(const BatchIn &b, const FastOut &o, uint32_t *scr, hipStream_t s);
+// k_lean dispatch order for skewed batches: documents by update-count class, longest class
+// first (longest-processing-time-first: a long document starts early instead of ending the
+// kernel).  ctr: 8 zeroed words.
+void launch_lean_order(const uint64_t *doc_upd, uint32_t n_docs, uint32_t *ctr, uint32_t *order, hipStream_t s);
 inline uint64_t lean_scratch_words(uint64_t n_updates, uint64_t n_docs, uint64_t n_bytes) {
   return 4 * n_updates + 64 * n_docs + n_bytes;
 }

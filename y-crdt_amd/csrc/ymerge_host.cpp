@@ -58,6 +58,7 @@ struct ymerge_ctx {
   DevBuf status, path, out_start, out_len, pack_off, counts, need, scr_off, scratch, sizes, spill_off, scan_tmp;
   DevBuf arena, packed, counter, stamps, plan_small, plan_big, rec, ovf, big_scratch, lean_scr, lean_tot, cscr;
   DevBuf gs_list, gs1, gs2; // long single-client documents (ygiant.hip)
+  DevBuf lean_ord;          // k_lean dispatch order: 8 counters, then n_docs document indices
   // lib0 v2: v1x arena + offsets + per-update status, v2 output arena + sizes + offsets,
   // state-vector rest offsets + pre-status
   DevBuf v2x, v2x_sz, v2x_off, v2_ust, v2_out, v2_osz, v2_ooff, v2_svoff, v2_svend, v2_pre;
@@ -72,6 +73,7 @@ struct ymerge_ctx {
   bool lean = true; // k_lean first (env YMERGE_LEAN=0: every document through k_decode + k_fast_merge)
   bool pack_stale = false; // pack_off not computed for the last merge (all documents on k_lean)
   uint32_t giant_min = ym::GS_MIN_U; // updates of a document for the grid-wide path (env YMERGE_GIANT_MIN, 0: off)
+  int lean_order = -1; // k_lean longest-first dispatch: env YMERGE_LEAN_ORDER 0/1, default n_docs >= 65536
   uint32_t compact_lpw = 16; // k_compact documents per wavefront (env YMERGE_COMPACT_LPW; C2: 16 best)
   // host staging: two pinned buffers (double-buffered H2D / D2H of caller memory)
   uint8_t *stage[2] = {nullptr, nullptr};
@@ -100,6 +102,7 @@ static bool ctx_init(ymerge_ctx *c, int device) {
   if (const char *v = getenv("YMERGE_LEAN")) c->lean = atoi(v) != 0;
   if (const char *v = getenv("YMERGE_COMPACT_LPW")) c->compact_lpw = (uint32_t)atoi(v);
   if (const char *v = getenv("YMERGE_GIANT_MIN")) c->giant_min = (uint32_t)atoi(v);
+  if (const char *v = getenv("YMERGE_LEAN_ORDER")) c->lean_order = atoi(v);
   // the fast kernel's LDS layout must fit one workgroup (160 KB on gfx950)
   int lds_max = 0;
   if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess) return false;
@@ -127,7 +130,7 @@ extern "C" void ymerge_ctx_destroy(ymerge_ctx *c) {
                     &c->sync_end, &c->sync_st, &c->rec, &c->ovf, &c->status, &c->path,
                     &c->out_start, &c->out_len, &c->pack_off, &c->counts, &c->need, &c->scr_off, &c->scratch,
                     &c->sizes, &c->spill_off, &c->scan_tmp, &c->arena, &c->packed, &c->counter, &c->stamps,
-                    &c->plan_small, &c->plan_big, &c->big_scratch, &c->lean_scr, &c->lean_tot, &c->cscr, &c->gs_list, &c->gs1, &c->gs2, &c->v2x, &c->v2x_sz, &c->v2x_off, &c->v2_ust,
+                    &c->plan_small, &c->plan_big, &c->big_scratch, &c->lean_scr, &c->lean_tot, &c->cscr, &c->gs_list, &c->gs1, &c->gs2, &c->lean_ord, &c->v2x, &c->v2x_sz, &c->v2x_off, &c->v2_ust,
                     &c->v2_out, &c->v2_osz, &c->v2_ooff, &c->v2_svoff, &c->v2_svend, &c->v2_pre})
     b->release();
   if (c->h_pinned) hipHostFree(c->h_pinned);
@@ -361,7 +364,16 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     if (!c->lean_tot.ensure(64 * 64)) return YMERGE_ERR_DEVICE;
     hipMemsetAsync(c->lean_tot.p, 0, 64 * 64, c->s);
     fo.lean_total = c->lean_tot.as<unsigned long long>();
-    ym::launch_lean(b, fo, lscr, c->s);
+    // large batches: long documents dispatched first (a skewed batch otherwise ends on the
+    // last long document to start)
+    ym::BatchIn bl = b;
+    if (c->lean_order == 1 || (c->lean_order < 0 && n >= 65536)) {
+      if (!c->lean_ord.ensure((size_t)n * 4 + 64)) return YMERGE_ERR_DEVICE;
+      hipMemsetAsync(c->lean_ord.p, 0, 32, c->s);
+      ym::launch_lean_order(d_doc_upd, n, c->lean_ord.as<uint32_t>(), c->lean_ord.as<uint32_t>() + 16, c->s);
+      bl.order = c->lean_ord.as<uint32_t>() + 16;
+    }
+    ym::launch_lean(bl, fo, lscr, c->s);
     if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
     // hand-over count and k_lean's output bytes (npath[6], the 64 partial sums) in one sync
     hipMemcpyAsync(c->h_pinned + 16, c->counter.as<uint32_t>() + 10, 4, hipMemcpyDeviceToHost, c->s);

@@ -1053,14 +1053,53 @@ __global__ void __launch_bounds__(64 * WPB, OCC) k_lean(BatchIn b, FastOut o, ui
   ym_set_grammar(b.v1x);
   const uint32_t lane = __lane_id();
   const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t d = blockIdx.x * WPB + w;
-  if (d >= b.n_docs) return;
+  const uint32_t slot = blockIdx.x * WPB + w;
+  if (slot >= b.n_docs) return;
+  const uint32_t d = b.order ? __builtin_amdgcn_readfirstlane(b.order[slot]) : slot;
   const uint64_t u0 = b.doc_upd[d], u1 = b.doc_upd[d + 1];
   const uint64_t nb = b.upd_off[u1] - b.upd_off[u0];
   if (scr && (u1 - u0 > LN_AW || nb >= 65536) && u1 - u0 <= LN_UMAX && nb < (1ull << 31))
     lean_doc<true, STAMPS>(b, o, lds[w], d, lane, scr);
   else
     lean_doc<false, STAMPS>(b, o, lds[w], d, lane, scr);
+}
+
+// update-count classes of the dispatch order (longest first)
+__device__ __forceinline__ uint32_t lean_class(uint64_t U) { return U > 2048 ? 0 : U > 512 ? 1 : U > 64 ? 2 : 3; }
+__global__ void __launch_bounds__(256) k_lean_order_count(const uint64_t *doc_upd, uint32_t n, uint32_t *ctr) {
+  __shared__ uint32_t c[4];
+  if (threadIdx.x < 4) c[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t d = blockIdx.x * 256 + threadIdx.x;
+  if (d < n) atomicAdd(&c[lean_class(doc_upd[d + 1] - doc_upd[d])], 1u);
+  __syncthreads();
+  if (threadIdx.x < 4 && c[threadIdx.x]) atomicAdd(&ctr[threadIdx.x], c[threadIdx.x]);
+}
+__global__ void __launch_bounds__(256) k_lean_order_place(const uint64_t *doc_upd, uint32_t n, uint32_t *ctr,
+                                                         uint32_t *order) {
+  __shared__ uint32_t c[4], base[4];
+  if (threadIdx.x < 4) c[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t d = blockIdx.x * 256 + threadIdx.x;
+  uint32_t k = 0, r = 0;
+  if (d < n) {
+    k = lean_class(doc_upd[d + 1] - doc_upd[d]);
+    r = atomicAdd(&c[k], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) { // this workgroup's run in its class: class start + claimed offset
+    uint32_t start = 0;
+    for (uint32_t q = 0; q < threadIdx.x; q++) start += ctr[q];
+    base[threadIdx.x] = c[threadIdx.x] ? start + atomicAdd(&ctr[4 + threadIdx.x], c[threadIdx.x]) : 0;
+  }
+  __syncthreads();
+  if (d < n) order[base[k] + r] = d;
+}
+void launch_lean_order(const uint64_t *doc_upd, uint32_t n_docs, uint32_t *ctr, uint32_t *order, hipStream_t s) {
+  if (!n_docs) return;
+  const dim3 g((n_docs + 255) / 256);
+  hipLaunchKernelGGL(k_lean_order_count, g, dim3(256), 0, s, doc_upd, n_docs, ctr);
+  hipLaunchKernelGGL(k_lean_order_place, g, dim3(256), 0, s, doc_upd, n_docs, ctr, order);
 }
 
 void launch_lean(const BatchIn &b, const FastOut &o, uint32_t *scr, hipStream_t s) {
