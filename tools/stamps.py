@@ -76,6 +76,26 @@ def main_compact(n, lpw):
         print(f"  {nm:12s} {v.mean():12.0f} cycles/doc {(v / upd).mean():8.0f} /update {100 * v.mean() / tot.mean():5.1f}%")
 
 
+def main_c5(n):
+    """k_plan_ring (diff planner) on C5-style documents (C2 merge outputs vs remote SVs)."""
+    b = workloads.text_docs(n, 1000)
+    e = ymerge.Engine(0)
+    out, off, st = e.merge_host(b.data, b.upd_off, b.doc_upd)
+    db = workloads.compacted_docs(out, off, sv_fn=lambda dd, oo: e.state_vector_host(dd, oo))
+    e.diff_host(db.data, db.upd_off, db.sv, db.sv_off)
+    L = ymerge.lib()
+    L.ymerge_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+    stt = np.zeros((n, 16), np.uint64)
+    assert L.ymerge_debug_stamps(e._ctx, n, stt.ctypes.data) == 0
+    ok = stt[:, 7] == 0xD1FF
+    s = stt[ok].astype(np.float64)
+    print(f"k_plan_ring docs {ok.sum()} of {n}, stats {e.stats()}")
+    print(f"  bytes/doc {s[:, 5].mean():.0f}; wave cycles: refill {s[:, 0].mean():.0f} ({s[:, 3].mean():.0f} rounds), "
+          f"steps {s[:, 1].mean():.0f} ({s[:, 4].mean():.0f} iterations), finish {s[:, 2].mean():.0f}")
+    print(f"  cycles per step iteration {(s[:, 1] / np.maximum(s[:, 4], 1)).mean():.0f}, "
+          f"per refill {(s[:, 0] / np.maximum(s[:, 3], 1)).mean():.0f}")
+
+
 def main_zipf(n):
     """Fast-path documents of a C3-style batch, phase cycles by update count."""
     b = workloads.zipf_docs(n, seed=0x5EED)
@@ -139,6 +159,8 @@ def main():
         return main_big(int(sys.argv[2]) if len(sys.argv) > 2 else 2000, "c4")
     if len(sys.argv) > 1 and sys.argv[1] == "c1":
         return main_c1()
+    if len(sys.argv) > 1 and sys.argv[1] == "c5":
+        return main_c5(int(sys.argv[2]) if len(sys.argv) > 2 else 20000)
     if len(sys.argv) > 1 and sys.argv[1] == "compact":
         return main_compact(int(sys.argv[2]) if len(sys.argv) > 2 else 10000, int(sys.argv[3]) if len(sys.argv) > 3 else 16)
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 2000

@@ -618,8 +618,11 @@ __global__ void __launch_bounds__(RING_NT) k_plan_ring(DiffBatch b, PlanScratch 
   RingRd R{row, (uint64_t)up, 0, 0, (uint64_t)up + un, un, F_OK};
   bool have = false, wait = false;
 
+  // diagnostic stamps (wave time): refill, steps, finish; refill rounds, step iterations
+  uint64_t t_ref = 0, t_stp = 0, n_ref = 0, n_stp = 0, tq = ps.stamps ? __builtin_amdgcn_s_memtime() : 0;
   for (;;) {
     if (!__any(active)) break;
+    if (ps.stamps) tq = __builtin_amdgcn_s_memtime();
     // ---- refill point: lanes that ran short, or are within 64 bytes of their ring's end
     const uint64_t a0 = R.sbase + pos;
     if (active && (!have || wait || (a0 + 64 > R.rb + RING && R.rb + RING < R.send))) {
@@ -643,9 +646,16 @@ __global__ void __launch_bounds__(RING_NT) k_plan_ring(DiffBatch b, PlanScratch 
         wait = false;
       }
     }
+    if (ps.stamps) {
+      const uint64_t now = __builtin_amdgcn_s_memtime();
+      t_ref += now - tq;
+      tq = now;
+      n_ref++;
+    }
     for (uint32_t step = 0; step < RING_STEPS; step++) {
       const bool can = active && !wait;
       if (!__any(can)) break;
+      if (ps.stamps) n_stp++;
       if (!can) continue;
       R.fail = F_OK;
       bool cn, sec_end = false, entry_end = false;
@@ -920,7 +930,9 @@ __global__ void __launch_bounds__(RING_NT) k_plan_ring(DiffBatch b, PlanScratch 
       }
       if (st == R_DONE) active = false;
     }
+    if (ps.stamps) t_stp += __builtin_amdgcn_s_memtime() - tq;
   }
+  const uint64_t tf0 = ps.stamps ? __builtin_amdgcn_s_memtime() : 0;
   // ---- after the walk (out of the step loop: the calls below do not hold its registers):
   // hash tables replayed in yrs' insertion order, re-encoded slice sizes, the output plan
   if (d >= b.n_docs) return;
@@ -961,6 +973,16 @@ __global__ void __launch_bounds__(RING_NT) k_plan_ring(DiffBatch b, PlanScratch 
     }
   }
   if (bail) ps.big[d] = PLAN_REDO;
+  if (ps.stamps) {
+    uint64_t *o = ps.stamps + (size_t)d * 16;
+    o[0] = t_ref;
+    o[1] = t_stp;
+    o[2] = __builtin_amdgcn_s_memtime() - tf0;
+    o[3] = n_ref;
+    o[4] = n_stp;
+    o[5] = un;
+    o[7] = 0xD1FF;
+  }
 }
 
 template <bool DIFF>

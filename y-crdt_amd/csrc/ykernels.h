@@ -158,6 +158,7 @@ struct PlanScratch {
   uint8_t *big, *status;
   uint64_t *size;
   uint32_t *n_big;
+  uint64_t *stamps = nullptr; // diagnostic (env YMERGE_STAMPS): k_plan_ring phase cycles, 16 per document
 };
 uint64_t plan_small_words();
 void launch_plan(bool diff, int pass, const DiffBatch &b, const PlanScratch &ps, hipStream_t s);

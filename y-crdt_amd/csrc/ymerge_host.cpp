@@ -585,6 +585,12 @@ static int plan_exec(ymerge_ctx *c, bool diff, const uint8_t *d_bytes, const uin
   ym::PlanScratch ps{c->plan_small.as<uint32_t>(), sw,       nullptr,
                      c->spill_off.as<uint64_t>(), c->path.as<uint8_t>(), c->status.as<uint8_t>(),
                      c->out_len.as<uint64_t>(),    c->counter.as<uint32_t>()};
+  if (c->want_stamps) { // diagnostic: k_plan_ring phase cycles
+    if (!c->stamps.ensure(nn * 16 * 8)) return YMERGE_ERR_DEVICE;
+    hipMemsetAsync(c->stamps.p, 0, nn * 16 * 8, c->s);
+    ps.stamps = c->stamps.as<uint64_t>();
+    c->stamps_docs = n_docs;
+  }
   hipMemsetAsync(c->counter.p, 0, 64, c->s);
   hipEventRecord(c->ev[0], c->s);
   ym::launch_plan(diff, 0, b, ps, c->s);
