@@ -519,20 +519,25 @@ struct RingRd {
   const uint32_t *row;
   uint64_t sbase, rb, rend, send;
   uint32_t un, fail;
+  int32_t rbq, rendq; // the ring's start and end relative to the update (32-bit hot path)
+  __device__ __forceinline__ void sync_rel() {
+    rbq = (int32_t)(int64_t)(rb - sbase);
+    rendq = (int32_t)(int64_t)(rend - sbase);
+  }
   __device__ __forceinline__ uint64_t at(uint32_t q) {
-    const uint64_t a = sbase + q;
     if (fail) return 0;
     if (q >= un) {
       fail = F_BAIL;
       return 0;
     }
-    if (a + 8 > rend && rend != send) {
+    if ((int32_t)q + 8 > rendq && rendq != (int32_t)un) {
       fail = F_SHORT;
       return 0;
     }
-    return ring_read8(row, (uint32_t)(a - rb));
+    return ring_read8(row, (uint32_t)((int32_t)q - rbq));
   }
-  // read_var_u32 (varint.rs:244-260, wrapping_shl) at q: bytes consumed
+  // read_var_u32 (varint.rs:244-260, wrapping_shl) at q: bytes consumed; canon = the
+  // re-encoding is the same bytes (no zero top group; a 5th byte below 16)
   __device__ __forceinline__ uint32_t var(uint32_t q, uint32_t &v, bool &canon) {
     const uint64_t x = at(q);
     const uint64_t m = ~x & 0x0000008080808080ull;
@@ -542,7 +547,8 @@ struct RingRd {
     const uint64_t xm = x & (nb >= 8 ? ~0ull : ((1ull << (8 * nb)) - 1));
     v = (uint32_t)((xm & 0x7F) | ((xm >> 1) & 0x3F80) | ((xm >> 2) & 0x1FC000) | ((xm >> 3) & 0xFE00000) |
                    ((xm >> 4) & 0x7F0000000ull));
-    canon = nb == varlen(v) && (nb != 5 || ((xm >> 32) & 0xFF) < 16);
+    const uint32_t last = (uint32_t)(xm >> (8 * (nb - 1))) & 0xFF;
+    canon = nb == 1 || (last != 0 && (nb < 5 || last < 16));
     return nb;
   }
 };
@@ -615,7 +621,7 @@ __global__ void __launch_bounds__(RING_NT) k_plan_ring(DiffBatch b, PlanScratch 
   // DeleteSet
   uint32_t nds = 0, ids = 0, dclient = 0, cpos = 0, nr = 0, kr = 0, prev_e = 0, dsz = 0;
   bool dcanon = true, dsq = true;
-  RingRd R{row, (uint64_t)up, 0, 0, (uint64_t)up + un, un, F_OK};
+  RingRd R{row, (uint64_t)up, 0, 0, (uint64_t)up + un, un, F_OK, 0, 0};
   bool have = false, wait = false;
 
   // diagnostic stamps (wave time): refill, steps, finish; refill rounds, step iterations
@@ -642,6 +648,7 @@ __global__ void __launch_bounds__(RING_NT) k_plan_ring(DiffBatch b, PlanScratch 
           for (uint32_t k = 0; k < 8; k++) dst[g + k] = x[k];
         }
         R.rend = R.rb + RING < R.send ? R.rb + RING : R.send;
+        R.sync_rel();
         have = true;
         wait = false;
       }
