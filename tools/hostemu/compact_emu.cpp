@@ -11,7 +11,8 @@ extern "C" void emu_compact_batch(const uint8_t *bytes, const uint64_t *upd_off,
   ym::ym_set_grammar(0);
   std::vector<uint32_t> hdr((size_t)n_docs * ym::CP_HDR + 1);
   std::vector<uint64_t> need(n_docs + 1), off(n_docs + 1, 0);
-  for (uint32_t d = 0; d < n_docs; d++) ym::compact_count_doc(b, hdr.data(), need.data(), d);
+  alignas(16) uint8_t cstage[ym::CP_STAGE];
+  for (uint32_t d = 0; d < n_docs; d++) ym::compact_count_doc(b, hdr.data(), need.data(), d, cstage);
   for (uint32_t d = 0; d < n_docs; d++) off[d + 1] = off[d] + need[d];
   std::vector<uint32_t> scr(off[n_docs] + 16);
   alignas(16) uint8_t stage[ym::CP_STAGE];

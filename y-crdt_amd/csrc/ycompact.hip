@@ -886,6 +886,24 @@ template <class W> __device__ void cp_encode(CDoc &D, W &w) {
 }
 
 // ------------------------------------------------------------------ the kernel
+// the update at byte a (ulen bytes) copied into this lane's LDS stage as aligned dwords (the
+// loads of a group issue together); the global bytes when it does not fit or there is no stage
+__device__ const uint8_t *cp_stage(const uint8_t *bytes, uint64_t a, uint32_t ulen, uint8_t *stage) {
+  if (!stage || ulen + 4 > CP_STAGE) return bytes + a;
+  const uint64_t a4 = a & ~3ull;
+  const uint32_t *src = (const uint32_t *)(bytes + a4), nd = (uint32_t)((a - a4) + ulen + 3) >> 2;
+  uint32_t *dst = (uint32_t *)stage;
+  for (uint32_t k = 0; k < nd; k += 8) {
+    uint32_t t[8];
+#pragma unroll
+    for (uint32_t j = 0; j < 8; j++) t[j] = k + j < nd ? src[k + j] : 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; j++)
+      if (k + j < nd) dst[k + j] = t[j];
+  }
+  return stage + (a - a4);
+}
+
 // document d of the batch (the kernel's lane body; tools/hostemu runs it on the CPU too)
 __device__ void compact_doc(const BatchIn &b, const FastOut &o, uint32_t *hdr, const uint64_t *scr_off,
                             uint32_t *scr, uint32_t d, uint8_t *stage, uint32_t *misc) {
@@ -950,21 +968,7 @@ __device__ void compact_doc(const BatchIn &b, const FastOut &o, uint32_t *hdr, c
     const uint64_t a = b.upd_off[u], z = b.upd_off[u + 1];
     const uint32_t ulen = (uint32_t)(z - a);
     D.uoff = (uint32_t)(a - B0);
-    D.up = b.bytes + a;
-    if (stage && ulen + 4 <= CP_STAGE) { // the update into this lane's LDS stage, aligned dwords
-      const uint64_t a4 = a & ~3ull;
-      const uint32_t *src = (const uint32_t *)(b.bytes + a4), nd = (uint32_t)((a - a4) + ulen + 3) >> 2;
-      uint32_t *dst = (uint32_t *)stage;
-      for (uint32_t k = 0; k < nd; k += 8) {
-        uint32_t t[8];
-#pragma unroll
-        for (uint32_t j = 0; j < 8; j++) t[j] = k + j < nd ? src[k + j] : 0u;
-#pragma unroll
-        for (uint32_t j = 0; j < 8; j++)
-          if (k + j < nd) dst[k + j] = t[j];
-      }
-      D.up = stage + (a - a4);
-    }
+    D.up = cp_stage(b.bytes, a, ulen, stage);
     CpSink sk{&D, D.up, 0, 0, 0, false};
     const int e = walk_update(D.up, ulen, sk);
     if (e) {
@@ -1118,7 +1122,7 @@ struct CpCountSink {
   __device__ int on_ds_done() { return 0; }
 };
 // document d: its count header and scratch words
-__device__ void compact_count_doc(const BatchIn &b, uint32_t *hdr, uint64_t *need, uint32_t d) {
+__device__ void compact_count_doc(const BatchIn &b, uint32_t *hdr, uint64_t *need, uint32_t d, uint8_t *stage) {
   uint32_t *h = hdr + (size_t)CP_HDR * d;
   for (uint32_t i = 0; i < CP_HDR; i++) h[i] = 0;
   const uint64_t u0 = b.doc_upd[d], u1 = b.doc_upd[d + 1];
@@ -1129,7 +1133,7 @@ __device__ void compact_count_doc(const BatchIn &b, uint32_t *hdr, uint64_t *nee
     for (uint64_t u = u0; u < u1; u++) {
       sk.ub = sk.ur = 0;
       const uint64_t a = b.upd_off[u], z = b.upd_off[u + 1];
-      const int e = walk_update(b.bytes + a, (uint32_t)(z - a), sk);
+      const int e = walk_update(cp_stage(b.bytes, a, (uint32_t)(z - a), stage), (uint32_t)(z - a), sk);
       if (sk.ub > h[H_MB]) h[H_MB] = sk.ub;
       if (sk.ur > h[H_MR]) h[H_MR] = sk.ur;
       if (e || h[H_OVER]) break;
@@ -1138,9 +1142,10 @@ __device__ void compact_count_doc(const BatchIn &b, uint32_t *hdr, uint64_t *nee
   need[d] = h[H_OVER] ? 0 : cp_words(h);
 }
 __global__ void __launch_bounds__(64) k_compact_count(BatchIn b, uint32_t *hdr, uint64_t *need) {
+  __shared__ __align__(16) uint8_t stage[64 * CP_STAGE];
   ym_set_grammar(0);
   const uint32_t d = blockIdx.x * 64 + threadIdx.x;
-  if (d < b.n_docs) compact_count_doc(b, hdr, need, d);
+  if (d < b.n_docs) compact_count_doc(b, hdr, need, d, stage + threadIdx.x * CP_STAGE);
 }
 
 void launch_compact_count(const BatchIn &b, uint32_t *hdr, uint64_t *need, hipStream_t s) {

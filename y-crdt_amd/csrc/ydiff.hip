@@ -486,7 +486,7 @@ __device__ __noinline__ uint32_t validate_doc(const uint8_t *up, uint32_t un, co
 // ------------------------------------------------------------------ ring planner
 // k_plan_ring: the common-shape planner.  Lane per document (a C5 batch has ~100k documents:
 // one lane each is the instruction-cheapest walk), but each lane reads its update from a
-// private 256-byte LDS ring instead of HBM: the ring is refilled with sixteen 16-byte loads at
+// private 192-byte LDS ring instead of HBM: the ring is refilled with twelve 16-byte loads at
 // one program point of the step loop, so a wave waits for memory once per refill round instead
 // of once per block.  One step consumes one whole item — a block, a section header, a
 // DeleteSet entry header or range — with branch-free LEB128 decodes of 8-byte LDS reads, so
@@ -495,8 +495,12 @@ __device__ __noinline__ uint32_t validate_doc(const uint8_t *up, uint32_t un, co
 // unsquashed DeleteSet ranges, more than 8 clients / DeleteSet entries, a varint longer than 5
 // bytes, a block header longer than the ring — leave the document to the general planner
 // (k_plan pass 0), marked ps.big[d] = PLAN_REDO; everything it plans is byte-identical to it.
-constexpr uint32_t RING = 256;          // ring bytes per lane
-constexpr uint32_t RING_STRIDE = 272;   // LDS bytes per lane (16-byte aligned rows)
+#ifndef YM_RING
+#define YM_RING 192
+#endif
+constexpr uint32_t RING = YM_RING;      // ring bytes per lane (a multiple of 64)
+constexpr uint32_t RING_STRIDE = RING + 16; // LDS bytes per lane (16-byte aligned rows)
+constexpr uint32_t RING_G = RING % 128 == 0 ? 8 : 4; // 16-byte loads per refill group
 constexpr uint32_t RING_NT = 256;       // lanes (documents) per workgroup
 constexpr uint32_t RING_STEPS = 10;     // item steps between refill points
 constexpr uint8_t PLAN_REDO = 3;
@@ -640,12 +644,13 @@ __global__ void __launch_bounds__(RING_NT) k_plan_ring(DiffBatch b, PlanScratch 
         const uint4 *q = (const uint4 *)R.rb;
         uint4 *dst = (uint4 *)row;
 #pragma unroll
-        for (uint32_t g = 0; g < RING / 16; g += 8) { // two groups of eight 16-byte loads
-          uint4 x[8];
+        for (uint32_t g = 0; g < RING / 16; g += RING_G) { // groups of 16-byte loads
+          uint4 x[RING_G];
 #pragma unroll
-          for (uint32_t k = 0; k < 8; k++) x[k] = R.rb + 16 * (g + k) < R.send ? q[g + k] : make_uint4(0, 0, 0, 0);
+          for (uint32_t k = 0; k < RING_G; k++)
+            x[k] = R.rb + 16 * (g + k) < R.send ? q[g + k] : make_uint4(0, 0, 0, 0);
 #pragma unroll
-          for (uint32_t k = 0; k < 8; k++) dst[g + k] = x[k];
+          for (uint32_t k = 0; k < RING_G; k++) dst[g + k] = x[k];
         }
         R.rend = R.rb + RING < R.send ? R.rb + RING : R.send;
         R.sync_rel();

@@ -60,7 +60,7 @@ size_t fast_lds_bytes(const FastCaps &c);
 void launch_lean(const BatchIn &b, const FastOut &o, uint32_t *scr, hipStream_t s);
 // k_lean dispatch order for skewed batches: documents by update-count class, longest class
 // first (longest-processing-time-first: a long document starts early instead of ending the
-// kernel).  ctr: 8 zeroed words.
+// kernel).  ctr: 16 zeroed words.
 void launch_lean_order(const uint64_t *doc_upd, uint32_t n_docs, uint32_t *ctr, uint32_t *order, hipStream_t s);
 inline uint64_t lean_scratch_words(uint64_t n_updates, uint64_t n_docs, uint64_t n_bytes) {
   return 4 * n_updates + 64 * n_docs + n_bytes;

@@ -369,7 +369,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     ym::BatchIn bl = b;
     if (c->lean_order == 1 || (c->lean_order < 0 && n >= 65536)) {
       if (!c->lean_ord.ensure((size_t)n * 4 + 64)) return YMERGE_ERR_DEVICE;
-      hipMemsetAsync(c->lean_ord.p, 0, 32, c->s);
+      hipMemsetAsync(c->lean_ord.p, 0, 64, c->s); // class counts and cursors (<= 16 words)
       ym::launch_lean_order(d_doc_upd, n, c->lean_ord.as<uint32_t>(), c->lean_ord.as<uint32_t>() + 16, c->s);
       bl.order = c->lean_ord.as<uint32_t>() + 16;
     }

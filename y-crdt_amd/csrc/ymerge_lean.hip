@@ -1065,20 +1065,23 @@ __global__ void __launch_bounds__(64 * WPB, OCC) k_lean(BatchIn b, FastOut o, ui
 }
 
 // update-count classes of the dispatch order (longest first)
-__device__ __forceinline__ uint32_t lean_class(uint64_t U) { return U > 2048 ? 0 : U > 512 ? 1 : U > 64 ? 2 : 3; }
+constexpr uint32_t LN_NCLS = 6;
+__device__ __forceinline__ uint32_t lean_class(uint64_t U) {
+  return U > 4096 ? 0 : U > 2048 ? 1 : U > 1024 ? 2 : U > 256 ? 3 : U > 64 ? 4 : 5;
+}
 __global__ void __launch_bounds__(256) k_lean_order_count(const uint64_t *doc_upd, uint32_t n, uint32_t *ctr) {
-  __shared__ uint32_t c[4];
-  if (threadIdx.x < 4) c[threadIdx.x] = 0;
+  __shared__ uint32_t c[LN_NCLS];
+  if (threadIdx.x < LN_NCLS) c[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t d = blockIdx.x * 256 + threadIdx.x;
   if (d < n) atomicAdd(&c[lean_class(doc_upd[d + 1] - doc_upd[d])], 1u);
   __syncthreads();
-  if (threadIdx.x < 4 && c[threadIdx.x]) atomicAdd(&ctr[threadIdx.x], c[threadIdx.x]);
+  if (threadIdx.x < LN_NCLS && c[threadIdx.x]) atomicAdd(&ctr[threadIdx.x], c[threadIdx.x]);
 }
 __global__ void __launch_bounds__(256) k_lean_order_place(const uint64_t *doc_upd, uint32_t n, uint32_t *ctr,
                                                          uint32_t *order) {
-  __shared__ uint32_t c[4], base[4];
-  if (threadIdx.x < 4) c[threadIdx.x] = 0;
+  __shared__ uint32_t c[LN_NCLS], base[LN_NCLS];
+  if (threadIdx.x < LN_NCLS) c[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t d = blockIdx.x * 256 + threadIdx.x;
   uint32_t k = 0, r = 0;
@@ -1087,10 +1090,10 @@ __global__ void __launch_bounds__(256) k_lean_order_place(const uint64_t *doc_up
     r = atomicAdd(&c[k], 1u);
   }
   __syncthreads();
-  if (threadIdx.x < 4) { // this workgroup's run in its class: class start + claimed offset
+  if (threadIdx.x < LN_NCLS) { // this workgroup's run in its class: class start + claimed offset
     uint32_t start = 0;
     for (uint32_t q = 0; q < threadIdx.x; q++) start += ctr[q];
-    base[threadIdx.x] = c[threadIdx.x] ? start + atomicAdd(&ctr[4 + threadIdx.x], c[threadIdx.x]) : 0;
+    base[threadIdx.x] = c[threadIdx.x] ? start + atomicAdd(&ctr[LN_NCLS + threadIdx.x], c[threadIdx.x]) : 0;
   }
   __syncthreads();
   if (d < n) order[base[k] + r] = d;
