@@ -15,8 +15,10 @@ pytestmark = pytest.mark.gpu
 def engine():
     # k_lean off: every document here reaches the tiled kernel (or the exact engine) as it
     # would for shapes k_lean hands over (tests/test_gpu_lean.py covers k_lean's BIG mode)
+    # (and the grid-wide long-document path off, so that C1 keeps exercising the tiled kernel;
+    # tests/test_gpu_giant.py covers that path)
     from test_gpu_parity import engine_with
-    e = engine_with(YMERGE_LEAN=0)
+    e = engine_with(YMERGE_LEAN=0, YMERGE_GIANT_MIN=0)
     yield e
     e.close()
 

@@ -71,10 +71,9 @@ __device__ __forceinline__ uint32_t gs_visit(const GsArgs &a, uint32_t i, FB blk
 
 __global__ void __launch_bounds__(256) k_gs_pre(GsArgs a) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= a.U) return;
   uint32_t nb = 0, nr = 0, bad = 0, cmin = 0xFFFFFFFFu, cmax = 0, maxend = 0;
   uint64_t bytes = 0, lens = 0, first = ~0ull;
-  bad |= gs_visit(
+  if (i < a.U) bad |= gs_visit(
       a, i,
       [&](uint32_t c, uint32_t k, uint32_t len, uint32_t, uint32_t meta) {
         if (meta & 12) bad |= GSB_BLOCK;
@@ -92,16 +91,27 @@ __global__ void __launch_bounds__(256) k_gs_pre(GsArgs a) {
         cmin = c < cmin ? c : cmin;
         cmax = c > cmax ? c : cmax;
       });
-  a.cnt[i] = nb | ((uint64_t)nr << 32);
-  a.bytes_[i] = bytes;
-  a.lens[i] = lens;
-  if (bad) atomicOr(&a.g[GS_BAD], bad);
-  if (nb || nr) {
-    atomicMin(&a.g[GS_CMIN], cmin);
-    atomicMax(&a.g[GS_CMAX], cmax);
+  if (i < a.U) {
+    a.cnt[i] = nb | ((uint64_t)nr << 32);
+    a.bl[i] = (bytes << 32) | lens;
+  } // block bytes (< 2^31 per document) | clock lengths (< 2^32)
+  // one atomic per wave for each global (a lane per update would serialise 10^5 atomics)
+  for (int o = 32; o > 0; o >>= 1) {
+    bad |= __shfl_xor(bad, o, 64);
+    const uint32_t c0 = __shfl_xor(cmin, o, 64), c1 = __shfl_xor(cmax, o, 64), m = __shfl_xor(maxend, o, 64);
+    cmin = c0 < cmin ? c0 : cmin;
+    cmax = c1 > cmax ? c1 : cmax;
+    maxend = m > maxend ? m : maxend;
+    const uint64_t f = __shfl_xor(first, o, 64);
+    first = f < first ? f : first;
   }
-  if (nr) atomicMax(&a.g[GS_MAXEND], maxend);
-  if (nb) atomicMin((unsigned long long *)(a.g + GS_FIRST), (unsigned long long)first);
+  if ((threadIdx.x & 63) == 0) {
+    if (bad) atomicOr(&a.g[GS_BAD], bad);
+    if (cmin != 0xFFFFFFFFu) atomicMin(&a.g[GS_CMIN], cmin);
+    if (cmax) atomicMax(&a.g[GS_CMAX], cmax);
+    if (maxend) atomicMax(&a.g[GS_MAXEND], maxend);
+    if (first != ~0ull) atomicMin((unsigned long long *)(a.g + GS_FIRST), (unsigned long long)first);
+  }
 }
 
 __device__ __forceinline__ uint32_t gs_hdr(const GsArgs &a) { // bytes of the one-section header
@@ -113,8 +123,8 @@ __global__ void __launch_bounds__(256) k_gs_write(GsArgs a) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= a.U) return;
   const uint32_t clock0 = (uint32_t)*(const uint64_t *)(a.g + GS_FIRST);
-  uint64_t expect = clock0 + a.s_lens[i];
-  uint8_t *dst = a.out + gs_hdr(a) + a.s_bytes[i];
+  uint64_t expect = clock0 + (a.s_bl[i] & 0xFFFFFFFFu);
+  uint8_t *dst = a.out + gs_hdr(a) + (a.s_bl[i] >> 32);
   const uint8_t *src = a.bytes + a.upd_off[a.u0 + i];
   uint32_t bad = 0;
   gs_visit(
@@ -178,7 +188,7 @@ __global__ void __launch_bounds__(256) k_gs_comp(GsArgs a) {
 
 __device__ __forceinline__ uint64_t gs_ds_base(const GsArgs &a) {
   const uint32_t K = (uint32_t)a.w_scan[a.nwords];
-  return gs_hdr(a) + a.s_bytes[a.U] + (K ? varlen(1) + varlen(a.g[GS_CMIN]) + varlen(K) : varlen(0));
+  return gs_hdr(a) + (a.s_bl[a.U] >> 32) + (K ? varlen(1) + varlen(a.g[GS_CMIN]) + varlen(K) : varlen(0));
 }
 
 __global__ void __launch_bounds__(256) k_gs_ds(GsArgs a) {
@@ -190,16 +200,19 @@ __global__ void __launch_bounds__(256) k_gs_ds(GsArgs a) {
 }
 
 __global__ void k_gs_final(GsArgs a, FastOut o) {
-  if (threadIdx.x || a.g[GS_BAD]) return;
-  const uint32_t K = (uint32_t)a.w_scan[a.nwords];
-  const uint64_t total = gs_ds_base(a) + a.k_off[K];
-  if (total > a.cap) return; // (cannot happen: verbatim blocks + squashed ranges) tiled kernel
+  if (threadIdx.x) return;
+  const uint32_t K = a.g[GS_BAD] ? 0 : (uint32_t)a.w_scan[a.nwords];
+  const uint64_t total = a.g[GS_BAD] ? 0 : gs_ds_base(a) + a.k_off[K];
+  if (a.g[GS_BAD] || total > a.cap) { // not the shape after all: the tiled kernel writes it
+    o.path[a.d] = 2;
+    return;
+  }
   Writer w{a.out, 0};
   w_var(w, 1);
   w_var(w, (uint32_t)a.s_cnt[a.U]);
   w_var(w, a.g[GS_CMIN]);
   w_var(w, (uint32_t)*(const uint64_t *)(a.g + GS_FIRST));
-  Writer v{a.out + gs_hdr(a) + a.s_bytes[a.U], 0};
+  Writer v{a.out + gs_hdr(a) + (a.s_bl[a.U] >> 32), 0};
   if (K) {
     w_var(v, 1);
     w_var(v, a.g[GS_CMIN]);
@@ -215,27 +228,27 @@ __global__ void k_gs_final(GsArgs a, FastOut o) {
 
 // documents the tiled kernel would take (path 2) with at least min_u updates: list[0] =
 // count, then (document, updates, ranges, first update, first byte, bytes) for up to GS_LIST
-__global__ void k_gs_find(BatchIn b, const uint8_t *path, const uint32_t *counts, uint32_t min_u, uint64_t *list) {
+__global__ void k_gs_find(BatchIn b, uint8_t *path, uint32_t min_u, uint64_t *list) {
   const uint32_t d = blockIdx.x * 256 + threadIdx.x;
   if (d >= b.n_docs || path[d] != 2) return;
   const uint64_t u0 = b.doc_upd[d], u1 = b.doc_upd[d + 1];
   if (u1 - u0 < min_u || u1 - u0 >= (1ull << 31)) return;
   const uint64_t k = atomicAdd((unsigned long long *)&list[0], 1ull);
   if (k < GS_LIST) {
+    path[d] = GS_PATH; // k_big_count skips it; k_gs_final sets 0 (written) or 2 (tiled kernel)
     uint64_t *e = list + 1 + 6 * k;
     e[0] = d;
     e[1] = u1 - u0;
-    e[2] = counts[4 * d + 3];
+    e[2] = 0;
     e[3] = u0;
     e[4] = b.upd_off[u0];
     e[5] = b.upd_off[u1] - b.upd_off[u0];
   }
 }
 
-void launch_gs_find(const BatchIn &b, const uint8_t *path, const uint32_t *counts, uint32_t min_u, uint64_t *list,
-                    hipStream_t s) {
+void launch_gs_find(const BatchIn &b, uint8_t *path, uint32_t min_u, uint64_t *list, hipStream_t s) {
   if (!b.n_docs) return;
-  hipLaunchKernelGGL(k_gs_find, dim3((b.n_docs + 255) / 256), dim3(256), 0, s, b, path, counts, min_u, list);
+  hipLaunchKernelGGL(k_gs_find, dim3((b.n_docs + 255) / 256), dim3(256), 0, s, b, path, min_u, list);
 }
 void launch_gs_pre(const GsArgs &a, hipStream_t s) {
   hipLaunchKernelGGL(k_gs_pre, dim3((a.U + 255) / 256), dim3(256), 0, s, a);

@@ -69,6 +69,7 @@ void launch_fast_merge(const BatchIn &b, const FastCaps &caps, const FastOut &o,
 // one long single-client document merged by grid-wide kernels (ygiant.hip)
 constexpr uint32_t GS_LIST = 16;     // such documents per batch (the rest: tiled kernel)
 constexpr uint32_t GS_MIN_U = 65536; // updates (env YMERGE_GIANT_MIN)
+constexpr uint8_t GS_PATH = 5;       // path of a listed document until k_gs_final decides
 struct GsArgs {
   const uint8_t *bytes;
   const uint64_t *upd_off;
@@ -77,8 +78,8 @@ struct GsArgs {
   uint32_t U, d;
   uint8_t *out; // the document's slot
   uint64_t cap;
-  uint64_t *cnt, *bytes_, *lens;       // [U]: blocks | ranges << 32, block bytes, clock lengths
-  uint64_t *s_cnt, *s_bytes, *s_lens; // [U + 1] exclusive scans
+  uint64_t *cnt, *bl;    // [U]: blocks | ranges << 32, block bytes << 32 | clock lengths
+  uint64_t *s_cnt, *s_bl; // [U + 1] exclusive scans
   uint32_t *g;                         // flags / client min, max / max range end / first block key
   uint32_t *bm;                        // deleted-clock bitmap [nwords]
   uint32_t nbits, nwords;
@@ -86,8 +87,7 @@ struct GsArgs {
   uint32_t *k_start, *k_len;           // runs = squashed ranges
   uint64_t *k_size, *k_off;
 };
-void launch_gs_find(const BatchIn &b, const uint8_t *path, const uint32_t *counts, uint32_t min_u, uint64_t *list,
-                    hipStream_t s);
+void launch_gs_find(const BatchIn &b, uint8_t *path, uint32_t min_u, uint64_t *list, hipStream_t s);
 void launch_gs_pre(const GsArgs &a, hipStream_t s);
 void launch_gs_rest(const GsArgs &a, const FastOut &o, uint32_t n_ranges, uint64_t *scan_tmp, hipStream_t s);
 

@@ -3,7 +3,7 @@
 // The fast path (ymerge_fast.hip) keeps a whole document in LDS: at most 1024 blocks,
 // 512 DeleteSet entries / ranges, 64 distinct DeleteSet clients.  Documents beyond
 // that (Zipf-tail tenants of C3, long per-op logs such as the automerge-paper trace,
-// delete-heavy logs) run here with the same semantics, one 1024-lane workgroup per
+// delete-heavy logs) run here with the same semantics, one 512-lane workgroup per
 // document, the SoA block / DeleteSet tables in HBM scratch and every phase a loop
 // over tiles of 1024 elements with a carry between tiles:
 //   k_big_count  per document: counts (blocks, entries, ranges) from the k_decode
@@ -25,7 +25,6 @@
 
 namespace ym {
 
-constexpr int BIG_NT = 1024;
 constexpr uint32_t BIG_DCAP = 1024;   // distinct DeleteSet clients per document
 constexpr uint32_t BIG_DTAB = 2048;   // LDS hash slots for them (u64)
 constexpr uint32_t BIG_CHUNK = 2048;  // LDS bitonic chunk of the sort (key u64 + value u32)
@@ -490,9 +489,9 @@ template <int NT> struct BigShared {
   __align__(16) uint8_t un[BIG_UNION + 64];
 };
 
-template <int NT>
-__global__ void __launch_bounds__(NT) k_big_merge(BatchIn b, const uint32_t *counts, const uint64_t *scr_off,
-                                                  uint32_t *scratch, FastOut o) {
+template <int NT, int OCC>
+__global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t *counts, const uint64_t *scr_off,
+                                                       uint32_t *scratch, FastOut o) {
   ym_set_grammar(b.v1x);
   const uint32_t d = blockIdx.x;
   if (d >= b.n_docs || o.path[d] != 2) return;
@@ -1283,7 +1282,14 @@ void launch_big_count(const BatchIn &b, const FastOut &o, uint32_t *counts, uint
 void launch_big_merge(const BatchIn &b, const uint32_t *counts, const uint64_t *scr_off, uint32_t *scratch,
                       const FastOut &o, hipStream_t s) {
   if (!b.n_docs) return;
-  hipLaunchKernelGGL((k_big_merge<BIG_NT>), dim3(b.n_docs), dim3(BIG_NT), 0, s, b, counts, scr_off, scratch, o);
+  // two 512-lane workgroups per CU (4 waves per SIMD at 128 VGPRs, 2 x 68 KB of LDS): twice the
+  // documents in flight of one 1024-lane workgroup per CU (C4: tiled 9.05 -> 6.81 ms);
+  // env YMERGE_BIG_NT=1024 selects the single-workgroup build (A/B)
+  static const int nt = getenv("YMERGE_BIG_NT") ? atoi(getenv("YMERGE_BIG_NT")) : 512;
+  if (nt == 1024)
+    hipLaunchKernelGGL((k_big_merge<1024, 4>), dim3(b.n_docs), dim3(1024), 0, s, b, counts, scr_off, scratch, o);
+  else
+    hipLaunchKernelGGL((k_big_merge<512, 4>), dim3(b.n_docs), dim3(512), 0, s, b, counts, scr_off, scratch, o);
 }
 
 } // namespace ym

@@ -259,7 +259,7 @@ static bool ensure_keep(ymerge_ctx *c, DevBuf &b, size_t bytes, size_t keep) {
 // kernel) when it is not that shape.  e = (document, updates, ranges, first update, first
 // byte, bytes) from k_gs_find.
 static int run_giant(ymerge_ctx *c, const ym::BatchIn &b, const ym::FastOut &fo, const uint64_t *e) {
-  const uint32_t d = (uint32_t)e[0], U = (uint32_t)e[1], NR = (uint32_t)e[2];
+  const uint32_t d = (uint32_t)e[0], U = (uint32_t)e[1];
   ym::GsArgs a{};
   a.bytes = b.bytes;
   a.upd_off = b.upd_off;
@@ -271,31 +271,30 @@ static int run_giant(ymerge_ctx *c, const ym::BatchIn &b, const ym::FastOut &fo,
   a.out = fo.out + 2 * e[4] + 64ull * d;
   a.cap = 2 * e[5] + 64;
   const size_t nu = (size_t)U + 1;
-  if (!c->gs1.ensure((6 * nu + 4) * 8) ||
-      !c->scan_tmp.ensure(ym::scan_tmp_elems((uint32_t)std::max<size_t>(nu, NR + 2)) * 8 + 64))
+  if (!c->gs1.ensure((4 * nu + 4) * 8) || !c->scan_tmp.ensure(ym::scan_tmp_elems((uint32_t)nu) * 8 + 64))
     return YMERGE_ERR_DEVICE;
   uint64_t *w = c->gs1.as<uint64_t>();
   a.cnt = w;
-  a.bytes_ = w + nu;
-  a.lens = w + 2 * nu;
-  a.s_cnt = w + 3 * nu;
-  a.s_bytes = w + 4 * nu;
-  a.s_lens = w + 5 * nu;
-  a.g = (uint32_t *)(w + 6 * nu);
+  a.bl = w + nu;
+  a.s_cnt = w + 2 * nu;
+  a.s_bl = w + 3 * nu;
+  a.g = (uint32_t *)(w + 4 * nu);
   hipMemsetAsync(a.g, 0, 32, c->s);
   hipMemsetAsync(a.g + 1, 0xFF, 4, c->s);  // client min
   hipMemsetAsync(a.g + 4, 0xFF, 8, c->s);  // first block key
   ym::launch_gs_pre(a, c->s);
   ym::launch_scan_u64(a.cnt, a.s_cnt, U, c->scan_tmp.as<uint64_t>(), c->s);
-  ym::launch_scan_u64(a.bytes_, a.s_bytes, U, c->scan_tmp.as<uint64_t>(), c->s);
-  ym::launch_scan_u64(a.lens, a.s_lens, U, c->scan_tmp.as<uint64_t>(), c->s);
+  ym::launch_scan_u64(a.bl, a.s_bl, U, c->scan_tmp.as<uint64_t>(), c->s);
   uint64_t *hp = c->h_pinned + 64; // flags, client min / max, max range end, first key, block count
   hipMemcpyAsync(hp, a.g, 32, hipMemcpyDeviceToHost, c->s);
   hipMemcpyAsync(hp + 4, a.s_cnt + U, 8, hipMemcpyDeviceToHost, c->s);
   if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
   const uint32_t *g = (const uint32_t *)hp;
-  const uint32_t nb_total = (uint32_t)(hp[4] & 0xFFFFFFFFu);
-  if (g[0] || g[1] != g[2] || nb_total == 0) return 0; // not the shape: tiled kernel
+  const uint32_t nb_total = (uint32_t)(hp[4] & 0xFFFFFFFFu), NR = (uint32_t)(hp[4] >> 32);
+  if (g[0] || g[1] != g[2] || nb_total == 0) { // not the shape: back to the tiled kernel
+    hipMemsetAsync(fo.path + d, 2, 1, c->s);
+    return 0;
+  }
   a.nbits = g[3];
   a.nwords = a.nbits / 32 + 2; // the last word stays clear (run ends)
   const size_t nw = a.nwords;
@@ -423,22 +422,16 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   // documents over the LDS capacities (path == 2): count, scratch offsets, tiled kernel
   uint32_t n_big = 0;
   if (fast && n_p2) {
-    ym::launch_big_count(b, fo, c->counts.as<uint32_t>(), c->need.as<uint64_t>(), c->counter.as<uint32_t>() + 2, c->s);
-    ym::launch_scan_u64(c->need.as<uint64_t>(), c->scr_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
-    hipMemcpyAsync(c->h_pinned + 10, c->scr_off.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, c->s);
-    hipMemcpyAsync(c->h_pinned + 11, c->counter.as<uint32_t>() + 2, 4, hipMemcpyDeviceToHost, c->s);
-    // long documents for the grid-wide single-client path, listed in the same sync
+    // long single-client documents first (ygiant.hip): listed and marked GS_PATH, merged by the
+    // grid-wide kernels; the ones that are not that shape return to path 2 before k_big_count
     const bool giant = c->giant_min && n_updates >= c->giant_min && !c->want_stamps;
-    constexpr size_t GSL = 1 + 6 * ym::GS_LIST;
     if (giant) {
+      constexpr size_t GSL = 1 + 6 * ym::GS_LIST;
       if (!c->gs_list.ensure(GSL * 8)) return YMERGE_ERR_DEVICE;
       hipMemsetAsync(c->gs_list.p, 0, 8, c->s);
-      ym::launch_gs_find(b, path, c->counts.as<uint32_t>(), c->giant_min, c->gs_list.as<uint64_t>(), c->s);
+      ym::launch_gs_find(b, path, c->giant_min, c->gs_list.as<uint64_t>(), c->s);
       hipMemcpyAsync(c->h_pinned + 128, c->gs_list.p, GSL * 8, hipMemcpyDeviceToHost, c->s);
-    }
-    if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
-    n_big = (uint32_t)(c->h_pinned[11] & 0xFFFFFFFFu);
-    if (giant) {
+      if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
       uint64_t ent[GSL];
       memcpy(ent, c->h_pinned + 128, sizeof ent);
       const uint64_t ng = std::min<uint64_t>(ent[0], ym::GS_LIST);
@@ -447,6 +440,12 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
         if (rc) return rc;
       }
     }
+    ym::launch_big_count(b, fo, c->counts.as<uint32_t>(), c->need.as<uint64_t>(), c->counter.as<uint32_t>() + 2, c->s);
+    ym::launch_scan_u64(c->need.as<uint64_t>(), c->scr_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
+    hipMemcpyAsync(c->h_pinned + 10, c->scr_off.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, c->s);
+    hipMemcpyAsync(c->h_pinned + 11, c->counter.as<uint32_t>() + 2, 4, hipMemcpyDeviceToHost, c->s);
+    if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
+    n_big = (uint32_t)(c->h_pinned[11] & 0xFFFFFFFFu);
     if (n_big) {
       if (!c->big_scratch.ensure((size_t)c->h_pinned[10] * 4 + 64)) return YMERGE_ERR_DEVICE;
       ym::launch_big_merge(b, c->counts.as<uint32_t>(), c->scr_off.as<uint64_t>(), c->big_scratch.as<uint32_t>(), fo,

@@ -86,19 +86,24 @@ void launch_scan_u64(const uint64_t *in, uint64_t *out, uint32_t n, uint64_t *tm
 
 namespace ym {
 // pack per-document outputs (start, len) into a contiguous arena at pack_off[d]
+// workgroup (x) per document; small batches also split each document over gridDim.y
+// workgroups (one long document would otherwise be copied by one workgroup)
 __global__ void __launch_bounds__(256) k_pack(const uint8_t *src, const uint64_t *start, const uint64_t *len,
                                              const uint64_t *pack_off, uint8_t *dst, uint32_t n_docs) {
   for (uint32_t d = blockIdx.x; d < n_docs; d += gridDim.x) {
     const uint8_t *s = src + start[d];
     uint8_t *o = dst + pack_off[d];
-    uint64_t n = len[d];
-    for (uint64_t i = threadIdx.x; i < n; i += 256) o[i] = s[i];
+    const uint64_t n = len[d];
+    const uint64_t part = (n + gridDim.y - 1) / gridDim.y, b0 = part * blockIdx.y;
+    const uint64_t b1 = b0 + part < n ? b0 + part : n;
+    for (uint64_t i = b0 + threadIdx.x; i < b1; i += 256) o[i] = s[i];
   }
 }
 void launch_pack(const uint8_t *src, const uint64_t *start, const uint64_t *len, const uint64_t *pack_off,
                  uint8_t *dst, uint32_t n_docs, hipStream_t s) {
   if (!n_docs) return;
   uint32_t g = n_docs < 8192 ? n_docs : 8192;
-  hipLaunchKernelGGL(k_pack, dim3(g), dim3(256), 0, s, src, start, len, pack_off, dst, n_docs);
+  const uint32_t ys = n_docs <= 64 ? 256 : n_docs <= 1024 ? 16 : 1;
+  hipLaunchKernelGGL(k_pack, dim3(g, ys), dim3(256), 0, s, src, start, len, pack_off, dst, n_docs);
 }
 } // namespace ym
