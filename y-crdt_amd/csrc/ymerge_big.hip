@@ -5,7 +5,7 @@
 // that (Zipf-tail tenants of C3, long per-op logs such as the automerge-paper trace,
 // delete-heavy logs) run here with the same semantics, one 512-lane workgroup per
 // document, the SoA block / DeleteSet tables in HBM scratch and every phase a loop
-// over tiles of 1024 elements with a carry between tiles:
+// over tiles of one element per lane with a carry between tiles:
 //   k_big_count  per document: counts (blocks, entries, ranges) from the k_decode
 //                records, first decode error, scratch words
 //   k_big_merge  gather records -> sort blocks by (client desc, clock asc, input order)
