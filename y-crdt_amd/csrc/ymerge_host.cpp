@@ -73,7 +73,7 @@ struct ymerge_ctx {
   bool lean = true; // k_lean first (env YMERGE_LEAN=0: every document through k_decode + k_fast_merge)
   bool pack_stale = false; // pack_off not computed for the last merge (all documents on k_lean)
   uint32_t giant_min = ym::GS_MIN_U; // updates of a document for the grid-wide path (env YMERGE_GIANT_MIN, 0: off)
-  int lean_order = -1; // k_lean longest-first dispatch: env YMERGE_LEAN_ORDER 0/1, default n_docs >= 65536
+  int lean_order = -1; // k_lean longest-first dispatch: env YMERGE_LEAN_ORDER 0/1, default for >= 8192 small docs
   uint32_t compact_lpw = 16; // k_compact documents per wavefront (env YMERGE_COMPACT_LPW; C2: 16 best)
   // host staging: two pinned buffers (double-buffered H2D / D2H of caller memory)
   uint8_t *stage[2] = {nullptr, nullptr};
@@ -366,7 +366,9 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     // large batches: long documents dispatched first (a skewed batch otherwise ends on the
     // last long document to start)
     ym::BatchIn bl = b;
-    if (c->lean_order == 1 || (c->lean_order < 0 && n >= 65536)) {
+    // (batches of many small documents: Zipf-like tenants, where one long document would
+    // otherwise end the kernel; also the ~48 MB groups of the pipelined host entry)
+    if (c->lean_order == 1 || (c->lean_order < 0 && n >= 8192 && n_updates < 256ull * n)) {
       if (!c->lean_ord.ensure((size_t)n * 4 + 64)) return YMERGE_ERR_DEVICE;
       hipMemsetAsync(c->lean_ord.p, 0, 64, c->s); // class counts and cursors (<= 16 words)
       ym::launch_lean_order(d_doc_upd, n, c->lean_ord.as<uint32_t>(), c->lean_ord.as<uint32_t>() + 16, c->s);
