@@ -31,6 +31,8 @@ namespace ym {
 
 constexpr uint32_t CP_MAXCL = 8, CP_MAXROOT = 4;
 constexpr uint32_t CP_STAGE = 256; // per-lane LDS copy of the current update (bytes)
+constexpr uint32_t CP_IS = 16, CP_IN = 64; // arrival index: one sample per 16 arrivals, 64 samples
+constexpr uint32_t CP_LANES = 16;          // documents per wavefront at most (LDS sized for them)
 constexpr uint32_t CNIL = 0xFFFFFFFFu;
 // item words
 enum : uint32_t {
@@ -70,9 +72,12 @@ enum : uint32_t {
   M_HCN = M_HCL + CP_MAXCL,         // their block counts (arrival capacities) [8]
   M_HCO = M_HCN + CP_MAXCL,         // their arrival arrays' offsets (pairs) [8]
   M_HNCL = M_HCO + CP_MAXCL,        // header clients
-  M_END = M_HNCL + 1
+  M_CLKEND = M_HNCL + 1,            // ClientBlockList::clock of each client [8]
+  M_IDX = M_CLKEND + CP_MAXCL,      // per client: start clock of every CP_IS-th arrival [8 x CP_IN]
+  M_END = M_IDX + CP_MAXCL * CP_IN
 };
 static_assert(M_END <= 1024, "misc area");
+static_assert(CP_LANES * (M_END * 4 + CP_STAGE) <= 48 * 1024, "three workgroups per CU");
 // per-document counts from k_compact_count (CP_HDR words per document): blocks, deleted
 // ranges, the most blocks / ranges of one update, distinct block clients (<= 8), and each
 // client's block count (its arrival array)
@@ -146,24 +151,33 @@ __device__ int cp_cl_add(CDoc &D, uint32_t client) { // BlockStore::get_client_b
   D.m[M_HEAD + c] = D.m[M_TAIL + c] = CNIL;
   D.m[M_NBLK + c] = 0;
   D.m[M_BEFORE + c] = 0;
+  D.m[M_CLKEND + c] = 0;
   return c;
 }
 __device__ uint32_t cp_fwd(CDoc &D, uint32_t x) {
   for (uint32_t g = D.ni; D.I(x, I_FWD) != CNIL && g; g--) x = D.I(x, I_FWD);
   return x;
 }
-__device__ uint32_t cp_clock(CDoc &D, int c) { // ClientBlockList::clock
-  if (c < 0 || D.m[M_TAIL + c] == CNIL) return 0;
-  const uint32_t t = D.m[M_TAIL + c];
-  return D.I(t, I_CLOCK) + D.I(t, I_LEN);
+__device__ uint32_t cp_clock(CDoc &D, int c) { // ClientBlockList::clock (kept by cp_push)
+  return c < 0 ? 0 : D.m[M_CLKEND + c];
 }
 // find_pivot: the cell (item or GC) containing clock, or CNIL
 __device__ uint32_t cp_cell(CDoc &D, int c, uint32_t clock) {
   if (c < 0) return CNIL;
   const uint32_t n = D.m[M_NBLK + c];
   const uint32_t *a = D.cb + 2ull * D.m[M_HCO + D.m[M_CBK + c]];
-  if (!n || a[0] > clock) return CNIL;
-  uint32_t lo = 0, hi = n - 1; // last arrived block starting <= clock
+  if (!n || D.m[M_IDX + c * CP_IN] > clock) return CNIL;
+  // last arrived block starting <= clock: the sampled starts in LDS narrow the search of the
+  // arrival array in HBM to one run of CP_IS arrivals (or to the arrivals past the samples)
+  const uint32_t *ix = D.m + M_IDX + c * CP_IN;
+  const uint32_t ns = (n + CP_IS - 1) / CP_IS < CP_IN ? (n + CP_IS - 1) / CP_IS : CP_IN;
+  uint32_t s0 = 0, s1 = ns - 1;
+  while (s0 < s1) {
+    const uint32_t mid = (s0 + s1 + 1) / 2;
+    if (ix[mid] <= clock) s0 = mid;
+    else s1 = mid - 1;
+  }
+  uint32_t lo = s0 * CP_IS, hi = s0 + 1 < ns ? (s0 + 1) * CP_IS - 1 : n - 1;
   while (lo < hi) {
     const uint32_t mid = (lo + hi + 1) / 2;
     if (a[2 * mid] <= clock) lo = mid;
@@ -415,8 +429,11 @@ __device__ void cp_push(CDoc &D, int c, uint32_t x) {
     return;
   }
   uint32_t *a = D.cb + 2ull * D.m[M_HCO + k];
-  a[2 * n] = D.I(x, I_CLOCK);
+  const uint32_t clock = D.I(x, I_CLOCK);
+  a[2 * n] = clock;
   a[2 * n + 1] = x;
+  if (n % CP_IS == 0 && n / CP_IS < CP_IN) D.m[M_IDX + c * CP_IN + n / CP_IS] = clock;
+  D.m[M_CLKEND + c] = clock + D.I(x, I_LEN);
   D.m[M_NBLK + c] = n + 1;
 }
 
@@ -1083,8 +1100,8 @@ __device__ void compact_doc(const BatchIn &b, const FastOut &o, uint32_t *hdr, c
 // less divergence and more waves in flight on a latency-bound, branchy lane body
 __global__ void __launch_bounds__(64) k_compact(BatchIn b, FastOut o, uint32_t *hdr, const uint64_t *scr_off,
                                                  uint32_t *scr, uint32_t lpw) {
-  __shared__ __align__(16) uint8_t stage[64 * CP_STAGE];
-  __shared__ uint32_t misc[64 * M_END];
+  __shared__ __align__(16) uint8_t stage[CP_LANES * CP_STAGE];
+  __shared__ uint32_t misc[CP_LANES * M_END];
   ym_set_grammar(0);
   const uint32_t d = blockIdx.x * lpw + threadIdx.x;
   if (threadIdx.x < lpw && d < b.n_docs)
@@ -1155,7 +1172,7 @@ void launch_compact_count(const BatchIn &b, uint32_t *hdr, uint64_t *need, hipSt
 void launch_compact(const BatchIn &b, const FastOut &o, uint32_t *hdr, const uint64_t *scr_off, uint32_t *scr,
                     uint32_t lpw, hipStream_t s) {
   if (!b.n_docs) return;
-  if (lpw < 1 || lpw > 64) lpw = 64;
+  if (lpw < 1 || lpw > CP_LANES) lpw = CP_LANES; // the LDS arrays hold CP_LANES documents
   hipLaunchKernelGGL(k_compact, dim3((b.n_docs + lpw - 1) / lpw), dim3(64), 0, s, b, o, hdr, scr_off, scr, lpw);
 }
 
