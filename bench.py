@@ -305,7 +305,7 @@ def run_compact(a, eng, batch, tensors, dev, world):
     if not a.no_cpu_baseline and world == 1:
         k = min(batch.n_docs, 1000)
         s = batch.prefix(k)
-        threads = min(8, os.cpu_count() or 1)
+        threads = min(16, os.cpu_count() or 1)  # the job's CPU share on the GPU box
         t = time.perf_counter()
         oracle.compact_batch(s.data, s.upd_off, s.doc_upd, threads=threads)
         ct = time.perf_counter() - t
