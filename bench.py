@@ -233,9 +233,18 @@ def run_merge(a, rank, world, dev):
         pcie = time.perf_counter() - t
         del g, h_o
 
-    compact = None
+    compact = v2 = None
     if a.workload == "c2" and not a.no_compact and rank == 0:
-        compact = run_compact(a, eng, batch, (t_b, t_u, t_d), dev, world)
+        # secondary measurements after the timed region: a failure is reported in the line,
+        # it never costs the headline
+        try:
+            compact = run_compact(a, eng, batch, (t_b, t_u, t_d), dev, world)
+        except Exception as e:  # noqa: BLE001
+            compact = {"error": repr(e)[:200]}
+        try:
+            v2 = run_v2(a, eng, batch, dev, world)
+        except Exception as e:  # noqa: BLE001
+            v2 = {"error": repr(e)[:200]}
 
     allst = dist.gather_stats([batch.n_docs, batch.n_bytes, out_bytes, n_err, elapsed, ms_pipe,
                                e2e or 0.0], device=dev)
@@ -279,8 +288,50 @@ def run_merge(a, rank, world, dev):
             "pcie_note": "input GB/s if only the pinned H2D of the input and D2H of the output ran"},
         "cpu_baseline": cpu,
         "store_compaction": compact,
+        "lib0_v2": v2,
     }
     return line
+
+
+def run_v2(a, eng, batch, dev, world):
+    """merge_updates_v2 (yrs/src/alt.rs:35-48) of the same documents with every update in lib0
+    v2 (converted on the device, yconvert_updates_v1_to_v2_batch_device), inputs resident;
+    rank 0's shard, the oracle's v2 merge on a bounded sample beside it."""
+    import ymerge
+    v2b, v2off, st = eng.convert_v1_to_v2_host(batch.data, batch.upd_off)
+    if st.any():
+        return {"error": "conversion status", "docs": int((st != 0).sum())}
+    n2 = int(v2off[-1])
+    t_b = torch.from_numpy(ymerge.padded(v2b[:n2])).to(dev)
+    t_u = torch.from_numpy(np.ascontiguousarray(v2off, np.uint64).view(np.int64)).to(dev)
+    t_d = torch.from_numpy(batch.doc_upd.view(np.int64)).to(dev)
+    torch.cuda.synchronize(dev)
+    args = (t_b.data_ptr(), n2, t_u.data_ptr(), batch.n_updates, t_d.data_ptr(), batch.n_docs)
+    eng.merge_device(*args, version=2)
+    runs = []
+    for _ in range(3):
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        r = eng.merge_device(*args, version=2)
+        torch.cuda.synchronize(dev)
+        runs.append(time.perf_counter() - t)
+    _, _, rst = r.to_host()
+    dt = min(runs)
+    cpu = None
+    if not a.no_cpu_baseline and world == 1:
+        import oracle
+        k = min(batch.n_docs, 1000)
+        u1 = int(batch.doc_upd[k])
+        threads = min(16, os.cpu_count() or 1)
+        t = time.perf_counter()
+        oracle.merge_batch(v2b[:int(v2off[u1])], v2off[:u1 + 1], batch.doc_upd[:k + 1], mode=1, threads=threads,
+                           version=2)
+        ct = time.perf_counter() - t
+        cpu = {"value": int(v2off[u1]) / ct / 1e9, "unit": "GB/s", "cores": threads, "kind": "port",
+               "sample": f"oracle merge_updates_v2 (fast mode) on the first {k} documents"}
+    return {"value": n2 / dt / 1e9, "unit": "GB/s", "ms": dt * 1e3, "docs_per_s": batch.n_docs / dt,
+            "v2_bytes_in": n2, "error_docs": int((rst != 0).sum()),
+            "kernel": "k_v2_decode + merge pipeline + k_v2_encode", "cpu_baseline": cpu}
 
 
 def run_compact(a, eng, batch, tensors, dev, world):

@@ -162,6 +162,12 @@ int yencode_state_vector_from_update_v2_batch_device(ymerge_ctx *ctx, const uint
 int ycompact_updates_v1_batch_device(ymerge_ctx *ctx, const uint8_t *d_bytes, uint64_t n_bytes,
                                      const uint64_t *d_upd_off, uint64_t n_updates, const uint64_t *d_doc_upd,
                                      uint64_t n_docs, ymerge_device_result *res);
+/* lib0 v1 -> v2 of every update of an arena (Update::decode_v1(u).encode_v2()): the updates are
+ * merged one per document and re-encoded by the v2 encoder; res lists one v2 update per input
+ * update.  Feeds the v2 entry points (bench, tests). */
+int yconvert_updates_v1_to_v2_batch_device(ymerge_ctx *ctx, const uint8_t *d_bytes, uint64_t n_bytes,
+                                           const uint64_t *d_upd_off, uint64_t n_updates,
+                                           ymerge_device_result *res);
 /* pack the last device result into host buffers: out (res->out_bytes), out_off (n_docs + 1,
  * document d at out[out_off[d] .. out_off[d+1])), status (n_docs) */
 int ymerge_result_to_host(ymerge_ctx *ctx, const ymerge_device_result *res, uint64_t n_docs, uint8_t *out,

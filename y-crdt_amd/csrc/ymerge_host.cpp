@@ -819,6 +819,26 @@ static int plan_v2_device(ymerge_ctx *c, bool diff, const uint8_t *d_bytes, cons
   return v2_encode(c, res, n, diff ? 0 : 1);
 }
 
+// lib0 v1 -> v2 for every update of an arena (Update::decode_v1(u).encode_v2(), yrs/src/
+// update.rs:714-749 + updates/encoder.rs): each update merged alone (a one-update document)
+// and written by the v2 encoder.  Used to feed the lib0 v2 paths (bench, tests).
+extern "C" int yconvert_updates_v1_to_v2_batch_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
+                                                     const uint64_t *d_upd_off, uint64_t n_updates,
+                                                     ymerge_device_result *res) {
+  if (!c || !res) return YMERGE_ERR_OTHER;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return YMERGE_ERR_DEVICE;
+  if (n_updates > 0xFFFFFFFFull) return YMERGE_ERR_OTHER;
+  std::vector<uint64_t> iota(n_updates + 1);
+  for (uint64_t i = 0; i <= n_updates; i++) iota[i] = i;
+  if (!c->in_doc_upd.ensure((n_updates + 1) * 8) ||
+      hipMemcpyAsync(c->in_doc_upd.p, iota.data(), (n_updates + 1) * 8, hipMemcpyHostToDevice, c->s) != hipSuccess)
+    return YMERGE_ERR_DEVICE;
+  int st = merge_device(c, d_bytes, n_bytes, d_upd_off, n_updates, c->in_doc_upd.as<uint64_t>(), n_updates, res);
+  if (st) return st;
+  return v2_encode(c, res, (uint32_t)n_updates, 0);
+}
+
 extern "C" int ymerge_updates_v2_batch_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
                                               const uint64_t *d_upd_off, uint64_t n_updates, const uint64_t *d_doc_upd,
                                               uint64_t n_docs, ymerge_device_result *res) {

@@ -104,6 +104,7 @@ def lib():
         getattr(L, f"yencode_state_vector_from_update_{v}").argtypes = [c.c_char_p, u32, c.POINTER(u32)]
     L.ymerge_updates_v2_batch_device.argtypes = [vp, vp, u64, vp, u64, vp, u64, c.POINTER(_DevRes)]
     L.ycompact_updates_v1_batch_device.argtypes = [vp, vp, u64, vp, u64, vp, u64, c.POINTER(_DevRes)]
+    L.yconvert_updates_v1_to_v2_batch_device.argtypes = [vp, vp, u64, vp, u64, c.POINTER(_DevRes)]
     L.ydiff_updates_v2_batch_device.argtypes = [vp, vp, vp, vp, vp, u64, c.POINTER(_DevRes)]
     L.yencode_state_vector_from_update_v2_batch_device.argtypes = [vp, vp, vp, u64, c.POINTER(_DevRes)]
     L.ymerge_binary_destroy.argtypes = [vp, u32]
@@ -419,3 +420,19 @@ class Engine:
                 np.asarray(doc_upd, np.uint64).view(np.int64)]
         return self._host_batch(args, lambda a, b, c: self.compact_device(a, int(upd_off[-1]), b, len(upd_off) - 1,
                                                                           c, len(doc_upd) - 1))
+
+    def convert_v1_to_v2_host(self, data, upd_off):
+        """yconvert_updates_v1_to_v2_batch_device over host arrays: every v1 update re-encoded
+        as lib0 v2 (out, out_off[n_updates + 1], status)."""
+        n = len(upd_off) - 1
+        ub = np.ascontiguousarray(data, dtype=np.uint8)
+        args = [ub if len(ub) else np.zeros(1, np.uint8), np.asarray(upd_off, np.uint64).view(np.int64)]
+
+        def run(a, b):
+            res = _DevRes()
+            rc = lib().yconvert_updates_v1_to_v2_batch_device(self._ctx, a, int(upd_off[-1]), b, n,
+                                                               ctypes.byref(res))
+            if rc:
+                raise DeviceError(f"v1 -> v2 conversion failed ({rc})")
+            return DeviceResult(self, res, n)
+        return self._host_batch(args, run)
