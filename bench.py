@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-compact", action="store_true", help="skip the store-based compaction line (c2)")
+    ap.add_argument("--v2", action="store_true", help="also time merge_updates_v2 of the C2 documents (lib0_v2)")
     return ap.parse_args()
 
 
@@ -241,10 +242,11 @@ def run_merge(a, rank, world, dev):
             compact = run_compact(a, eng, batch, (t_b, t_u, t_d), dev, world)
         except Exception as e:  # noqa: BLE001
             compact = {"error": repr(e)[:200]}
-        try:
-            v2 = run_v2(a, eng, batch, dev, world)
-        except Exception as e:  # noqa: BLE001
-            v2 = {"error": repr(e)[:200]}
+        if a.v2:
+            try:
+                v2 = run_v2(a, eng, batch, dev, world)
+            except Exception as e:  # noqa: BLE001
+                v2 = {"error": repr(e)[:200]}
 
     allst = dist.gather_stats([batch.n_docs, batch.n_bytes, out_bytes, n_err, elapsed, ms_pipe,
                                e2e or 0.0], device=dev)
