@@ -42,7 +42,8 @@ METRIC_DIFF = "input GB/s + docs served/sec, batched diff_updates_v1 (sync-step-
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); > 1 without WORLD_SIZE starts them via torch.distributed.run")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
@@ -52,7 +53,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-compact", action="store_true", help="skip the store-based compaction line (c2)")
-    ap.add_argument("--v2", action="store_true", help="also time merge_updates_v2 of the C2 documents (lib0_v2)")
+    ap.add_argument("--no-v2", action="store_true", help="skip the merge_updates_v2 line of the C2 documents (lib0_v2)")
     return ap.parse_args()
 
 
@@ -242,7 +243,7 @@ def run_merge(a, rank, world, dev):
             compact = run_compact(a, eng, batch, (t_b, t_u, t_d), dev, world)
         except Exception as e:  # noqa: BLE001
             compact = {"error": repr(e)[:200]}
-        if a.v2:
+        if not a.no_v2:
             try:
                 v2 = run_v2(a, eng, batch, dev, world)
             except Exception as e:  # noqa: BLE001
@@ -331,8 +332,12 @@ def run_v2(a, eng, batch, dev, world):
         ct = time.perf_counter() - t
         cpu = {"value": int(v2off[u1]) / ct / 1e9, "unit": "GB/s", "cores": threads, "kind": "port",
                "sample": f"oracle merge_updates_v2 (fast mode) on the first {k} documents"}
+    alg = n2 + int(r.out_bytes)  # v2 in + v2 out (per launch)
     return {"value": n2 / dt / 1e9, "unit": "GB/s", "ms": dt * 1e3, "docs_per_s": batch.n_docs / dt,
-            "v2_bytes_in": n2, "error_docs": int((rst != 0).sum()),
+            "v2_bytes_in": n2, "v2_bytes_out": int(r.out_bytes), "error_docs": int((rst != 0).sum()),
+            "roofline": {"bound": "hbm", "achieved": alg / dt / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": alg / dt / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                         "note": "algorithmic v2 in + v2 out over the host-timed call (all stages, one sync)"},
             "kernel": "k_v2_decode + merge pipeline + k_v2_encode", "cpu_baseline": cpu}
 
 
@@ -460,6 +465,9 @@ def run_diff(a, rank, world, dev):
 def main():
     a = parse()
     import dist
+    code = dist.relaunch(a.gpus, os.path.abspath(__file__), sys.argv[1:])  # before any GPU call
+    if code is not None:
+        sys.exit(code)
     rank, world, local = dist.init_from_env("nccl")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)

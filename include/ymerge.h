@@ -85,7 +85,8 @@ typedef struct {
   float ms_decode; /* merge: k_decode (ms_fast = k_fast_merge only) */
   float ms_big;    /* merge: documents over the LDS capacities (k_big_count + k_big_merge) */
   uint32_t docs_overlap; /* merge: of docs_big, documents with overlapping updates (run order, splices) */
-  uint64_t docs_big; /* merge: documents written by the tiled kernel (docs_exact: exact engine) */
+  uint64_t docs_big; /* merge: documents written by the tiled kernel or the grid-wide kernels
+                        (docs_giant; docs_exact: exact engine) */
   uint64_t docs_tiny; /* merge: documents of <= 4 updates (<= 4 KB) written one lane each by the
                          lane-per-document engine (not counted in docs_exact) */
   float ms_tiny;      /* merge: exact-engine stage time when it ran tiny documents only */
@@ -162,9 +163,13 @@ int yencode_state_vector_from_update_v2_batch_device(ymerge_ctx *ctx, const uint
 int ycompact_updates_v1_batch_device(ymerge_ctx *ctx, const uint8_t *d_bytes, uint64_t n_bytes,
                                      const uint64_t *d_upd_off, uint64_t n_updates, const uint64_t *d_doc_upd,
                                      uint64_t n_docs, ymerge_device_result *res);
-/* lib0 v1 -> v2 of every update of an arena (Update::decode_v1(u).encode_v2()): the updates are
- * merged one per document and re-encoded by the v2 encoder; res lists one v2 update per input
- * update.  Feeds the v2 entry points (bench, tests). */
+/* lib0 v1 -> v2 of every update of an arena: each update u becomes
+ * merge_updates_v1([u]) re-encoded by EncoderV2 (yrs/src/alt.rs:15-28 then
+ * Update::encode_v2, yrs/src/updates/encoder.rs:182-528).  For a canonical update this equals
+ * Update::decode_v1(u).encode_v2(); they differ where merge itself rewrites a single update
+ * (overlapping same-client blocks sliced, adjacent Skips joined, update.rs:611-679, 854) and
+ * merge-only rejections give a nonzero status.  res lists one v2 update per input update.
+ * Feeds the v2 entry points (bench, tests). */
 int yconvert_updates_v1_to_v2_batch_device(ymerge_ctx *ctx, const uint8_t *d_bytes, uint64_t n_bytes,
                                            const uint64_t *d_upd_off, uint64_t n_updates,
                                            ymerge_device_result *res);

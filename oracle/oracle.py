@@ -117,8 +117,9 @@ def encode_state_vector_from_update_v1(update):
     return _take(out, olen)
 
 
-def merge_updates_v2(updates, mode=1):
-    """lib0 v2 merge (yrs/src/alt.rs:35-48)."""
+def merge_updates_v2(updates, mode=1, inputs_v1=False):
+    """lib0 v2 merge (yrs/src/alt.rs:35-48).  inputs_v1: v1 inputs, the merged Update encoded
+    with EncoderV2 (Update::merge_updates(decode_v1 each).encode_v2())."""
     bufs = [_buf(u) for u in updates]
     n = len(bufs)
     ptrs = (ctypes.POINTER(ctypes.c_uint8) * max(1, n))(*[ctypes.cast(b[0], ctypes.POINTER(ctypes.c_uint8)) for b in bufs])
@@ -126,8 +127,9 @@ def merge_updates_v2(updates, mode=1):
     out = ctypes.POINTER(ctypes.c_uint8)()
     olen = ctypes.c_size_t()
     L = lib()
-    L.yo_merge_updates_v2.argtypes = L.yo_merge_updates_v1.argtypes
-    st = L.yo_merge_updates_v2(ptrs, lens, n, mode, ctypes.byref(out), ctypes.byref(olen))
+    fn = L.yo_merge_updates_v1_to_v2 if inputs_v1 else L.yo_merge_updates_v2
+    fn.argtypes = L.yo_merge_updates_v1.argtypes
+    st = fn(ptrs, lens, n, mode, ctypes.byref(out), ctypes.byref(olen))
     if st:
         raise OracleError(st)
     return _take(out, olen)

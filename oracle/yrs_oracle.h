@@ -54,6 +54,8 @@ int yo_merge_updates_v2(const uint8_t *const *updates, const size_t *lens, size_
 int yo_diff_updates_v2(const uint8_t *update, size_t update_len, const uint8_t *sv, size_t sv_len, uint8_t **out,
                        size_t *out_len);
 int yo_encode_state_vector_from_update_v2(const uint8_t *update, size_t len, uint8_t **out, size_t *out_len);
+int yo_merge_updates_v1_to_v2(const uint8_t *const *updates, const size_t *lens, size_t n, int mode, uint8_t **out,
+                              size_t *out_len);
 int yo_convert_update_v1_to_v2(const uint8_t *update, size_t len, uint8_t **out, size_t *out_len);
 int yo_convert_update_v2_to_v1(const uint8_t *update, size_t len, uint8_t **out, size_t *out_len);
 /* y-sync (yrs/src/sync/protocol.rs:62-69, 219-272): SyncStep1 message of an update's state

@@ -852,8 +852,11 @@ static void ds_encode2(enc2_t *e, const hb_t *t, const idr_t *vals) {
 }
 
 /* ------------------------------------------------------------------ public API (alt.rs:35-48, 63-66, 88-97) */
-int yo_merge_updates_v2(const uint8_t *const *updates, const size_t *lens, size_t n, int mode, uint8_t **out,
-                        size_t *out_len) {
+/* in_v1: the inputs are v1 (Update::decode_v1), the merged Update still encoded with EncoderV2:
+ * Update::merge_updates(us).encode_v2() -- what yconvert_updates_v1_to_v2_batch_device computes
+ * per update (the DeleteSet keeps the merged map's order, no v1 round trip in between). */
+static int merge_to_v2(const uint8_t *const *updates, const size_t *lens, size_t n, int mode, bool in_v1,
+                       uint8_t **out, size_t *out_len) {
   *out = NULL;
   *out_len = 0;
   upd_t *ups = calloc(n + 1, sizeof(upd_t));
@@ -861,7 +864,7 @@ int yo_merge_updates_v2(const uint8_t *const *updates, const size_t *lens, size_
   bool unsupported = false;
   size_t decoded = 0;
   for (size_t i = 0; i < n; i++) {
-    err = decode_update2(&ups[i], updates[i], lens[i]);
+    err = in_v1 ? decode_update(&ups[i], updates[i], lens[i]) : decode_update2(&ups[i], updates[i], lens[i]);
     decoded = i + 1;
     if (err) break;
     if (ups[i].unsupported) unsupported = true;
@@ -897,6 +900,15 @@ int yo_merge_updates_v2(const uint8_t *const *updates, const size_t *lens, size_
     return err;
   }
   return e2_finish(&e, out, out_len);
+}
+
+int yo_merge_updates_v2(const uint8_t *const *updates, const size_t *lens, size_t n, int mode, uint8_t **out,
+                        size_t *out_len) {
+  return merge_to_v2(updates, lens, n, mode, false, out, out_len);
+}
+int yo_merge_updates_v1_to_v2(const uint8_t *const *updates, const size_t *lens, size_t n, int mode, uint8_t **out,
+                              size_t *out_len) {
+  return merge_to_v2(updates, lens, n, mode, true, out, out_len);
 }
 
 int yo_diff_updates_v2(const uint8_t *update, size_t update_len, const uint8_t *svb, size_t sv_len, uint8_t **out,

@@ -1,0 +1,94 @@
+"""yconvert_updates_v1_to_v2_batch_device: every update u becomes merge_updates_v1([u])
+re-encoded by EncoderV2 (include/ymerge.h; yrs/src/alt.rs:15-28, Update::encode_v2
+yrs/src/updates/encoder.rs:182-528), i.e. Update::merge_updates([decode_v1(u)]).encode_v2().
+Checked against the oracle's restatement of exactly that (oracle.merge_updates_v2(...,
+inputs_v1=True)).  It is not always Update::decode_v1(u).encode_v2(): merge rewrites
+overlapping same-client blocks and adjacent Skips, and a DeleteSet of >= 2 clients comes out
+in the merged map's order, not the decoded map's (hashbrown iteration depends on the table's
+capacity and insertion order)."""
+import pytest
+
+from overlaps import _item, _var, update
+
+
+
+def _skip(n):
+    return bytes([10]) + _var(n)
+
+
+def _section(client, clock, blocks):
+    return _var(len(blocks)) + _var(client) + _var(clock) + b"".join(blocks)
+
+
+def _raw_update(sections, ds=b"\x00"):
+    return _var(len(sections)) + b"".join(sections) + ds
+
+
+def edge_updates():
+    return [
+        # one client in two sections of one update, the second overlapping the first
+        # (decode appends both to one block queue; merge slices the covered part,
+        # update.rs:611-679)
+        update([(5, 0, [("i", "abc")]), (5, 1, [("i", "xyzw")])]),
+        update([(7, 2, [("i", "hello")]), (7, 0, [("i", "he")]), (9, 0, [("g", 3)])], [(7, [(0, 2)])]),
+        # adjacent Skips inside one section (joined by BlockCarrier::try_squash, update.rs:854)
+        _raw_update([_section(3, 0, [_item("ab"), _skip(3), _skip(2), _item("cd")])]),
+        _raw_update([_section(3, 4, [_skip(1), _skip(1), _skip(1)]), _section(2, 0, [_item("q")])]),
+        # a trailing Skip and an empty section
+        _raw_update([_section(11, 0, [_item("z"), _skip(4)]), _section(12, 0, [])]),
+    ]
+
+
+@pytest.mark.gpu
+def test_convert_v1_to_v2_device(oracle):
+    """Per-op text updates (multi-client DeleteSets included)."""
+    import ymerge
+    import workloads
+    b = workloads.text_docs(20, 100, seed=77, max_clients=3)
+    e = ymerge.Engine(0)
+    try:
+        out, off, st = e.convert_v1_to_v2_host(b.data, b.upd_off)
+    finally:
+        e.close()
+    assert not st.any()
+    same = 0
+    for i in range(b.n_updates):
+        u = bytes(b.data[int(b.upd_off[i]):int(b.upd_off[i + 1])])
+        want = oracle.merge_updates_v2([u], inputs_v1=True)
+        assert out[int(off[i]):int(off[i + 1])].tobytes() == want, i
+        same += want == oracle.convert_update_v1_to_v2(u)
+    assert same > 0.9 * b.n_updates  # mostly decode-then-encode too (not the multi-client DeleteSets)
+
+
+def test_convert_edge_cases_differ_from_decode_encode(oracle):
+    """CPU pin: the edge cases above are ones where merge-then-encode is not decode-then-encode
+    (so the GPU test below checks the documented semantics, not a coincidence)."""
+    differ = 0
+    for u in edge_updates():
+        code, merged = oracle.status_of(oracle.merge_updates_v1, [u])
+        assert code == 0
+        direct = oracle.merge_updates_v2([u], inputs_v1=True)
+        assert direct == oracle.convert_update_v1_to_v2(merged)  # single-client DeleteSets: no order question
+        differ += direct != oracle.convert_update_v1_to_v2(u)
+    assert differ >= 3
+
+
+@pytest.mark.gpu
+def test_convert_v1_to_v2_device_merge_semantics(oracle):
+    """Overlapping same-client blocks and adjacent Skips: the entry is merge-then-encode."""
+    import numpy as np
+    import ymerge
+    ups = edge_updates()
+    data = np.frombuffer(b"".join(ups), np.uint8).copy()
+    offs = np.concatenate([[0], np.cumsum([len(u) for u in ups])]).astype(np.uint64)
+    e = ymerge.Engine(0)
+    try:
+        out, off, st = e.convert_v1_to_v2_host(data, offs)
+    finally:
+        e.close()
+    for i, u in enumerate(ups):
+        code, merged = oracle.status_of(oracle.merge_updates_v1, [u])
+        assert int(st[i]) == code, (i, int(st[i]), code)
+        if code == 0:
+            want = oracle.merge_updates_v2([u], inputs_v1=True)
+            assert out[int(off[i]):int(off[i + 1])].tobytes() == want, i

@@ -228,3 +228,17 @@ def test_lean_c3_zipf(engine, oracle):
     st = engine.stats()
     assert st["docs_lean"] == b.n_docs and st["docs_exact"] == 0 and st["docs_big"] == 0, st
 
+
+
+def test_lean_scratch_unavailable_degrades(oracle):
+    """No k_lean BIG-mode scratch (env YMERGE_LEAN_SCR_MAX=0 stands in for a failed hipMalloc):
+    the BIG documents are handed over to the fast/tiled path and the batch is still exact."""
+    rng = np.random.default_rng(0x5C4)
+    docs = [text_log(rng, [3, 9], 2000), text_log(rng, [5], 300), text_log(rng, [1, 2, 4], 1500)]
+    e = engine_with(YMERGE_LEAN_SCR_MAX=0)
+    try:
+        check_batch(e, oracle, batch_of(docs))
+        st = e.stats()
+        assert st["docs_lean"] == 1, st  # the 300-update document fits LDS
+    finally:
+        e.close()

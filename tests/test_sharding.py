@@ -84,3 +84,38 @@ def test_two_rank_sharded_merge(oracle, use_gpu):
     assert int(stats[:, 1].sum()) == full.n_bytes
     assert int(stats[:, 2].sum()) == len(out)
     assert stats[:, 4].max() == pytest.approx(0.2)
+
+
+_LAUNCH_SCRIPT = r'''
+import json, os, sys
+sys.path.insert(0, {ydir!r})
+import dist
+import torch
+code = dist.relaunch(int(sys.argv[1]), os.path.abspath(__file__), sys.argv[1:], need_gpus=False)
+if code is not None:
+    sys.exit(code)
+r, w, local = dist.init_from_env("gloo")
+st = dist.gather_stats([r, w, local])
+if r == 0:
+    print(json.dumps({{"world": w, "ranks": sorted(int(x) for x in st[:, 0])}}))
+dist.finalize()
+'''
+
+
+def test_bench_gpus_flag_starts_ranks(tmp_path):
+    """`bench.py --gpus N` without WORLD_SIZE starts N ranks (dist.relaunch, the launcher path
+    bench.py uses before any GPU call); with WORLD_SIZE set, a mismatching --gpus fails."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "launch.py"
+    script.write_text(_LAUNCH_SCRIPT.format(ydir=os.path.join(root, "y-crdt_amd")))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, str(script), "2"], env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line == {"world": 2, "ranks": [0, 1]}
+    bad = subprocess.run([sys.executable, str(script), "2"], env=dict(env, WORLD_SIZE="1"), capture_output=True,
+                         text=True, timeout=120)
+    assert bad.returncode != 0 and "WORLD_SIZE=1" in bad.stderr

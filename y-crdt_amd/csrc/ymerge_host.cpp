@@ -59,6 +59,8 @@ struct ymerge_ctx {
   DevBuf arena, packed, counter, stamps, plan_small, plan_big, rec, ovf, big_scratch, lean_scr, lean_tot, cscr;
   DevBuf gs_list, gs1, gs2; // long single-client documents (ygiant.hip)
   DevBuf lean_ord;          // k_lean dispatch order: 8 counters, then n_docs document indices
+  DevBuf lean_dbg;          // YMERGE_LEAN_DEBUG hand-over reasons (this context's device only)
+  uint64_t lean_scr_max = ~0ull; // env YMERGE_LEAN_SCR_MAX: cap on the k_lean BIG-mode scratch (tests)
   // lib0 v2: v1x arena + offsets + per-update status, v2 output arena + sizes + offsets,
   // state-vector rest offsets + pre-status
   DevBuf v2x, v2x_sz, v2x_off, v2_ust, v2_out, v2_osz, v2_ooff, v2_svoff, v2_svend, v2_pre;
@@ -103,6 +105,7 @@ static bool ctx_init(ymerge_ctx *c, int device) {
   if (const char *v = getenv("YMERGE_COMPACT_LPW")) c->compact_lpw = (uint32_t)atoi(v);
   if (const char *v = getenv("YMERGE_GIANT_MIN")) c->giant_min = (uint32_t)atoi(v);
   if (const char *v = getenv("YMERGE_LEAN_ORDER")) c->lean_order = atoi(v);
+  if (const char *v = getenv("YMERGE_LEAN_SCR_MAX")) c->lean_scr_max = strtoull(v, nullptr, 10);
   // the fast kernel's LDS layout must fit one workgroup (160 KB on gfx950)
   int lds_max = 0;
   if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess) return false;
@@ -130,7 +133,7 @@ extern "C" void ymerge_ctx_destroy(ymerge_ctx *c) {
                     &c->sync_end, &c->sync_st, &c->rec, &c->ovf, &c->status, &c->path,
                     &c->out_start, &c->out_len, &c->pack_off, &c->counts, &c->need, &c->scr_off, &c->scratch,
                     &c->sizes, &c->spill_off, &c->scan_tmp, &c->arena, &c->packed, &c->counter, &c->stamps,
-                    &c->plan_small, &c->plan_big, &c->big_scratch, &c->lean_scr, &c->lean_tot, &c->cscr, &c->gs_list, &c->gs1, &c->gs2, &c->lean_ord, &c->v2x, &c->v2x_sz, &c->v2x_off, &c->v2_ust,
+                    &c->plan_small, &c->plan_big, &c->big_scratch, &c->lean_scr, &c->lean_tot, &c->cscr, &c->gs_list, &c->gs1, &c->gs2, &c->lean_ord, &c->lean_dbg, &c->v2x, &c->v2x_sz, &c->v2x_off, &c->v2_ust,
                     &c->v2_out, &c->v2_osz, &c->v2_ooff, &c->v2_svoff, &c->v2_svend, &c->v2_pre})
     b->release();
   if (c->h_pinned) hipHostFree(c->h_pinned);
@@ -346,11 +349,11 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     c->stamps_docs = n_docs;
   }
   ym::FastOut fo{arena, ostart, olen, status, path, stamps, nullptr, c->counter.as<uint32_t>() + 4};
-  static DevBuf dbgbuf;
-  if (getenv("YMERGE_LEAN_DEBUG") && dbgbuf.ensure(nn * 32)) {
-    hipMemsetAsync(dbgbuf.p, 0xFF, nn * 32, c->s);
-    fo.dbg = dbgbuf.as<uint32_t>();
+  if (getenv("YMERGE_LEAN_DEBUG") && c->lean_dbg.ensure(nn * 32)) {
+    hipMemsetAsync(c->lean_dbg.p, 0xFF, nn * 32, c->s);
+    fo.dbg = c->lean_dbg.as<uint32_t>();
   }
+  (void)hipGetLastError(); // a failed optional allocation must not fail the launches below
   // k_lean: one wavefront per document for the common shape; the rest (path 3) goes on to
   // k_decode + k_fast_merge, which are skipped when k_lean wrote every document
   const bool lean = c->lean && c->fast_threads;
@@ -359,7 +362,11 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   if (lean) {
     // BIG k_lean documents keep their size-proportional tables in HBM (untouched otherwise)
     const uint64_t lw = ym::lean_scratch_words(n_updates, n_docs, n_bytes);
-    uint32_t *lscr = c->lean_scr.ensure(lw * 4 + 64) ? c->lean_scr.as<uint32_t>() : nullptr;
+    // without it k_lean hands its BIG documents over (path 3) instead of failing the batch;
+    // the failed hipMalloc's sticky error is cleared so the launch check below stays meaningful
+    uint32_t *lscr = nullptr;
+    if (lw * 4 + 64 <= c->lean_scr_max && c->lean_scr.ensure(lw * 4 + 64)) lscr = c->lean_scr.as<uint32_t>();
+    (void)hipGetLastError();
     if (!c->lean_tot.ensure(64 * 64)) return YMERGE_ERR_DEVICE;
     hipMemsetAsync(c->lean_tot.p, 0, 64 * 64, c->s);
     fo.lean_total = c->lean_tot.as<unsigned long long>();
@@ -522,10 +529,10 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   c->stats.docs_exact = n_exact - n_tiny;
   c->stats.docs_tiny = n_tiny;
   c->stats.ms_tiny = n_exact == n_tiny ? t12 : 0.0f;
-  c->stats.docs_big = n_big;
+  c->stats.docs_big = n_big + n_giant; // grid-path documents leave path 2 before k_big_count
   c->stats.docs_overlap = n_overlap;
   c->stats.docs_giant = n_giant;
-  c->stats.docs_fast = n_docs - n_exact - n_big - c->stats.docs_lean;
+  c->stats.docs_fast = n_docs - n_exact - c->stats.docs_big - c->stats.docs_lean;
   c->stats.ms_big = t61;
   c->stats.ms_fast = t01;
   c->stats.ms_exact = t12;

@@ -8,6 +8,9 @@ on CPU for tests) carries only the barrier around the timed region and one
 all-gather of a fixed-size per-rank stats vector after the batch.
 """
 import os
+import socket
+import subprocess
+import sys
 
 import numpy as np
 import torch
@@ -29,6 +32,35 @@ def init_from_env(backend=None):
             kw["device_id"] = torch.device("cuda", local)
         torch.distributed.init_process_group(backend, **kw)
     return rank, world, local
+
+
+def relaunch(n, script, argv, need_gpus=True):
+    """Make `python script --gpus n` mean n ranks on this node.
+
+    Inside a torch.distributed.run rank (WORLD_SIZE set) the requested count must equal the
+    world size; otherwise, for n > 1, the n rank processes are started as ONE child
+    (`python -m torch.distributed.run --nproc-per-node n ...`, rendezvous on 127.0.0.1) and
+    its exit code is returned: the caller exits with it.  Called before anything touches the
+    GPU (torch.cuda.device_count() does not initialise it on this image).  Returns None when
+    this process should run the work itself."""
+    if "WORLD_SIZE" in os.environ:
+        world = int(os.environ["WORLD_SIZE"])
+        if n is not None and n != world:
+            raise SystemExit(f"--gpus {n} but WORLD_SIZE={world}: launch one rank per GPU")
+        return None
+    if n is None or n <= 1:
+        return None
+    if need_gpus:
+        have = torch.cuda.device_count()
+        if have < n:
+            raise SystemExit(f"--gpus {n} but only {have} GPU(s) visible")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", script] + list(argv)
+    return subprocess.call(cmd)
 
 
 def shard(n_total, rank, world):
