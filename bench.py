@@ -11,6 +11,8 @@ Workloads (BASELINE.json configs; inputs resident in HBM before the timed region
   c4 (configs[3])           2,000 delete-heavy docs x 5,000 updates (GC'd snapshot + per-op log)
   c5 (configs[4])           diff_updates_v1 of 100,000 compacted docs (C2 merge outputs) against
                             per-document remote state vectors (sync-step-2 serving); weak scaling
+  corpus                    the reference's real inputs: small-test-dataset.bin's 5,320 documents tiled
+                            to D=106,400 per GPU, plus the five editing traces batched (a second block)
 One step = one full batched call over the GPU's shard.  For N > 1 (torch.distributed.run,
 one rank per GPU) documents are sharded by splitmix64(doc_id) % N with no data-path
 collective; RCCL carries the barrier, the max-over-ranks time and a per-shard stats gather.
@@ -46,7 +48,7 @@ def parse():
                     help="ranks (one per GPU); > 1 without WORLD_SIZE starts them via torch.distributed.run")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "corpus"])
     ap.add_argument("--docs", type=int, default=None, help="documents (per GPU for c2/c4/c5, total for c3)")
     ap.add_argument("--ops", type=int, default=None, help="updates per document (c2/c4/c5)")
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="target wall time of one CPU-baseline run")
@@ -128,7 +130,47 @@ def build_merge(a, rank, world):
         return batch, f"C4: {docs} delete-heavy docs x {ops} updates per GPU (70% deletes, GC'd snapshot + " \
                       "per-op log, withheld/duplicated updates)", "weak", {"docs_per_gpu": docs,
                                                                          "updates_per_doc": ops}
+    if w == "corpus":
+        docs = a.docs or 106_400
+        batch = workloads.tile(workloads.dataset_docs(), docs)
+        return batch, f"corpus: assets/bench-input/small-test-dataset.bin (5,320 real Yjs documents, " \
+                      f"compatibility_tests.rs:437-476) tiled to {docs} docs per GPU, batched merge_updates_v1", \
+            "weak", {"docs_per_gpu": docs}
     raise ValueError(w)
+
+
+def run_traces(eng, dev):
+    """The five assets/editing-traces sequential traces, one document each, in one batch."""
+    import workloads
+    import ymerge
+    tb = workloads.traces_batch()
+    t_b = torch.from_numpy(ymerge.padded(tb.data)).to(dev)
+    t_u = torch.from_numpy(tb.upd_off.view(np.int64)).to(dev)
+    t_d = torch.from_numpy(tb.doc_upd.view(np.int64)).to(dev)
+    args = (t_b.data_ptr(), tb.n_bytes, t_u.data_ptr(), tb.n_updates, t_d.data_ptr(), tb.n_docs)
+    eng.merge_device(*args)
+    runs = []
+    for _ in range(3):
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        r = eng.merge_device(*args)
+        torch.cuda.synchronize(dev)
+        runs.append(time.perf_counter() - t)
+    st = eng.stats()
+    _, _, rst = r.to_host()
+    dt = min(runs)
+    return {"value": tb.n_bytes / dt / 1e9, "unit": "GB/s", "ms": dt * 1e3, "docs": tb.n_docs,
+            "updates": tb.n_updates, "bytes_in": tb.n_bytes, "bytes_out": int(r.out_bytes),
+            "error_docs": int((rst != 0).sum()), "paths": path_stats(st)}
+
+
+def path_stats(st):
+    """Documents and device ms per merge path (the routing table of DESIGN.md section 5)."""
+    return {"docs_lean": int(st["docs_lean"]), "docs_fast": int(st["docs_fast"]), "docs_tiled": int(st["docs_big"]),
+            "docs_grid": int(st["docs_giant"]), "docs_overlap": int(st["docs_overlap"]),
+            "docs_exact": int(st["docs_exact"]), "docs_tiny": int(st["docs_tiny"]),
+            "k_lean_ms": st["ms_lean"], "k_decode_ms": st["ms_decode"], "k_fast_merge_ms": st["ms_fast"],
+            "tiled_grid_ms": st["ms_big"], "exact_ms": st["ms_exact"]}
 
 
 def cpu_merge_baseline(batch, a):
@@ -235,7 +277,12 @@ def run_merge(a, rank, world, dev):
         pcie = time.perf_counter() - t
         del g, h_o
 
-    compact = v2 = None
+    compact = v2 = traces = None
+    if a.workload == "corpus" and rank == 0:
+        try:
+            traces = run_traces(eng, dev)
+        except Exception as e:  # noqa: BLE001
+            traces = {"error": repr(e)[:200]}
     if a.workload == "c2" and not a.no_compact and rank == 0:
         # secondary measurements after the timed region: a failure is reported in the line,
         # it never costs the headline
@@ -282,6 +329,7 @@ def run_merge(a, rank, world, dev):
                      "exact_path_ms": ms_exact, "docs_big_path": docs_big, "docs_exact_path": docs_exact,
                      "docs_tiny_path": docs_tiny,
                      "alg_bytes_per_launch": alg_bytes},
+        "paths": path_stats(kstats[-1]),
         "end_to_end": None if e2e is None else {
             "value": float(allst[:, 1].sum()) / float(allst[:, 6].max()) / 1e9, "unit": "GB/s",
             "note": "pinned host arena -> H2D -> merge -> pack -> D2H (pageable numpy), one batch",
@@ -293,6 +341,8 @@ def run_merge(a, rank, world, dev):
         "store_compaction": compact,
         "lib0_v2": v2,
     }
+    if traces is not None:
+        line["editing_traces"] = traces
     return line
 
 
@@ -318,6 +368,7 @@ def run_v2(a, eng, batch, dev, world):
         r = eng.merge_device(*args, version=2)
         torch.cuda.synchronize(dev)
         runs.append(time.perf_counter() - t)
+    st_k = eng.stats()
     _, _, rst = r.to_host()
     dt = min(runs)
     cpu = None
@@ -338,7 +389,9 @@ def run_v2(a, eng, batch, dev, world):
             "roofline": {"bound": "hbm", "achieved": alg / dt / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": alg / dt / 1e9 / HBM_PEAK_GBS, "traffic": None,
                          "note": "algorithmic v2 in + v2 out over the host-timed call (all stages, one sync)"},
-            "kernel": "k_v2_decode + merge pipeline + k_v2_encode", "cpu_baseline": cpu}
+            "kernel": "k_v2_decode + merge pipeline + k_v2_encode", "stages_ms": {
+                "v2_to_v1x": st_k["ms_v2_decode"], "merge": st_k["ms_v2_merge"], "v1x_to_v2": st_k["ms_v2_encode"]},
+            "cpu_baseline": cpu}
 
 
 def run_compact(a, eng, batch, tensors, dev, world):

@@ -94,6 +94,8 @@ typedef struct {
   float ms_lean;      /* merge: k_lean (ms_decode / ms_fast then time the documents it handed over) */
   uint64_t docs_giant; /* merge: of docs_big, long single-client documents merged by the grid-wide
                           kernels of ygiant.hip instead of one tiled workgroup */
+  float ms_v2_decode, ms_v2_merge, ms_v2_encode; /* merge_updates_v2: the v2 -> v1x transcode, the v1
+                          pipeline, the v2 encode (incl. their host syncs) */
 } ymerge_stats;
 
 /* Device-resident result, owned by the context, valid until the next batch.

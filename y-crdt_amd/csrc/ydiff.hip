@@ -25,6 +25,8 @@
 #include "yseq.h"
 #include "ywin.h"
 #include "ywalk.h"
+#include "ylds.h"
+#include "ywave.h"
 #include "ykernels.h"
 
 namespace ym {
@@ -503,7 +505,10 @@ constexpr uint32_t RING_STRIDE = RING + 16; // LDS bytes per lane (16-byte align
 constexpr uint32_t RING_G = RING % 128 == 0 ? 8 : 4; // 16-byte loads per refill group
 constexpr uint32_t RING_NT = 256;       // lanes (documents) per workgroup
 constexpr uint32_t RING_STEPS = 10;     // item steps between refill points
+constexpr uint32_t LP_SLOW = 16;        // k_plan_lane: lanes that wait for a full step before the wave runs it
 constexpr uint8_t PLAN_REDO = 3;
+constexpr uint8_t PLAN_WAVE = 4;         // planned by k_plan_wave (k_plan_lane's long documents)
+constexpr uint64_t PW_MIN = 64 * 1024;   // update bytes from which a document gets a wavefront
 
 enum : uint32_t { R_NCL, R_SEC, R_BLOCK, R_NDS, R_DENT, R_DRANGE, R_DONE };
 
@@ -997,6 +1002,1219 @@ __global__ void __launch_bounds__(RING_NT) k_plan_ring(DiffBatch b, PlanScratch 
   }
 }
 
+// ------------------------------------------------------------------ wave planner
+// k_plan_wave: the common-shape planner with ONE WAVEFRONT per document.  The ring planner
+// above walks a document with one lane, so a wave runs 64 documents whose lanes sit on
+// different item kinds: it is instruction-issue bound (~960 instructions per item step).
+// Here all 64 lanes parse one document.  The v1 grammar interleaves raw string bytes with
+// varints, so a ballot over continuation bits does not find block boundaries; a block's end is
+// only known by parsing it.  A client section's blocks are parsed in windows of 64 chunks of
+// 64 bytes (4 KB staged in LDS with 16-byte loads):
+//   1 speculation: every lane parses blocks from the start of its own chunk (a guess; lane
+//     0's start is the true boundary), recording the block starts it visits in a 64-bit mask
+//     and the position where it leaves the chunk (its exit);
+//   2 stitch: lane i's true entry is lane i-1's exit.  When that position is in lane i's mask
+//     the two parses coincide from there on (a parse is a function of its start position), so
+//     lane i's exit is right too; lanes whose entry is not in their mask parse again from it,
+//     in rounds, until every lane agrees with its predecessor.  A parse from a wrong offset
+//     falls back onto the true boundaries within a block or two, so one round is the norm;
+//   3 the block starts at or after each lane's entry are its true blocks; a wave prefix sum of
+//     their counts gives every block its index in the section, which ends after the block
+//     count of its header (the parse past that point belongs to the next section header);
+//   4 every lane walks its true blocks once more with the validation (canonical varints,
+//     ASCII strings, info byte as re-encoded), summing clock lengths; a prefix sum gives each
+//     block its clock; the lane holding the first block past the remote clock records it.
+// The DeleteSet is varints only: a 512-byte window of it is split by a ballot over terminator
+// bytes (bit 7 clear), a prefix sum gives every varint its index, one decode per varint start
+// goes to LDS; the entry headers are then read in turn and each entry's ranges checked
+// lane-parallel (squashed, canonical, no u32 overflow).
+// It plans the ring planner's shapes (canonical blocks with Deleted / ASCII String content or
+// GC, squashed DeleteSet entries, <= 8 clients and entries, u32 varints of <= 5 bytes) minus
+// Skip blocks and zero-length items, and a block must fit one window; every other document is
+// marked PLAN_REDO for k_plan.  It fills the same scratch records as plan_doc and ends in the
+// same plan_finish, so its plans are byte-identical to the ring's and the general planner's.
+constexpr uint32_t PW_WPB = 4;                   // documents (one wavefront each) per workgroup
+constexpr uint32_t PW_C = 64;                    // chunk bytes per lane
+constexpr uint32_t PW_BURN = 0;                  // bytes parsed before a chunk to fall onto the true blocks
+constexpr uint32_t PW_SB = 64 * PW_C + 512 + 16; // block window bytes: 64 chunks + one block's slack + alignment
+constexpr uint32_t PW_DB = 512;                  // DeleteSet window bytes (8 per lane)
+constexpr uint32_t PW_SW = PW_SB / 4 + 4;        // block stage words (var_at reads 8 bytes at any p < PW_SB)
+constexpr uint32_t PW_DW = PW_DB / 4 + 4;        // DeleteSet stage words, then values and metas
+constexpr uint32_t PW_UW = PW_SW > PW_DW + 2 * PW_DB ? PW_SW : PW_DW + 2 * PW_DB;
+constexpr uint32_t PW_FAIL = 0xFFFF0000u;        // exits >= this: the parse stopped
+constexpr uint32_t PW_SHORT = 0xFFFFFFFEu;       // ...at the end of the staged bytes (more follow)
+constexpr uint32_t PW_BAD = 0xFFFFFFFFu;         // ...on bytes that are not a planned block
+constexpr uint32_t PW_NCL = 8, PW_NSV = 32, PW_NONE = 0xFFFFFFFFu;
+static_assert(PW_NCL == 8, "small_caps(): 8 clients, 8 DeleteSet entries");
+
+struct PwLds {
+  uint32_t u[PW_UW];         // block stage | DeleteSet stage, values, metas (pos | canon << 16 | fine << 17 | n << 20)
+  uint32_t svt[2 * PW_NSV];  // remote state vector entries (client, clock)
+  uint32_t cl[CLW * PW_NCL]; // plan_doc's per-client records
+  uint32_t sec[SECW * PW_NCL];
+  uint32_t de[DEW * PW_NCL];
+  uint32_t keys[PW_NCL];
+};
+
+struct PwB {
+  uint32_t kind, len, info, ropos, rbytes;
+  bool ok;
+};
+// One block at window byte p (Update::decode_block, yrs/src/update.rs:433-488, with
+// ItemContent::decode of refs 1 / 4, block.rs:1786-1835): the position after it, or PW_SHORT /
+// PW_BAD.  The block is a short program of fields read by one loop (the lanes of a wave parse
+// different block kinds, so a branch per field kind would cost every lane every kind): 2 bits
+// per field, low end first -- 0 varint, 1 varint + that many bytes, 2 parent info (1 = a named
+// root: the two ID varints that follow become one string), 3 end.  FULL adds the plan checks
+// (o.ok): canonical varints, the info byte as re-encoded (Item::info, block.rs:1363-1369: 0x10
+// never, 0x20 only with a decoded parent_sub), parent info 0 / 1, ASCII strings (UTF-16 length
+// == byte length), non-zero length.
+template <bool FULL>
+YM_INLINE uint32_t pw_block(const uint32_t *w, uint32_t p, uint32_t lim, bool more, PwB &o) {
+  if (p >= lim) return more ? PW_SHORT : PW_BAD;
+  const uint32_t info = lds_byte(w, p), ref = info & 15;
+  // the content kinds planned here, tested first (a speculative parse rejects most wrong offsets
+  // on their first byte): GC, Deleted (1), String (4); Skip (info 10) is the general planner's
+  if (info != 0 && ref != 1 && ref != 4) return PW_BAD;
+  const uint32_t no = info & 0x80 ? 2u : 0u, nr = info & 0x40 ? 2u : 0u;
+  const bool par = info != 0 && (info & 0xC0) == 0, sub = par && (info & 0x20);
+  const uint32_t content = ref == 4 ? 1u : 0u;
+  uint32_t pat;
+  if (info == 0) {
+    pat = 0u | (3u << 2);
+  } else {
+    uint32_t sh = 2 * (no + nr); // origin / right origin: plain varints
+    pat = 0;
+    if (par) {
+      pat |= 2u << sh; // parent info, then an ID's two varints (or the root name)
+      sh += 6;
+      if (sub) {
+        pat |= 1u << sh;
+        sh += 2;
+      }
+    }
+    pat |= content << sh;
+    pat |= 3u << (sh + 2);
+  }
+  uint32_t q = p + 1, fi = 0, v = 0, st = 0, ropos = q, roend = q;
+  bool cn = true, pbad = false;
+  for (;;) {
+    const uint32_t k = pat & 3;
+    if (k == 3) break;
+    if (fi == no) ropos = q;
+    if (fi == no + nr) roend = q;
+    if (q >= lim) {
+      st = more ? PW_SHORT : PW_BAD;
+      break;
+    }
+    const VarR r = var_at(w, q, lim);
+    if (!r.fine) {
+      st = more && q + 5 > lim ? PW_SHORT : PW_BAD;
+      break;
+    }
+    cn &= r.canon;
+    v = r.v;
+    q += r.n;
+    if (k == 1) {
+      if (v > lim - q) {
+        st = more ? PW_SHORT : PW_BAD;
+        break;
+      }
+      q += v;
+    }
+    pat >>= 2;
+    if (k == 2) {
+      pbad = v > 1;
+      if (v == 1) pat = ((pat >> 4) << 2) | 1u; // the name string replaces the ID
+    }
+    fi++;
+  }
+  if (st) return st;
+  o.info = info;
+  o.kind = info == 0 ? BK_GC : BK_ITEM;
+  o.len = v;
+  o.ropos = ropos;
+  o.rbytes = roend - ropos;
+  if (FULL) {
+    bool ok = cn && !pbad && v != 0 && !(info & 0x10) && !((info & 0x20) && (info & 0xC0));
+    if (content && v > 1) { // String: ASCII (one byte: one UTF-16 unit whatever it is)
+      uint32_t hi = 0;
+      const uint32_t s0 = q - v, q0 = s0 >> 2, q1 = (q - 1) >> 2;
+      for (uint32_t k = q0; k <= q1; k++) {
+        uint32_t x = w[k];
+        if (k == q0) x &= 0xFFFFFFFFu << (8 * (s0 & 3));
+        if (k == q1 && (q & 3)) x &= 0xFFFFFFFFu >> (8 * (4 - (q & 3)));
+        hi |= x;
+      }
+      ok = ok && !(hi & 0x80808080u);
+    }
+    o.ok = ok;
+  }
+  return q;
+}
+// Speculative parse of one lane's chunk [cs, ce) from p (cs <= p): the block starts it visits
+// (mask) and where it leaves the chunk.  A parse that fails moves on by one byte, so the walk is
+// a function N of the position (N(x) = the end of the block at x when x parses, else x + 1)
+// and always leaves the chunk; from a true block start N follows the true blocks until one of
+// them fails, which the validating walk finds.
+// A lane's first parse starts PW_BURN bytes before its chunk (lane 0: at the true start), so a
+// wrong offset has that long to fall onto the true blocks before the chunk begins.
+YM_INLINE uint32_t pw_spec(const uint32_t *w, uint32_t p, uint32_t cs, uint32_t ce, uint32_t lim, bool more,
+                           uint64_t &mask) {
+  mask = 0;
+  PwB o;
+  while (p < ce) {
+    if (p >= cs) mask |= 1ull << (p - cs);
+    const uint32_t q = pw_block<false>(w, p, lim, more, o);
+    p = q >= PW_FAIL ? p + 1 : q;
+  }
+  return p;
+}
+
+// The DeleteSet of one update (IdSet::decode, id_set.rs:412-426) from update byte P on, read
+// by one wavefront: windows of PW_DB bytes staged in u (PW_DW + 2 PW_DB words); a ballot over
+// terminator bytes (bit 7 clear) splits a window into varints, a prefix sum numbers them, one
+// decode per varint start goes to LDS (value; position, canonical, fits-the-window flags,
+// length); the entry headers are then read in turn and each entry's ranges checked lane-parallel
+// (no u32 overflow; DIFF: squashed, canonical), its plan record written to de (DEW words, lane
+// 0).  false: a shape for k_plan (malformed, unsquashed, more than capE entries).
+template <bool DIFF>
+__device__ __noinline__ bool pw_deleteset(uint32_t *u, uint32_t *de, const uint8_t *up, uint32_t un, uint32_t P,
+                                          uint32_t lane, uint32_t capE, uint32_t &nds) {
+  const uintptr_t A0 = (uintptr_t)up;
+  int32_t wb = 0;
+  uint32_t lim = 0;
+  bool more = false;
+  auto stage = [&](uint32_t Q, uint32_t nbytes) {
+    wsync(); // every lane is done with the previous stage
+    const uintptr_t ab = (A0 + Q) & ~(uintptr_t)15;
+    wb = (int32_t)(int64_t)(ab - A0);
+    const uint32_t avail = (uint32_t)((int64_t)un - wb);
+    lim = avail < nbytes ? avail : nbytes;
+    more = avail > nbytes;
+    const uint4 *src = (const uint4 *)ab;
+    uint4 *dst = (uint4 *)u;
+    const uint32_t n16 = (lim + 15) >> 4;
+    for (uint32_t k = lane; k < n16; k += 64) dst[k] = src[k];
+    wsync();
+  };
+  uint32_t *val = u + PW_DW, *meta = u + PW_DW + PW_DB;
+  uint32_t nvar = 0, nfine = 0, kk = 0;
+  bool fshort = false;
+  auto ds_stage = [&](uint32_t Q) {
+    stage(Q, PW_DB);
+    const uint32_t off0 = (uint32_t)((int32_t)Q - wb), bq = 8 * lane;
+    const uint64_t x = ((uint64_t)u[2 * lane + 1] << 32) | u[2 * lane];
+    const uint32_t lo = off0 > bq ? (off0 - bq < 8 ? off0 - bq : 8u) : 0u;
+    const uint32_t hi = lim > bq ? (lim - bq < 8 ? lim - bq : 8u) : 0u;
+    const uint32_t vm = hi > lo ? ((1u << hi) - 1) & ~((1u << lo) - 1) : 0u;
+    uint32_t tm = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) tm |= (uint32_t)((~x >> (8 * k + 7)) & 1) << k;
+    tm &= vm;
+    const uint32_t pt = shfl(tm, (int)((lane + 63) & 63));
+    uint32_t sm = ((tm << 1) | (lane > 0 ? (pt >> 7) & 1 : 0u)) & 0xFF;
+    if (off0 >= bq && off0 < bq + 8) sm |= 1u << (off0 - bq);
+    sm &= vm;
+    const uint32_t cnt = (uint32_t)__builtin_popcount(sm);
+    const uint32_t inc = wincl(cnt, lane);
+    uint32_t idx = inc - cnt, firstbad = PW_NONE, m = sm;
+    while (m) {
+      const uint32_t k = (uint32_t)__builtin_ctz(m);
+      m &= m - 1;
+      const VarR r = var_at(u, bq + k, lim);
+      val[idx] = r.v;
+      meta[idx] = (bq + k) | (r.canon ? 1u << 16 : 0u) | (r.fine ? 1u << 17 : 0u) | (r.n << 20);
+      if (!r.fine && firstbad == PW_NONE) firstbad = idx;
+      idx++;
+    }
+    nvar = rdlane(inc, 63);
+    // the first varint that does not end inside the window: cut by the window end, or malformed
+    uint32_t fb = firstbad;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = shfl(fb, (int)(lane ^ (uint32_t)o));
+      fb = y < fb ? y : fb;
+    }
+    nfine = fb == PW_NONE ? nvar : fb;
+    wsync();
+    fshort = more && (nfine == nvar || (meta[nfine] & 0xFFFF) + 5 > lim);
+    kk = 0;
+  };
+  // varints [kk, kk + n) readable in this window: restage at varint kk when the window cut
+  // them; false = they are malformed or past the update's end (k_plan reports the error)
+  auto ds_need = [&](uint32_t n) -> bool {
+    if (kk + n <= nfine) return true;
+    if (!fshort) return false;
+    const uint32_t Q = kk < nvar ? (uint32_t)wb + (meta[kk] & 0xFFFF) : (uint32_t)wb + lim;
+    ds_stage(Q);
+    return kk + n <= nfine;
+  };
+  bool bail = false;
+  nds = 0;
+  ds_stage(P);
+  if (!ds_need(1)) bail = true;
+  else nds = val[kk++];
+  if (DIFF && nds > capE) bail = true;
+  for (uint32_t i = 0; i < nds && !bail; i++) {
+    if (!ds_need(2)) {
+      bail = true;
+      break;
+    }
+    const uint32_t client = val[kk], nr = val[kk + 1];
+    bool dcanon = (meta[kk + 1] >> 16) & 1;
+    const uint32_t cpos = (uint32_t)wb + (meta[kk + 1] & 0xFFFF);
+    uint32_t epos = cpos + (meta[kk + 1] >> 20);
+    kk += 2;
+    uint32_t dsz = varlen(nr), rr = nr, r0 = 0, prev_e = 0;
+    while (rr) {
+      if (kk + 2 > nfine && !ds_need(2)) {
+        bail = true;
+        break;
+      }
+      const uint32_t avail = (nfine - kk) / 2, m = rr < avail ? rr : avail;
+      bool bad = false, unsq = false, cn = true;
+      uint32_t sz = 0;
+      for (uint32_t r = lane; r < m; r += 64) {
+        const uint32_t s = val[kk + 2 * r], l = val[kk + 2 * r + 1];
+        cn &= (meta[kk + 2 * r] >> 16) & (meta[kk + 2 * r + 1] >> 16) & 1;
+        bad |= (uint64_t)s + l > 0xFFFFFFFFull;
+        const uint32_t pe = r == 0 ? prev_e : val[kk + 2 * r - 2] + val[kk + 2 * r - 1];
+        unsq |= (r0 + r > 0) && s < pe;
+        sz += varlen(s) + varlen(l);
+      }
+      if (__ballot(bad) || (DIFF && __ballot(unsq))) { // overflow: k_plan; unsquashed: squash of a clone
+        bail = true;
+        break;
+      }
+      dcanon = dcanon && !__ballot(!cn);
+      dsz += rdlane(wincl(sz, lane), 63);
+      prev_e = val[kk + 2 * m - 2] + val[kk + 2 * m - 1];
+      const uint32_t lm = meta[kk + 2 * m - 1];
+      epos = (uint32_t)wb + (lm & 0xFFFF) + (lm >> 20);
+      kk += 2 * m;
+      rr -= m;
+      r0 += m;
+    }
+    if (bail) break;
+    if (DIFF && lane == 0) {
+      uint32_t *r = de + DEW * i;
+      r[0] = client;
+      r[1] = cpos;
+      r[2] = epos;
+      r[3] = nr;
+      r[4] = 1u | (dcanon ? 2u : 0u);
+      r[5] = 0;
+      r[6] = 0;
+      r[7] = varlen(client) + dsz;
+    }
+  }
+  wsync();
+  return !bail;
+
+}
+
+// One document on one wavefront (all 64 lanes call it with the same d).
+template <bool DIFF>
+__device__ __noinline__ void pw_plan_doc(const DiffBatch &b, const PlanScratch &ps, PwLds &S, uint32_t lane,
+                                         uint32_t d) {
+  if (b.pre_status && b.pre_status[d]) { // e.g. a y-sync message that is not SyncStep1
+    if (lane == 0) {
+      ps.big[d] = 0;
+      ps.status[d] = b.pre_status[d];
+      ps.size[d] = 0;
+    }
+    return;
+  }
+  const uint64_t o0 = b.upd_off[d], o1 = b.upd_off[d + 1];
+  const uint8_t *up = b.bytes + o0;
+  const uint32_t un = (uint32_t)(o1 - o0);
+  uint32_t *scr = ps.small + (size_t)d * ps.small_words;
+  const PlanCaps cap = small_caps();
+  const PlanLayout L = plan_layout(cap);
+  bool bail = o1 - o0 >= (1ull << 31);
+  uint32_t nsv = 0;
+  if (DIFF && !bail) { // remote state vector, decoded before the update (alt.rs:77-78), by lane 0
+    uint32_t fl = 0;
+    if (lane == 0) {
+      const uint8_t *svp = b.sv + b.sv_off[d];
+      const uint32_t svn = (uint32_t)((b.sv_end ? b.sv_end[d] : b.sv_off[d + 1]) - b.sv_off[d]);
+      Cur s{svp, svn, 0};
+      bool cn;
+      uint32_t len = 0, clk, n = 0;
+      uint64_t c;
+      bool bl = rd_var_u32(s, len, cn) || (len && (uint64_t)buckets_for(len) * 17ull > ALLOC_LIMIT);
+      for (uint32_t i = 0; i < len && !bl; i++) {
+        if (rd_var_u64(s, c, cn) || rd_var_u32(s, clk, cn)) {
+          bl = true;
+          break;
+        }
+        if (c >> 32) continue; // no u32 block client can match it
+        uint32_t k = 0;
+        while (k < n && S.svt[2 * k] != (uint32_t)c) k++;
+        if (k == n) {
+          if (n == PW_NSV) {
+            bl = true;
+            break;
+          }
+          n++;
+        }
+        S.svt[2 * k] = (uint32_t)c; // a client listed twice keeps its last clock (HashMap::insert)
+        S.svt[2 * k + 1] = clk;
+      }
+      fl = (bl ? 1u : 0u) | (n << 8);
+    }
+    fl = rdlane(pin(fl), 0);
+    bail = fl & 1;
+    nsv = fl >> 8;
+    wsync();
+  }
+
+  // ---- staging: window byte p <-> update byte wb + p (wb: the 16-byte aligned base)
+  const uintptr_t A0 = (uintptr_t)up;
+  int32_t wb = 0;
+  uint32_t lim = 0;
+  bool more = false;
+  auto stage = [&](uint32_t P, uint32_t nbytes) {
+    wsync(); // every lane is done with the previous stage
+    const uintptr_t ab = (A0 + P) & ~(uintptr_t)15;
+    wb = (int32_t)(int64_t)(ab - A0);
+    const uint32_t avail = (uint32_t)((int64_t)un - wb);
+    lim = avail < nbytes ? avail : nbytes;
+    more = avail > nbytes;
+    const uint4 *src = (const uint4 *)ab;
+    uint4 *dst = (uint4 *)S.u;
+    const uint32_t n16 = (lim + 15) >> 4;
+    for (uint32_t k = lane; k < n16; k += 64) dst[k] = src[k];
+    wsync();
+  };
+  // a header varint (re-emitted from its value: canonical form not required) at update byte P
+  auto hdr_var = [&](uint32_t &P, uint32_t &v) -> bool {
+    uint32_t p = (uint32_t)((int32_t)P - wb);
+    if (p + 16 > lim && more) {
+      stage(P, PW_SB);
+      p = (uint32_t)((int32_t)P - wb);
+    }
+    const VarR r = var_at(S.u, p, lim);
+    if (p >= lim || !r.fine) return false;
+    v = r.v;
+    P += r.n;
+    return true;
+  };
+
+  uint32_t P = 0, ncl = 0, nclients = 0, nsec = 0, nds = 0;
+  uint32_t n_win = 0, n_round = 0; // diagnostic stamps (YMERGE_STAMPS): windows, stitch rounds
+  if (!bail) {
+    stage(0, PW_SB);
+    if (!hdr_var(P, ncl) || ncl > cap.C) bail = true;
+  }
+  // ---- client sections
+  for (uint32_t isec = 0; isec < ncl && !bail; isec++) {
+    uint32_t nb, client, clock;
+    if (!hdr_var(P, nb) || !hdr_var(P, client) || !hdr_var(P, clock)) {
+      bail = true;
+      break;
+    }
+    uint32_t e = nclients;
+    for (uint32_t f = 0; f < nclients; f++)
+      if (S.keys[f] == client) {
+        e = f;
+        break;
+      }
+    if (e == nclients) { // entry(..).or_default (the hash table is replayed after the walk)
+      if (nclients == PW_NCL) {
+        bail = true;
+        break;
+      }
+      nclients++;
+      wsync();
+      if (lane < CLW) {
+        uint32_t v = 0;
+        if (DIFF && lane == 4)
+          for (uint32_t k = 0; k < nsv; k++)
+            if (S.svt[2 * k] == client) v = S.svt[2 * k + 1];
+        S.cl[CLW * e + lane] = v;
+      }
+      if (lane == 0) S.keys[e] = client;
+      wsync();
+    }
+    uint32_t *cr = S.cl + CLW * e;
+    const uint32_t nstored = cr[0], remote = cr[4];
+    uint32_t lkind = cr[1] & 0xFF, lclock = cr[2], llen = cr[3], found = cr[5], count = cr[10];
+    if (((uint64_t)nstored + nb) * 32ull > ALLOC_LIMIT || nsec >= cap.C) {
+      bail = true;
+      break;
+    }
+    uint32_t kb = PW_NONE, R = nb;
+    uint64_t clk = clock;
+    while (R && !bail) {
+      // ---- one window of this section's blocks, from the true block start P
+      stage(P, PW_SB);
+      n_win++;
+      const uint32_t off0 = (uint32_t)((int32_t)P - wb);
+      const uint32_t cs = off0 + PW_C * lane, ce = cs + PW_C;
+      uint64_t mask;
+      uint32_t ex = pw_spec(S.u, lane == 0 ? cs : (cs - PW_BURN > off0 ? cs - PW_BURN : off0), cs, ce, lim, more,
+                            mask);
+      uint32_t t = cs;
+      for (;;) { // stitch: until every lane agrees with its predecessor's exit
+        const uint32_t pex = shfl(ex, (int)((lane + 63) & 63));
+        t = lane == 0 ? off0 : pex;
+        const bool cons = lane == 0 || t >= ce || ((mask >> (t - cs)) & 1);
+        if (!__ballot(!cons)) break;
+        n_round++;
+        if (!cons) { // parse again from the entry until it meets the chain already parsed
+          uint64_t nm = 0;
+          uint32_t p = t;
+          PwB o;
+          while (p < ce) {
+            if ((mask >> (p - cs)) & 1) { // merged: the rest of the chain and the exit stand
+              nm |= mask & (~0ull << (p - cs));
+              p = ex;
+              break;
+            }
+            nm |= 1ull << (p - cs);
+            const uint32_t q = pw_block<false>(S.u, p, lim, more, o);
+            p = q >= PW_FAIL ? p + 1 : q;
+          }
+          mask = nm;
+          ex = p;
+        }
+      }
+      // this lane's block starts from its true entry on (true blocks up to the first that fails)
+      mask = t >= ce ? 0ull : mask & (~0ull << (t - cs));
+      const uint32_t cnt = (uint32_t)__builtin_popcountll(mask);
+      const uint32_t inc = wincl(cnt, lane), exc = inc - cnt, tot = rdlane(inc, 63);
+      const uint32_t nw0 = R < tot ? R : tot;
+      // ---- validating walk of the true blocks, clock lengths
+      const uint32_t k = exc < nw0 ? (cnt < nw0 - exc ? cnt : nw0 - exc) : 0u;
+      uint32_t p = t, lkd = 0, lcl = 0, lln = 0, j = 0, fst = 0;
+      uint64_t sum = 0;
+      for (; j < k; j++) {
+        PwB o;
+        const uint32_t q = pw_block<true>(S.u, p, lim, more, o);
+        if (q >= PW_FAIL || !o.ok) {
+          fst = q == PW_SHORT ? PW_SHORT : PW_BAD;
+          break;
+        }
+        lkd = o.kind;
+        lcl = (uint32_t)sum;
+        lln = o.len;
+        sum += o.len;
+        p = q;
+      }
+      // the first block of the window that fails: past the stage -> the window ends before it;
+      // not a planned block -> k_plan
+      uint32_t nw = nw0;
+      const uint64_t fm = __ballot(fst != 0);
+      if (fm) {
+        const uint32_t fl = (uint32_t)__builtin_ctzll(fm);
+        const uint32_t gf = rdlane(exc + j, fl);
+        if (rdlane(fst, fl) == PW_BAD || gf == 0) {
+          bail = true;
+          break;
+        }
+        nw = gf;
+      }
+      if (exc >= nw) { // blocks past the window's last committed one
+        sum = 0;
+        j = 0;
+      }
+      if (__ballot(sum >= (1ull << 25))) { // keeps the wave's clock sums in u32 (longer runs: k_plan)
+        bail = true;
+        break;
+      }
+      const uint32_t kw = j; // blocks this lane commits
+      const uint32_t s32 = (uint32_t)sum;
+      const uint32_t cinc = wincl(s32, lane), cexc = cinc - s32, ctot = rdlane(cinc, 63);
+      if (clk + ctot > 0xFFFFFFFFull) { // clock += len would overflow (a debug-build panic)
+        bail = true;
+        break;
+      }
+      const uint32_t lastl = (uint32_t)__builtin_ctzll(__ballot(kw > 0 && exc + kw == nw));
+      lkind = rdlane(lkd, lastl);
+      lclock = (uint32_t)clk + rdlane(cexc + lcl, lastl);
+      llen = rdlane(lln, lastl);
+      const uint32_t pend = rdlane(p, lastl);
+      if (DIFF) {
+        if (found) {
+          if (kb == PW_NONE) kb = P; // a section after the one holding the client's first diff block
+          count += nw;
+        } else {
+          // Update::encode_diff: the first block whose end passes the remote clock
+          const uint64_t fmask = __ballot(kw > 0 && clk + cexc + sum > (uint64_t)remote);
+          if (fmask) {
+            const uint32_t fl = (uint32_t)__builtin_ctzll(fmask);
+            uint32_t jf = 0, kbw = 0;
+            if (lane == fl) {
+              uint32_t q = t, c = (uint32_t)clk + cexc;
+              for (uint32_t jj = 0; jj < kw; jj++) {
+                PwB o;
+                const uint32_t qn = pw_block<true>(S.u, q, lim, more, o);
+                if ((uint64_t)c + o.len > remote) {
+                  const uint32_t off = remote > c ? remote - c : 0u;
+                  const uint32_t blen = qn - q;
+                  uint32_t sz;
+                  if (off == 0) {
+                    sz = blen;
+                  } else if (o.kind != BK_ITEM) {
+                    sz = 1 + varlen(o.len - off);
+                  } else { // ItemSlice::encode with an offset (see the ring planner)
+                    const uint32_t rest = o.len - off;
+                    sz = 1 + varlen(client) + varlen(c + off - 1) + o.rbytes + varlen(rest) +
+                         ((o.info & 15) == 4 ? rest : 0u);
+                  }
+                  uint32_t *sr = S.cl + CLW * e;
+                  sr[6] = (uint32_t)wb + q;
+                  sr[7] = c;
+                  sr[8] = o.len;
+                  sr[9] = off;
+                  sr[11] = sz;
+                  if (off == 0) {
+                    sr[14] = 1;
+                  } else if (o.kind == BK_ITEM) {
+                    const uint32_t has_ps = (o.info & 0xE0) == 0x20 ? 1u : 0u;
+                    sr[12] = (uint32_t)wb + o.ropos;
+                    sr[13] = o.rbytes | ((o.info & 15) << 8) | (has_ps << 12) | ((qn - o.ropos) << 16);
+                    sr[14] = 2;
+                  }
+                  jf = jj;
+                  kbw = qn;
+                  break;
+                }
+                c += o.len;
+                q = qn;
+              }
+            }
+            jf = rdlane(pin(jf), fl);
+            kbw = rdlane(pin(kbw), fl);
+            wsync();
+            found = 1;
+            count = nw - (rdlane(exc, fl) + jf); // the found block and every later one of the window
+            kb = (uint32_t)wb + kbw;
+          }
+        }
+      }
+      R -= nw;
+      clk += ctot;
+      P = (uint32_t)wb + pend;
+    }
+    if (bail) break;
+    // ---- section record (plan_doc's sec / cl updates)
+    if (kb == PW_NONE) kb = P;
+    wsync();
+    if (lane == 0) {
+      uint32_t *sr = S.sec + SECW * nsec;
+      sr[0] = e;
+      sr[1] = kb;
+      sr[2] = P;
+      sr[3] = 1;
+      sr[4] = P - kb;
+      cr[0] = nstored + nb;
+      cr[1] = lkind | 0x100;
+      cr[2] = lclock;
+      cr[3] = llen;
+      cr[5] = found;
+      cr[10] = count;
+    }
+    nsec++;
+    wsync();
+  }
+
+  // ---- DeleteSet
+  if (!bail) bail = !pw_deleteset<DIFF>(S.u, S.de, up, un, P, lane, cap.E, nds);
+
+  // ---- the plan (lane 0): scratch records, hash tables replayed in yrs' insertion order
+  if (lane != 0) return;
+  if (!bail) {
+    for (uint32_t f = 0; f < nclients; f++) {
+      scr[L.ct_keys + f] = S.keys[f];
+      for (uint32_t k = 0; k < CLW; k++) scr[L.cl + CLW * f + k] = S.cl[CLW * f + k];
+    }
+    for (uint32_t s = 0; s < nsec * SECW; s++) scr[L.sec + s] = S.sec[s];
+    if (DIFF)
+      for (uint32_t s = 0; s < nds * DEW; s++) scr[L.de + s] = S.de[s];
+    GHB ct{scr + L.ct_slot, scr + L.ct_keys, L.BC, 0, 0, 0};
+    GHB dt{scr + L.dt_slot, scr + L.dt_keys, L.BE, 0, 0, 0};
+    if (ncl && !ct.reserve(ncl, scr + L.ct_tmp)) bail = true;
+    for (uint32_t f = 0; f < nclients && !bail; f++) {
+      if (!ct.reserve(1, scr + L.ct_tmp)) bail = true;
+      else ct.place(ct.keys[f], f);
+    }
+    if (DIFF) {
+      const uint32_t *de = scr + L.de;
+      for (uint32_t i = 0; i < nds && !bail; i++) {
+        const uint32_t dc = de[DEW * i];
+        if (!dt.reserve(1, scr + L.dt_tmp)) {
+          bail = true;
+          break;
+        }
+        const int f = dt.find(dc);
+        if (f >= 0) { // replaced in place: the slot now names entry i
+          for (uint32_t s = 0; s < dt.buckets; s++)
+            if (dt.slot[s] == (uint32_t)f + 1) dt.slot[s] = i + 1;
+          dt.keys[i] = dc;
+        } else {
+          dt.place(dc, i);
+        }
+      }
+    }
+    if (!bail) {
+      uint64_t sz = 0;
+      const uint32_t stt = plan_finish<DIFF>(scr, L, cap, ct, nsec, dt, false, 0u, sz);
+      if (stt == PLAN_OVF) {
+        bail = true;
+      } else {
+        if (b.frame && !stt) sz += 2 + varlen(sz); // y-sync message framing
+        ps.big[d] = 0;
+        ps.status[d] = (uint8_t)stt;
+        ps.size[d] = stt ? 0 : sz;
+      }
+    }
+  }
+  if (bail) ps.big[d] = PLAN_REDO;
+  if (ps.stamps) {
+    uint64_t *o = ps.stamps + (size_t)d * 16;
+    o[0] = n_win;
+    o[1] = n_round;
+    o[2] = bail ? 1 : 0;
+    o[5] = un;
+    o[7] = 0xD1FE;
+  }
+}
+
+
+// Documents of >= PW_MIN bytes (listed by k_plan_lane; every document when ps.wave_list is
+// null), a wavefront each, grid-stride.
+template <bool DIFF>
+__global__ void __launch_bounds__(64 * PW_WPB) k_plan_wave(DiffBatch b, PlanScratch ps) {
+  ym_set_grammar(b.v1x);
+  __shared__ __align__(16) PwLds lds_all[PW_WPB];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t n = ps.wave_list ? *ps.wave_n : b.n_docs;
+  for (uint32_t i = blockIdx.x * PW_WPB + wv; i < n; i += gridDim.x * PW_WPB)
+    pw_plan_doc<DIFF>(b, ps, lds_all[wv], lane, ps.wave_list ? ps.wave_list[i] : i);
+}
+
+// k_plan_lane: the ring planner's lane-per-document walk (a lane per document is the
+// cheapest walk in parse steps: a wavefront per document needs ~10x more, k_plan_wave above)
+// without the two costs that held the ring planner at ~570 VALU + ~450 SALU instructions per
+// item step (SQ counters, profiles/r04/r04h_*): per-field branches that the 64 documents of a
+// wave take differently (every step paid for every kind), and the DeleteSet walked range by
+// range in the same loop.
+//   * A block of the common kinds (GC; an Item with an origin and / or right origin and
+//     Deleted or String content) is parsed straight-line from a 32-byte window of its ring:
+//     per-byte masks (varint terminators, zero bytes, bytes >= 16) with a multiply per dword,
+//     the content length's end as the n-th terminator, the canonical-varint checks as mask
+//     algebra, the ASCII check as one mask test.  Everything else -- section headers,
+//     parent-form or re-encoded blocks, blocks longer than the window, a section's last block,
+//     the client's first diff block -- takes the full step (one field-program loop).
+//   * A lane stops at its DeleteSet; the wavefront then reads its documents' DeleteSets in
+//     turn, all 64 lanes on one (pw_deleteset).
+// Same shapes, records and plans as the ring planner.
+template <bool DIFF>
+__global__ void __launch_bounds__(RING_NT) k_plan_lane(DiffBatch b, PlanScratch ps) {
+  ym_set_grammar(b.v1x);
+  __shared__ __align__(16) uint32_t ring_lds[RING_NT * RING_STRIDE / 4];
+  const uint32_t t = threadIdx.x;
+  const uint32_t d = blockIdx.x * RING_NT + t;
+  uint32_t *row = ring_lds + t * (RING_STRIDE / 4);
+  bool active = d < b.n_docs;
+  if (active && b.pre_status && b.pre_status[d]) { // e.g. a y-sync message that is not SyncStep1
+    ps.big[d] = 0;
+    ps.status[d] = b.pre_status[d];
+    ps.size[d] = 0;
+    active = false;
+  }
+  if (active && ps.wave_list && b.upd_off[d + 1] - b.upd_off[d] >= PW_MIN) { // one long update: k_plan_wave
+    ps.big[d] = PLAN_WAVE;
+    ps.wave_list[atomicAdd(ps.wave_n, 1u)] = d;
+    active = false;
+  }
+  const uint8_t *up = nullptr, *svp = nullptr;
+  uint32_t un = 0, svn = 0, nsv = 0;
+  uint32_t *scr = nullptr;
+  const PlanCaps cap = small_caps();
+  const PlanLayout L = plan_layout(cap);
+  bool bail = false;
+  if (active) {
+    const uint64_t o0 = b.upd_off[d], o1 = b.upd_off[d + 1];
+    up = b.bytes + o0;
+    un = (uint32_t)(o1 - o0);
+    if (o1 - o0 >= (1ull << 31)) bail = true;
+    scr = ps.small + (size_t)d * ps.small_words;
+    if (DIFF && !bail) { // remote state vector, decoded before the update (alt.rs:77-78)
+      svp = b.sv + b.sv_off[d];
+      svn = (uint32_t)((b.sv_end ? b.sv_end[d] : b.sv_off[d + 1]) - b.sv_off[d]);
+      // entries with a u32 client id go to a small table (the sq region: unsquashed ranges
+      // are the general planner's); a client listed twice keeps its last clock (HashMap::insert)
+      Cur s{svp, svn, 0};
+      bool cn;
+      uint32_t len = 0, clk;
+      uint64_t c;
+      if (rd_var_u32(s, len, cn) || (len && (uint64_t)buckets_for(len) * 17ull > ALLOC_LIMIT)) bail = true;
+      uint32_t *svt = scr + L.sq;
+      for (uint32_t i = 0; i < len && !bail; i++) {
+        if (rd_var_u64(s, c, cn) || rd_var_u32(s, clk, cn)) {
+          bail = true;
+          break;
+        }
+        if (c >> 32) continue;
+        uint32_t k = 0;
+        while (k < nsv && svt[2 * k] != (uint32_t)c) k++;
+        if (k == nsv) {
+          if (nsv == cap.R / 2) {
+            bail = true;
+            break;
+          }
+          nsv++;
+        }
+        svt[2 * k] = (uint32_t)c;
+        svt[2 * k + 1] = clk;
+      }
+    }
+    if (bail) active = false;
+  }
+  GHB ct{scr + L.ct_slot, scr + L.ct_keys, L.BC, 0, 0, 0};
+  GHB dt{scr + L.dt_slot, scr + L.dt_keys, L.BE, 0, 0, 0};
+  uint32_t *cl = scr + L.cl, *sec = scr + L.sec, *de = scr + L.de;
+  uint32_t st = R_NCL, pos = 0, ncl = 0, isec = 0, nb = 0, j = 0, client = 0, clock = 0, nclients = 0;
+  // current section (plan_doc's per-client record, kept in registers while the section runs)
+  uint32_t e = 0, nstored = 0, lkind = 0, lclock = 0, llen = 0, remote = 0, found = 0, count = 0, kb = 0, pure = 1,
+           ssize = 0, nsec = 0;
+  uint32_t nds = 0;
+  RingRd R{row, (uint64_t)up, 0, 0, (uint64_t)up + un, un, F_OK, 0, 0};
+  bool have = false, wait = false, need_slow = false;
+
+  // diagnostic stamps (wave time): refill, steps, finish; refill rounds, step iterations
+  uint64_t t_ref = 0, t_stp = 0, n_ref = 0, n_stp = 0, tq = ps.stamps ? __builtin_amdgcn_s_memtime() : 0;
+  for (;;) {
+    if (!__any(active)) break;
+    if (ps.stamps) tq = __builtin_amdgcn_s_memtime();
+    // ---- refill point: lanes that ran short, or are within 64 bytes of their ring's end
+    const uint64_t a0 = R.sbase + pos;
+    if (active && (!have || wait || (a0 + 64 > R.rb + RING && R.rb + RING < R.send))) {
+      if (have && wait && R.rb == (a0 & ~15ull)) { // an item longer than a fresh ring
+        bail = true;
+        active = false;
+      } else {
+        R.rb = a0 & ~15ull;
+        const uint4 *q = (const uint4 *)R.rb;
+        uint4 *dst = (uint4 *)row;
+#pragma unroll
+        for (uint32_t g = 0; g < RING / 16; g += RING_G) { // groups of 16-byte loads
+          uint4 x[RING_G];
+#pragma unroll
+          for (uint32_t k = 0; k < RING_G; k++)
+            x[k] = R.rb + 16 * (g + k) < R.send ? q[g + k] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+          for (uint32_t k = 0; k < RING_G; k++) dst[g + k] = x[k];
+        }
+        R.rend = R.rb + RING < R.send ? R.rb + RING : R.send;
+        R.sync_rel();
+        have = true;
+        wait = false;
+      }
+    }
+    if (ps.stamps) {
+      const uint64_t now = __builtin_amdgcn_s_memtime();
+      t_ref += now - tq;
+      tq = now;
+      n_ref++;
+    }
+    for (uint32_t step = 0; step < RING_STEPS; step++) {
+      const bool can = active && !wait;
+      if (!__any(can)) break;
+      if (ps.stamps) n_stp++;
+      bool fast_done = false;
+      if (can && !need_slow && st == R_BLOCK && !(ps.lane_dbg & 1)) {
+        // ---- fast step: a block of the common kinds, straight-line from a 32-byte window of the
+        //      ring (every lane runs the same instructions whatever its block's kind)
+        const int32_t o = (int32_t)pos - R.rbq;
+        if (!(o >= 0 && o + 36 <= (int32_t)RING_STRIDE && ((int32_t)pos + 32 <= R.rendq || R.rendq == (int32_t)un))) {
+          wait = true; // the window runs past the ring: refill first
+        } else {
+          const uint32_t *wr = row + (o >> 2);
+          const uint32_t sh = (uint32_t)o & 3;
+          uint32_t x[8];
+          {
+            uint32_t a[9];
+#pragma unroll
+            for (int k = 0; k < 9; k++) a[k] = wr[k];
+#pragma unroll
+            for (int k = 0; k < 8; k++) x[k] = __builtin_amdgcn_alignbyte(a[k + 1], a[k], sh);
+          }
+          // byte masks, bit i = window byte i: varint terminators (bit 7 clear), zero bytes,
+          // bytes of 16 and more (their low 7 bits); one multiply gathers a dword's four bits
+          uint32_t T0 = 0, Z = 0, G = 0;
+#pragma unroll
+          for (int k = 0; k < 8; k++) {
+            const uint32_t dw = x[k];
+            const uint32_t nz = (((dw & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | dw) & 0x80808080u;
+            const uint32_t ge = ((dw & 0x70707070u) + 0x70707070u) & 0x80808080u;
+            T0 |= (((((~dw & 0x80808080u) >> 7) * 0x204081u) >> 21) & 0xFu) << (4 * k);
+            Z |= (((((~nz & 0x80808080u) >> 7) * 0x204081u) >> 21) & 0xFu) << (4 * k);
+            G |= ((((ge >> 7) * 0x204081u) >> 21) & 0xFu) << (4 * k);
+          }
+          const uint32_t info = x[0] & 0xFF, ref = info & 15;
+          const bool gc = info == 0, str = !gc && ref == 4;
+          // GC, or an Item with an origin and / or a right origin (no parent info), Deleted or
+          // String content, info byte as re-encoded (no 0x10; 0x20 only with a parent)
+          const bool shape = gc || ((info & 0x30) == 0 && (info & 0xC0) != 0 && (ref == 1 || ref == 4));
+          const uint32_t nv = gc ? 1u : (info & 0x80 ? 2u : 0u) + (info & 0x40 ? 2u : 0u) + 1u;
+          const uint32_t T = T0 & ~1u, B = T0 | 1u; // B: where a varint may start after
+          uint32_t tt = T, s = 0;
+#pragma unroll
+          for (uint32_t k = 1; k < 5; k++) { // s = end of the varint before the last (0: info)
+            const uint32_t c = (uint32_t)__builtin_ctz(tt | 0x80000000u);
+            s = k < nv ? c : s;
+            tt = k < nv ? tt & (tt - 1) : tt;
+          }
+          const uint32_t e = tt ? (uint32_t)__builtin_ctz(tt) : 32u; // end of the content length
+          const uint32_t R1 = e < 31 ? (2u << e) - 2u : 0xFFFFFFFEu;
+          // canonical varints only (the block is copied verbatim): a multi-byte varint does not
+          // end in a zero byte, none is longer than 5 bytes, a 5-byte one ends below 16
+          const uint32_t multi = T & R1 & ~(B << 1);
+          const uint32_t ge5 = multi & ~(B << 2) & ~(B << 3) & ~(B << 4);
+          const bool canon = ((multi & Z) | (ge5 & ~(B << 5)) | (ge5 & G)) == 0;
+          const uint32_t n = e - s;
+          const uint64_t xv = ring_read8(row, (uint32_t)o + (s < 31 ? s + 1 : 0u));
+          const uint64_t xm = xv & (n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1));
+          const uint32_t len = (uint32_t)((xm & 0x7F) | ((xm >> 1) & 0x3F80) | ((xm >> 2) & 0x1FC000) |
+                                          ((xm >> 3) & 0xFE00000) | ((xm >> 4) & 0x7F0000000ull));
+          const bool fits = !str || (e < 32 && len <= 31 - e);
+          const uint32_t pm = str && fits && len > 1 ? ((1u << len) - 1u) << (e + 1) : 0u;
+          const uint32_t blen = e + 1 + (str ? len : 0u);
+          bool fast = shape && e < 32 && canon && len != 0 && fits && (pm & ~T0) == 0 && blen <= un - pos &&
+                      (uint64_t)clock + len <= 0xFFFFFFFFull && j + 1 < nb;
+          if (DIFF) fast = fast && (found || clock + len <= remote); // the first diff block: the full step
+          if (fast) {
+            nstored++;
+            lkind = gc ? BK_GC : BK_ITEM;
+            lclock = clock;
+            llen = len;
+            if (DIFF && found) {
+              if (kb == 0xFFFFFFFFu) kb = pos;
+              count++;
+              ssize += blen;
+            }
+            clock += len;
+            pos += blen;
+            j++;
+            fast_done = true;
+          } else {
+            need_slow = true;
+          }
+        }
+      } else if (can && st != R_BLOCK) {
+        need_slow = true;
+      } else if (can && (ps.lane_dbg & 1)) {
+        need_slow = true;
+      }
+      // ---- full step (section headers, other block shapes, a section's last block, the
+      //      client's first diff block), batched: it runs once enough lanes wait for it or no
+      //      lane made progress, so a wave pays for it once per LP_SLOW lanes, not once per step
+      const uint64_t slow_m = __ballot(can && need_slow);
+      if (!slow_m) continue;
+      if ((uint32_t)__builtin_popcountll(slow_m) < LP_SLOW && __ballot(fast_done)) continue;
+      if (!(can && need_slow)) continue;
+      need_slow = false;
+      R.fail = F_OK;
+      bool cn, sec_end = false;
+      // ---- the item's field program: one loop reads the varints of every item kind (lanes of
+      //      a wave sit on different kinds -- string blocks, DeleteSet ranges, headers -- and run
+      //      the same instructions); 2 bits per field, low end first: 0 varint, 1 varint + that
+      //      many bytes, 2 parent info (1: the ID's two varints become the root name), 3 end
+      uint32_t q = pos, info = 0, pat, no = 0, nr2 = 0;
+      if (st == R_BLOCK) {
+        info = (uint32_t)(R.at(q) & 0xFF);
+        q++;
+        const uint32_t ref = info & 15;
+        if (info == 0 || info == 10) {
+          pat = 0u | (3u << 2); // GC / Skip: length
+        } else {
+          if (ref != 1 && ref != 4 && !R.fail) R.fail = F_BAIL; // cold content kinds: general planner
+          no = info & 0x80 ? 2u : 0u;
+          nr2 = info & 0x40 ? 2u : 0u;
+          uint32_t sh = 2 * (no + nr2);
+          pat = 0;
+          if ((info & 0xC0) == 0) {
+            pat |= 2u << sh;
+            sh += 6;
+            if (info & 0x20) {
+              pat |= 1u << sh;
+              sh += 2;
+            }
+          }
+          pat |= (ref == 4 ? 1u : 0u) << sh;
+          pat |= 3u << (sh + 2);
+        }
+      } else {
+        pat = st == R_SEC ? 3u << 6 : (st == R_DENT || st == R_DRANGE) ? 3u << 4 : 3u << 2;
+      }
+      uint32_t fi = 0, v = 0, f0 = 0, f1 = 0, f2 = 0, ropos = q, roend = q, p1 = q, ncan = 0;
+      bool pbad = false;
+      for (;;) {
+        const uint32_t k = pat & 3;
+        if (k == 3 || R.fail) break;
+        if (fi == no) ropos = q;
+        if (fi == no + nr2) roend = q;
+        if (fi == 1) p1 = q;
+        const uint32_t n = R.var(q, v, cn);
+        if (R.fail) break;
+        ncan |= (cn ? 0u : 1u) << fi;
+        q += n;
+        f0 = fi == 0 ? v : f0;
+        f1 = fi == 1 ? v : f1;
+        f2 = fi == 2 ? v : f2;
+        if (k == 1) {
+          if (v > un - q) {
+            R.fail = F_BAIL;
+            break;
+          }
+          q += v;
+        }
+        pat >>= 2;
+        if (k == 2) {
+          pbad = v > 1;
+          if (v == 1) pat = ((pat >> 4) << 2) | 1u; // the name string replaces the ID
+        }
+        fi++;
+      }
+      if (st == R_BLOCK) {
+        // ---- one block (Update::decode_block, update.rs:433-488 + ItemContent::decode)
+        const uint32_t kind = info == 0 ? BK_GC : info == 10 ? BK_SKIP : BK_ITEM, len = v;
+        const uint32_t rbytes = roend - ropos;
+        bool reenc = ncan != 0;
+        if (kind == BK_ITEM) {
+          // 0x10 never re-emitted; 0x20 only when parent_sub was decoded; parent info 0 / 1
+          reenc |= pbad || (info & 0x10) || ((info & 0x20) && (info & 0xC0));
+          if ((info & 15) == 4 && !R.fail && len > 1) { // len == 1: one UTF-16 unit whatever the byte
+            uint64_t hib = 0;
+            const uint32_t s0 = q - len;
+            const uint64_t a = R.sbase + s0;
+            if (a + len + 8 <= R.rend || (R.rend == R.send && a + len <= R.rend)) {
+              for (uint32_t k = 0; k < len; k += 8) {
+                const uint32_t n8 = len - k < 8 ? len - k : 8;
+                hib |= ring_read8(row, (uint32_t)(a + k - R.rb)) & (n8 == 8 ? ~0ull : ((1ull << (8 * n8)) - 1));
+              }
+            } else { // payload past the ring: read it from HBM (the lane refills after it)
+              for (uint32_t k = 0; k < len; k++) hib |= up[s0 + k];
+              wait = true;
+            }
+            if (hib & 0x8080808080808080ull) R.fail = F_BAIL; // non-ASCII: UTF-16 length / split checks
+          }
+        }
+        if (!R.fail && reenc) R.fail = F_BAIL; // re-encoded sizes: general planner
+        if (!R.fail) {
+          const uint32_t bpos = pos, blen = q - pos;
+          pos = q;
+          if (kind == BK_ITEM && len == 0) { // Item::new -> None: dropped
+            if (kb != 0xFFFFFFFFu) pure = 0;
+          } else if ((uint64_t)clock + len > 0xFFFFFFFFull) {
+            R.fail = F_BAIL;
+          } else {
+            nstored++;
+            lkind = kind;
+            lclock = clock;
+            llen = len;
+            if (DIFF) {
+              if (!found) {
+                if (kind != BK_SKIP && clock + len > remote) {
+                  found = 1;
+                  const uint32_t off = remote > clock ? remote - clock : 0;
+                  uint32_t sz;
+                  if (off == 0) {
+                    sz = blen;
+                  } else if (kind != BK_ITEM) {
+                    sz = 1 + varlen(len - off);
+                  } else {
+                    // ItemSlice::encode with an offset (emit_block): origin (client, clock + off - 1)
+                    // synthesised, right origin copied (canonical here), no parent info, content
+                    // sliced (ASCII string: byte offset = UTF-16 offset)
+                    const uint32_t rest = len - off;
+                    sz = 1 + varlen(client) + varlen(clock + off - 1) + rbytes + varlen(rest) +
+                         ((info & 15) == 4 ? rest : 0u);
+                  }
+                  uint32_t *sr = cl + CLW * e;
+                  sr[6] = bpos;
+                  sr[7] = clock;
+                  sr[8] = len;
+                  sr[9] = off;
+                  sr[11] = sz;
+                  if (off == 0) {
+                    sr[14] = 1;
+                  } else if (kind == BK_ITEM) { // OP_SLICE: right origin bytes, ref, parent_sub flag
+                    const uint32_t has_ps = (info & 0xE0) == 0x20 ? 1u : 0u;
+                    sr[12] = ropos;
+                    sr[13] = rbytes | ((info & 15) << 8) | (has_ps << 12) | ((pos - ropos) << 16);
+                    sr[14] = 2;
+                  }
+                  count = 1;
+                  kb = pos;
+                }
+              } else {
+                if (kb == 0xFFFFFFFFu) kb = bpos;
+                count++;
+                ssize += blen;
+              }
+            }
+            clock += len;
+          }
+          if (!R.fail && ++j == nb) sec_end = true;
+        }
+      } else if (st == R_SEC) {
+        // ---- section header: blocks count, client, first clock
+        nb = f0;
+        client = f1;
+        clock = f2;
+        if (!R.fail) {
+          pos = q;
+          uint32_t f = 0;
+          while (f < nclients && ct.keys[f] != client) f++;
+          if (f == nclients) { // entry(..).or_default (the table itself is built after the walk)
+            nclients++;
+            ct.keys[f] = client;
+            uint32_t *sr = cl + CLW * f;
+            for (uint32_t k = 0; k < CLW; k++) sr[k] = 0;
+            if (DIFF) {
+              const uint32_t *svt = scr + L.sq;
+              uint32_t rc = 0;
+              for (uint32_t k = 0; k < nsv; k++)
+                if (svt[2 * k] == client) rc = svt[2 * k + 1];
+              sr[4] = rc;
+            }
+          }
+          e = f;
+          const uint32_t *sr = cl + CLW * e;
+          nstored = sr[0];
+          lkind = sr[1];
+          lclock = sr[2];
+          llen = sr[3];
+          remote = sr[4];
+          found = sr[5];
+          count = sr[10];
+          if (((uint64_t)nstored + nb) * 32ull > ALLOC_LIMIT || nsec >= cap.C) R.fail = F_BAIL;
+          kb = 0xFFFFFFFFu;
+          pure = 1;
+          ssize = 0;
+          j = 0;
+          if (nb) st = R_BLOCK;
+          else sec_end = true;
+        }
+      } else if (st == R_NCL) {
+        ncl = f0;
+        if (!R.fail && ncl > cap.C) R.fail = F_BAIL;
+        if (!R.fail) {
+          pos = q;
+          st = ncl ? R_SEC : R_NDS;
+        }
+      }
+      if (R.fail == F_SHORT) { // nothing consumed: the item is read again after the refill
+        wait = true;
+        continue;
+      }
+      if (R.fail) {
+        bail = true;
+        active = false;
+        continue;
+      }
+      if (sec_end) {
+        if (kb == 0xFFFFFFFFu) kb = pos;
+        uint32_t *sr = sec + SECW * nsec++;
+        sr[0] = e;
+        sr[1] = kb;
+        sr[2] = pos;
+        sr[3] = pure;
+        sr[4] = ssize;
+        uint32_t *cr = cl + CLW * e;
+        cr[0] = nstored;
+        cr[1] = lkind | 0x100;
+        cr[2] = lclock;
+        cr[3] = llen;
+        cr[5] = found;
+        cr[10] = count;
+        st = ++isec < ncl ? R_SEC : R_NDS;
+      }
+      if (st == R_NDS) active = false; // the DeleteSet: read by the whole wavefront below
+    }
+    if (ps.stamps) t_stp += __builtin_amdgcn_s_memtime() - tq;
+  }
+  const uint64_t tf0 = ps.stamps ? __builtin_amdgcn_s_memtime() : 0;
+  // ---- DeleteSets: the wavefront reads each of its documents' DeleteSet in turn (pw_deleteset,
+  //      the wave planner's parse) in its lanes' ring rows, free by now
+  bool ds_ok = true;
+  {
+    uint64_t dm = __ballot(d < b.n_docs && !bail && st == R_NDS && !(ps.lane_dbg & 2));
+    if (ps.lane_dbg & 2) ds_ok = false;
+    uint32_t *wl = ring_lds + (t & ~63u) * (RING_STRIDE / 4);
+    const uint32_t lane = t & 63;
+    while (dm) {
+      const uint32_t lx = (uint32_t)__builtin_ctzll(dm);
+      dm &= dm - 1;
+      const uint8_t *upx = (const uint8_t *)rdlane64((uint64_t)up, lx);
+      uint32_t *scx = (uint32_t *)rdlane64((uint64_t)scr, lx);
+      uint32_t ndx = 0;
+      const bool okx = pw_deleteset<DIFF>(wl, scx + L.de, upx, rdlane(un, lx), rdlane(pos, lx), lane, cap.E, ndx);
+      if (lane == lx) {
+        ds_ok = okx;
+        nds = ndx;
+      }
+    }
+    __threadfence(); // lane 0's DeleteSet records, read by every lane's plan below
+  }
+  // ---- after the walk (out of the step loop: the calls below do not hold its registers):
+  // hash tables replayed in yrs' insertion order, re-encoded slice sizes, the output plan
+  if (d >= b.n_docs) return;
+  if (!bail && st == R_NDS && ds_ok) {
+    if (ncl && !ct.reserve(ncl, scr + L.ct_tmp)) bail = true;
+    for (uint32_t f = 0; f < nclients && !bail; f++) {
+      if (!ct.reserve(1, scr + L.ct_tmp)) bail = true;
+      else ct.place(ct.keys[f], f);
+    }
+    if (DIFF) {
+      for (uint32_t i = 0; i < nds && !bail; i++) {
+        const uint32_t dc = de[DEW * i];
+        if (!dt.reserve(1, scr + L.dt_tmp)) {
+          bail = true;
+          break;
+        }
+        const int f = dt.find(dc);
+        if (f >= 0) { // replaced in place: the slot now names entry i
+          for (uint32_t s = 0; s < dt.buckets; s++)
+            if (dt.slot[s] == (uint32_t)f + 1) dt.slot[s] = i + 1;
+          dt.keys[i] = dc;
+        } else {
+          dt.place(dc, i);
+        }
+      }
+    }
+    if (!bail) {
+      uint64_t sz = 0;
+      const uint32_t stt = plan_finish<DIFF>(scr, L, cap, ct, nsec, dt, false, 0u, sz);
+      if (stt == PLAN_OVF) {
+        bail = true;
+      } else {
+        if (b.frame && !stt) sz += 2 + varlen(sz); // y-sync message framing
+        ps.big[d] = 0;
+        ps.status[d] = (uint8_t)stt;
+        ps.size[d] = stt ? 0 : sz;
+      }
+    }
+  }
+  if (bail || (st == R_NDS && !ds_ok)) ps.big[d] = PLAN_REDO;
+  if (ps.stamps) {
+    uint64_t *o = ps.stamps + (size_t)d * 16;
+    o[0] = t_ref;
+    o[1] = t_stp;
+    o[2] = __builtin_amdgcn_s_memtime() - tf0;
+    o[3] = n_ref;
+    o[4] = n_stp;
+    o[5] = un;
+    o[7] = 0xD1FF;
+  }
+}
+
 template <bool DIFF>
 __global__ void __launch_bounds__(64) k_plan(DiffBatch b, PlanScratch ps, int pass) {
   ym_set_grammar(b.v1x);
@@ -1274,13 +2492,31 @@ __global__ void __launch_bounds__(64) k_exec_cold(DiffBatch b, PlanScratch ps, c
 
 void launch_plan(bool diff, int pass, const DiffBatch &b, const PlanScratch &ps, hipStream_t s) {
   if (!b.n_docs) return;
-  if (pass == 0) { // common shapes: ring planner; the rest (ps.big = PLAN_REDO) in k_plan pass 0
+  if (pass == 0 && ps.planner == 1) { // common shapes, the ring planner (env YMERGE_PLANNER=ring)
     dim3 gr((b.n_docs + RING_NT - 1) / RING_NT), tr(RING_NT);
     if (diff)
       hipLaunchKernelGGL(k_plan_ring<true>, gr, tr, 0, s, b, ps);
     else
       hipLaunchKernelGGL(k_plan_ring<false>, gr, tr, 0, s, b, ps);
+  } else if (pass == 0 && ps.planner == 2) { // every document on a wavefront (env YMERGE_PLANNER=wave)
+    PlanScratch pw = ps;
+    pw.wave_list = nullptr;
+    dim3 gr((b.n_docs + PW_WPB - 1) / PW_WPB), tr(64 * PW_WPB);
+    if (diff)
+      hipLaunchKernelGGL(k_plan_wave<true>, gr, tr, 0, s, b, pw);
+    else
+      hipLaunchKernelGGL(k_plan_wave<false>, gr, tr, 0, s, b, pw);
+  } else if (pass == 0) { // lane per document; documents of >= PW_MIN bytes on a wavefront each
+    dim3 gr((b.n_docs + RING_NT - 1) / RING_NT), tr(RING_NT), gw(256), tw(64 * PW_WPB);
+    if (diff) {
+      hipLaunchKernelGGL(k_plan_lane<true>, gr, tr, 0, s, b, ps);
+      hipLaunchKernelGGL(k_plan_wave<true>, gw, tw, 0, s, b, ps);
+    } else {
+      hipLaunchKernelGGL(k_plan_lane<false>, gr, tr, 0, s, b, ps);
+      hipLaunchKernelGGL(k_plan_wave<false>, gw, tw, 0, s, b, ps);
+    }
   }
+  // the documents the common-shape planners left (ps.big = PLAN_REDO)
   dim3 g((b.n_docs + 63) / 64), t(64);
   if (diff)
     hipLaunchKernelGGL(k_plan<true>, g, t, 0, s, b, ps, pass);

@@ -159,6 +159,11 @@ struct PlanScratch {
   uint64_t *size;
   uint32_t *n_big;
   uint64_t *stamps = nullptr; // diagnostic (env YMERGE_STAMPS): k_plan_ring phase cycles, 16 per document
+  uint32_t planner = 0;        // pass 0 common-shape planner: 0 k_plan_lane (+ k_plan_wave for long updates),
+                               // 1 k_plan_ring, 2 k_plan_wave for every document (env YMERGE_PLANNER=ring|wave)
+  uint32_t *wave_list = nullptr; // planner 0: documents k_plan_lane leaves to k_plan_wave (n_docs words)
+  uint32_t *wave_n = nullptr;    // ... and their count (zeroed before the launch)
+  uint32_t lane_dbg = 0;         // k_plan_lane diagnostics (env YMERGE_LANE_DBG): 1 no fast step, 2 no wave DeleteSet
 };
 uint64_t plan_small_words();
 void launch_plan(bool diff, int pass, const DiffBatch &b, const PlanScratch &ps, hipStream_t s);

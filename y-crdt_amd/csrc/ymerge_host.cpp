@@ -47,6 +47,15 @@ struct DevBuf {
 };
 
 thread_local uint8_t g_last_error = 0;
+// YMERGE_ERR_DEVICE with the HIP error named on stderr when env YMERGE_VERBOSE is set
+int dev_err(const char *where, hipError_t e = hipSuccess) {
+  static const bool verbose = getenv("YMERGE_VERBOSE") != nullptr;
+  if (verbose) {
+    if (e == hipSuccess) e = hipPeekAtLastError();
+    fprintf(stderr, "ymerge: device error at %s: %s\n", where, hipGetErrorString(e));
+  }
+  return YMERGE_ERR_DEVICE;
+}
 ymerge_batch_result *alloc_result(uint64_t n_docs, uint64_t out_bytes);
 
 } // namespace
@@ -59,6 +68,7 @@ struct ymerge_ctx {
   DevBuf arena, packed, counter, stamps, plan_small, plan_big, rec, ovf, big_scratch, lean_scr, lean_tot, cscr;
   DevBuf gs_list, gs1, gs2; // long single-client documents (ygiant.hip)
   DevBuf lean_ord;          // k_lean dispatch order: 8 counters, then n_docs document indices
+  DevBuf plan_wlist;        // diff / SV: documents k_plan_lane leaves to k_plan_wave
   DevBuf lean_dbg;          // YMERGE_LEAN_DEBUG hand-over reasons (this context's device only)
   uint64_t lean_scr_max = ~0ull; // env YMERGE_LEAN_SCR_MAX: cap on the k_lean BIG-mode scratch (tests)
   // lib0 v2: v1x arena + offsets + per-update status, v2 output arena + sizes + offsets,
@@ -67,6 +77,7 @@ struct ymerge_ctx {
   bool want_stamps = false;
   uint64_t *h_pinned = nullptr;
   hipEvent_t ev[10];
+  hipEvent_t v2ev[4] = {}; // lib0 v2 merge: start, after the v2 -> v1x transcode, after the merge, after the encode
   ymerge_stats stats{};
   uint64_t stamps_docs = 0; // documents covered by `stamps` (last merge batch)
   // tiny-document updates / bytes, blocks (must equal FAST_BCAP, ymerge_fast.hip), DS entries, DS ranges
@@ -76,6 +87,9 @@ struct ymerge_ctx {
   bool pack_stale = false; // pack_off not computed for the last merge (all documents on k_lean)
   uint32_t giant_min = ym::GS_MIN_U; // updates of a document for the grid-wide path (env YMERGE_GIANT_MIN, 0: off)
   int lean_order = -1; // k_lean longest-first dispatch: env YMERGE_LEAN_ORDER 0/1, default for >= 8192 small docs
+  // diff / SV common-shape planner (env YMERGE_PLANNER): 0 "lane" k_plan_lane + k_plan_wave for
+  // long updates, 1 "ring" k_plan_ring (default: fastest measured on C5 so far), 2 "wave"
+  uint32_t planner = 1;
   uint32_t compact_lpw = 16; // k_compact documents per wavefront (env YMERGE_COMPACT_LPW; C2: 16 best)
   // host staging: two pinned buffers (double-buffered H2D / D2H of caller memory)
   uint8_t *stage[2] = {nullptr, nullptr};
@@ -96,6 +110,8 @@ static bool ctx_init(ymerge_ctx *c, int device) {
   if (hipHostMalloc((void **)&c->h_pinned, 1024 * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess) return false;
   for (auto &e : c->ev)
     if (hipEventCreate(&e) != hipSuccess) return false;
+  for (auto &e : c->v2ev)
+    if (hipEventCreate(&e) != hipSuccess) return false;
   // YMERGE_FAST_THREADS: workgroup size of the fast path (256/512/1024); 0 routes every
   // document through the exact engine (used by the parity tests to cover both engines)
   if (const char *v = getenv("YMERGE_FAST_THREADS")) c->fast_threads = atoi(v);
@@ -105,6 +121,8 @@ static bool ctx_init(ymerge_ctx *c, int device) {
   if (const char *v = getenv("YMERGE_COMPACT_LPW")) c->compact_lpw = (uint32_t)atoi(v);
   if (const char *v = getenv("YMERGE_GIANT_MIN")) c->giant_min = (uint32_t)atoi(v);
   if (const char *v = getenv("YMERGE_LEAN_ORDER")) c->lean_order = atoi(v);
+  if (const char *v = getenv("YMERGE_PLANNER"))
+    c->planner = strcmp(v, "lane") == 0 ? 0u : strcmp(v, "wave") == 0 ? 2u : 1u;
   if (const char *v = getenv("YMERGE_LEAN_SCR_MAX")) c->lean_scr_max = strtoull(v, nullptr, 10);
   // the fast kernel's LDS layout must fit one workgroup (160 KB on gfx950)
   int lds_max = 0;
@@ -133,7 +151,7 @@ extern "C" void ymerge_ctx_destroy(ymerge_ctx *c) {
                     &c->sync_end, &c->sync_st, &c->rec, &c->ovf, &c->status, &c->path,
                     &c->out_start, &c->out_len, &c->pack_off, &c->counts, &c->need, &c->scr_off, &c->scratch,
                     &c->sizes, &c->spill_off, &c->scan_tmp, &c->arena, &c->packed, &c->counter, &c->stamps,
-                    &c->plan_small, &c->plan_big, &c->big_scratch, &c->lean_scr, &c->lean_tot, &c->cscr, &c->gs_list, &c->gs1, &c->gs2, &c->lean_ord, &c->lean_dbg, &c->v2x, &c->v2x_sz, &c->v2x_off, &c->v2_ust,
+                    &c->plan_small, &c->plan_big, &c->big_scratch, &c->lean_scr, &c->lean_tot, &c->cscr, &c->gs_list, &c->gs1, &c->gs2, &c->lean_ord, &c->lean_dbg, &c->plan_wlist, &c->v2x, &c->v2x_sz, &c->v2x_off, &c->v2_ust,
                     &c->v2_out, &c->v2_osz, &c->v2_ooff, &c->v2_svoff, &c->v2_svend, &c->v2_pre})
     b->release();
   if (c->h_pinned) hipHostFree(c->h_pinned);
@@ -150,6 +168,8 @@ extern "C" void ymerge_ctx_destroy(ymerge_ctx *c) {
   if (c->s_in) hipStreamDestroy(c->s_in);
   if (c->s_out) hipStreamDestroy(c->s_out);
   for (auto &e : c->ev)
+    if (e) hipEventDestroy(e);
+  for (auto &e : c->v2ev)
     if (e) hipEventDestroy(e);
   if (c->s) hipStreamDestroy(c->s);
   delete c;
@@ -588,11 +608,15 @@ static int plan_exec(ymerge_ctx *c, bool diff, const uint8_t *d_bytes, const uin
   const uint64_t sw = ym::plan_small_words();
   if (!c->status.ensure(nn) || !c->path.ensure(nn) || !c->out_len.ensure(nn * 8) || !c->pack_off.ensure(nn * 8) ||
       !c->need.ensure(nn * 8) || !c->spill_off.ensure(nn * 8) || !c->scan_tmp.ensure(ym::scan_tmp_elems(n) * 8 + 64) ||
-      !c->counter.ensure(64) || !c->plan_small.ensure(nn * sw * 4))
+      !c->counter.ensure(64) || !c->plan_small.ensure(nn * sw * 4) || !c->plan_wlist.ensure(nn * 4))
     return YMERGE_ERR_DEVICE;
   ym::PlanScratch ps{c->plan_small.as<uint32_t>(), sw,       nullptr,
                      c->spill_off.as<uint64_t>(), c->path.as<uint8_t>(), c->status.as<uint8_t>(),
                      c->out_len.as<uint64_t>(),    c->counter.as<uint32_t>()};
+  ps.planner = c->planner;
+  if (const char *v = getenv("YMERGE_LANE_DBG")) ps.lane_dbg = (uint32_t)atoi(v);
+  ps.wave_list = c->plan_wlist.as<uint32_t>();
+  ps.wave_n = c->counter.as<uint32_t>() + 8; // zeroed with the counters below
   if (c->want_stamps) { // diagnostic: k_plan_ring phase cycles
     if (!c->stamps.ensure(nn * 16 * 8)) return YMERGE_ERR_DEVICE;
     hipMemsetAsync(c->stamps.p, 0, nn * 16 * 8, c->s);
@@ -602,10 +626,10 @@ static int plan_exec(ymerge_ctx *c, bool diff, const uint8_t *d_bytes, const uin
   hipMemsetAsync(c->counter.p, 0, 64, c->s);
   hipEventRecord(c->ev[0], c->s);
   ym::launch_plan(diff, 0, b, ps, c->s);
-  if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
+  if (hipGetLastError() != hipSuccess) return dev_err("plan launch");
   hipEventRecord(c->ev[1], c->s);
   hipMemcpyAsync(c->h_pinned + 9, c->counter.p, 4, hipMemcpyDeviceToHost, c->s);
-  if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
+  if (hipError_t e = hipStreamSynchronize(c->s); e != hipSuccess) return dev_err("plan", e);
   const uint32_t n_big = (uint32_t)(c->h_pinned[9] & 0xFFFFFFFFu);
   if (n_big) {
     ym::launch_big_need(d_upd_off, ps.big, n, c->need.as<uint64_t>(), c->s);
@@ -624,7 +648,7 @@ static int plan_exec(ymerge_ctx *c, bool diff, const uint8_t *d_bytes, const uin
   hipEventRecord(c->ev[4], c->s);
   ym::launch_exec(b, ps, c->pack_off.as<uint64_t>(), c->arena.as<uint8_t>(), c->s);
   hipEventRecord(c->ev[3], c->s);
-  if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
+  if (hipError_t e = hipStreamSynchronize(c->s); e != hipSuccess) return dev_err("exec", e);
   if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
   float t01 = 0, t12 = 0, t43 = 0, t03 = 0;
   hipEventElapsedTime(&t01, c->ev[0], c->ev[1]);
@@ -795,15 +819,23 @@ static int merge_v2_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_byt
   if (hipSetDevice(c->device) != hipSuccess) return YMERGE_ERR_DEVICE;
   if (n_docs > 0xFFFFFFFFull) return YMERGE_ERR_OTHER;
   uint64_t xbytes = 0;
+  hipEventRecord(c->v2ev[0], c->s);
   int st = v2_transcode(c, d_bytes, d_upd_off, n_updates, &xbytes);
   if (st) return st;
+  hipEventRecord(c->v2ev[1], c->s);
   st = merge_device(c, c->v2x.as<uint8_t>(), xbytes, c->v2x_off.as<uint64_t>(), n_updates, d_doc_upd, n_docs, res);
   if (st) return st;
+  hipEventRecord(c->v2ev[2], c->s);
   ym::launch_v2_doc_status(d_doc_upd, c->v2_ust.as<uint8_t>(), (uint32_t)n_docs, res->d_status,
                            (uint64_t *)res->d_out_len, c->s);
   st = v2_encode(c, res, (uint32_t)n_docs, 0);
+  hipEventRecord(c->v2ev[3], c->s);
+  hipEventSynchronize(c->v2ev[3]);
   c->stats.bytes_in = n_bytes;
   c->stats.bytes_out = res->out_bytes;
+  hipEventElapsedTime(&c->stats.ms_v2_decode, c->v2ev[0], c->v2ev[1]);
+  hipEventElapsedTime(&c->stats.ms_v2_merge, c->v2ev[1], c->v2ev[2]);
+  hipEventElapsedTime(&c->stats.ms_v2_encode, c->v2ev[2], c->v2ev[3]);
   return st;
 }
 // diff_updates_v2 (diff = true) / encode_state_vector_from_update_v2: one update per document
@@ -933,8 +965,8 @@ extern "C" int ymerge_updates_v2_batch(ymerge_ctx *c, const uint8_t *bytes, cons
 // producer thread stages group g + 1 into HBM (stream s_in) while this thread merges group g
 // on the engine stream and the DMA engine returns group g - 1's packed output (stream
 // s_out) straight into the pinned result arena.  H2D, compute and D2H overlap; each
-// group is an ordinary merge_device call over its documents (absolute byte offsets, so the
-// input arena and the per-document slots are shared).
+// group is an ordinary merge_device call over its documents and its slice of the input
+// arena (offsets rebased to the slice), so device memory scales with the group.
 constexpr uint64_t GROUP_BYTES = 48ull << 20;
 static int host_merge_pipelined(ymerge_ctx *c, const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_updates,
                                 const uint64_t *doc_upd, uint64_t n_docs, ymerge_batch_result **out) {
@@ -954,17 +986,23 @@ static int host_merge_pipelined(ymerge_ctx *c, const uint8_t *bytes, const uint6
     if ((!c->ev_out[k] && hipEventCreateWithFlags(&c->ev_out[k], hipEventDisableTiming) != hipSuccess) ||
         (!c->ev_packed[k] && hipEventCreateWithFlags(&c->ev_packed[k], hipEventDisableTiming) != hipSuccess))
       return YMERGE_ERR_DEVICE;
-  if (!stage_init(c) || !c->in_bytes.ensure(nbytes + 16) || !c->in_upd_off.ensure((n_updates + 1) * 8) ||
+  if (!stage_init(c) || !c->in_bytes.ensure(nbytes + 16) || !c->in_upd_off.ensure((n_updates + G + 1) * 8) ||
       !c->grp_doc_upd.ensure((n_docs + G + 1) * 8))
     return YMERGE_ERR_DEVICE;
-  // rebased document tables of every group (group k's documents index its slice of upd_off)
-  std::vector<uint64_t> gdu(n_docs + G + 1);
-  std::vector<uint64_t> gdu_off(G + 1, 0);
+  // rebased tables of every group: its documents index its slice of the update offsets, and
+  // those count from the group's first byte rounded down to 16 (the kernels' aligned loads), so
+  // each merge_device call sizes its slots and scratch by the group, not the whole batch
+  std::vector<uint64_t> gdu(n_docs + G + 1), guo(n_updates + G + 1);
+  std::vector<uint64_t> gdu_off(G + 1, 0), guo_off(G + 1, 0), gbase(G);
   for (size_t k = 0; k < G; k++) {
     gdu_off[k + 1] = gdu_off[k] + (gd[k + 1] - gd[k]) + 1;
     for (uint64_t d = gd[k]; d <= gd[k + 1]; d++) gdu[gdu_off[k] + d - gd[k]] = doc_upd[d] - doc_upd[gd[k]];
+    const uint64_t u0 = doc_upd[gd[k]], u1 = doc_upd[gd[k + 1]];
+    gbase[k] = upd_off[u0] & ~15ull;
+    guo_off[k + 1] = guo_off[k] + (u1 - u0) + 1;
+    for (uint64_t u = u0; u <= u1; u++) guo[guo_off[k] + u - u0] = upd_off[u] - gbase[k];
   }
-  if (hipMemcpyAsync(c->in_upd_off.p, upd_off, (n_updates + 1) * 8, hipMemcpyHostToDevice, c->s_in) != hipSuccess ||
+  if (hipMemcpyAsync(c->in_upd_off.p, guo.data(), guo_off[G] * 8, hipMemcpyHostToDevice, c->s_in) != hipSuccess ||
       hipMemcpyAsync(c->grp_doc_upd.p, gdu.data(), gdu_off[G] * 8, hipMemcpyHostToDevice, c->s_in) != hipSuccess ||
       hipStreamSynchronize(c->s_in) != hipSuccess)
     return YMERGE_ERR_DEVICE;
@@ -1016,8 +1054,10 @@ static int host_merge_pipelined(ymerge_ctx *c, const uint8_t *bytes, const uint6
       break;
     }
     ymerge_device_result dr{};
-    rc = merge_device(c, c->in_bytes.as<uint8_t>(), nbytes, c->in_upd_off.as<uint64_t>() + doc_upd[gd[k]],
-                      doc_upd[gd[k + 1]] - doc_upd[gd[k]], c->grp_doc_upd.as<uint64_t>() + gdu_off[k], nd, &dr);
+    const uint64_t u0 = doc_upd[gd[k]], u1 = doc_upd[gd[k + 1]];
+    rc = merge_device(c, c->in_bytes.as<uint8_t>() + gbase[k], upd_off[u1] - gbase[k],
+                      c->in_upd_off.as<uint64_t>() + guo_off[k], u1 - u0, c->grp_doc_upd.as<uint64_t>() + gdu_off[k], nd,
+                      &dr);
     if (rc) break;
     // pack group k into packed2[k & 1] once group k - 2's D2H from it has drained
     const int pb = (int)(k & 1);

@@ -4,6 +4,9 @@ C1  automerge-paper trace replay, one doc (tests/golden/automerge-paper.json.gz)
 C2  n docs x k ops, 1-4 clients, 80/20 insert/delete, synced replicas (seed 0xC0FFEE)
 C3  Zipf(1.5) op counts on [1, 1e4] (seed 0x5EED)
 C4  delete-heavy docs: GC'd snapshot + per-op log, 10% withheld, 5% duplicated (seed 0xDE1E7E)
+corpus  the reference's own inputs: assets/bench-input/small-test-dataset.bin (5,320 real Yjs
+        documents, compatibility_tests.rs:437-476) tiled to a batch size, and the five
+        assets/editing-traces sequential traces, one document each
 """
 import ctypes
 import functools
@@ -193,6 +196,92 @@ def trace_updates(path=None, client=1):
     _L().yw_free(b)
     _L().yw_free(uo)
     return Batch(data, upd_off, np.array([0, len(pos)], np.uint64), name="C1"), d["endContent"]
+
+
+def _golden(name):
+    return os.path.join(os.path.dirname(_HERE), "tests", "golden", name)
+
+
+@functools.lru_cache(maxsize=2)
+def dataset_docs():
+    """small-test-dataset.bin as a Batch of its 5,320 documents (each test's update list;
+    the format test_data_set reads, yrs/src/tests/compatibility_tests.rs:437-476: var_u32
+    count, per test var_u32 n + n read_buf updates, then the expected text / map / array,
+    skipped here)."""
+    data = open(_golden("small-test-dataset.bin"), "rb").read()
+    n, i = _rv(data, 0)
+    parts, offs, dus, tot = [], [0], [0], 0
+    for _ in range(n):
+        k, i = _rv(data, i)
+        for _ in range(k):
+            ln, i = _rv(data, i)
+            parts.append(data[i:i + ln])
+            tot += ln
+            offs.append(tot)
+            i += ln
+        dus.append(len(offs) - 1)
+        ln, i = _rv(data, i)  # expected text
+        i += ln
+        i = _skip_any(data, i)  # expected map
+        i = _skip_any(data, i)  # expected array
+    return Batch(np.frombuffer(b"".join(parts), np.uint8).copy(), np.array(offs, np.uint64),
+                 np.array(dus, np.uint64), name="small-test-dataset")
+
+
+def _skip_any(b, i):
+    """Past one lib0 Any (yrs/src/any.rs:37-83)."""
+    t = b[i]
+    i += 1
+    if t in (127, 126, 121, 120):
+        return i
+    if t == 125:  # signed varint
+        while b[i] & 0x80:
+            i += 1
+        return i + 1
+    if t in (124, 123, 122):
+        return i + {124: 4, 123: 8, 122: 8}[t]
+    if t in (119, 116):
+        n, i = _rv(b, i)
+        return i + n
+    if t == 118:
+        n, i = _rv(b, i)
+        for _ in range(n):
+            k, i = _rv(b, i)
+            i = _skip_any(b, i + k)
+        return i
+    if t == 117:
+        n, i = _rv(b, i)
+        for _ in range(n):
+            i = _skip_any(b, i)
+        return i
+    raise ValueError(f"bad Any tag {t}")
+
+
+def tile(batch, n_docs):
+    """The batch's documents repeated in order up to n_docs documents (one arena)."""
+    reps = -(-n_docs // batch.n_docs)
+    nb, nu = batch.n_bytes, batch.n_updates
+    data = np.tile(batch.data[:nb], reps)
+    uo = np.concatenate([batch.upd_off[:-1].astype(np.uint64) + np.uint64(r * nb) for r in range(reps)] +
+                        [np.array([reps * nb], np.uint64)])
+    du = np.concatenate([batch.doc_upd[:-1].astype(np.uint64) + np.uint64(r * nu) for r in range(reps)] +
+                        [np.array([reps * nu], np.uint64)])
+    full = Batch(data, uo, du, name=f"{batch.name}x{reps}")
+    return full.prefix(n_docs) if n_docs < full.n_docs else full
+
+
+def traces_batch():
+    """The five sequential editing traces, one document each (per-op updates, client 1)."""
+    bs = [trace_updates(t)[0] for t in TRACES]
+    parts, uos, dus, tb, tu = [], [], [0], 0, 0
+    for b in bs:
+        parts.append(b.data[:b.n_bytes])
+        uos.append(b.upd_off[:-1].astype(np.uint64) + np.uint64(tb))
+        tb += b.n_bytes
+        tu += b.n_updates
+        dus.append(tu)
+    return Batch(np.concatenate(parts), np.concatenate(uos + [np.array([tb], np.uint64)]),
+                 np.array(dus, np.uint64), name="traces")
 
 
 def _var(x):

@@ -40,7 +40,8 @@ class _Stats(ctypes.Structure):
                 ("ms_tail", ctypes.c_float), ("ms_decode", ctypes.c_float), ("ms_big", ctypes.c_float),
                 ("docs_overlap", ctypes.c_uint32), ("docs_big", ctypes.c_uint64), ("docs_tiny", ctypes.c_uint64),
                 ("ms_tiny", ctypes.c_float), ("docs_lean", ctypes.c_uint64), ("ms_lean", ctypes.c_float),
-                ("docs_giant", ctypes.c_uint64)]
+                ("docs_giant", ctypes.c_uint64), ("ms_v2_decode", ctypes.c_float), ("ms_v2_merge", ctypes.c_float),
+                ("ms_v2_encode", ctypes.c_float)]
 
 
 class _DevRes(ctypes.Structure):
