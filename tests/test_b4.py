@@ -65,13 +65,17 @@ def test_b4_merge_gpu(oracle):
 
 
 @pytest.mark.gpu
-def test_b4_sv_and_diff_gpu(oracle):
-    import ymerge
+@pytest.mark.parametrize("planner", ["ring", "lane", "wave"])
+def test_b4_sv_and_diff_gpu(oracle, planner):
+    """b4 and its merge through each planner (the merged form is canonical, 375 KB: under
+    "lane" it is a k_plan_wave document; b4 itself has 7-byte client varints, which the
+    common-shape planners hand to k_plan)."""
     from test_gpu_diff import check_diff, check_sv
+    from test_gpu_parity import engine_with
     u = corpus.b4_update()
     m = oracle.merge_updates_v1([u])
     (client, clock), = oracle.parse_sv(oracle.encode_state_vector_from_update_v1(u))
-    eng = ymerge.Engine(0)
+    eng = engine_with(YMERGE_PLANNER=planner)
     try:
         check_sv(eng, oracle, [u, m])
         svs = _remote_svs(client, clock)

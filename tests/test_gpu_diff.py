@@ -17,10 +17,21 @@ from test_oracle_kats import ALT_DIFF, ALT_MERGE_1, ALT_MERGE_2, ALT_SV, COMPAT
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def engine():
+@pytest.fixture(scope="module", params=["ring", "lane", "wave"])
+def engine(request):
+    """Every test runs under each common-shape planner (env YMERGE_PLANNER, read at engine
+    creation): k_plan_ring, k_plan_lane (+ k_plan_wave for long updates), k_plan_wave for every
+    document; the shapes each one hands over go to the general k_plan either way."""
     import ymerge
-    e = ymerge.Engine(0)
+    old = os.environ.get("YMERGE_PLANNER")
+    os.environ["YMERGE_PLANNER"] = request.param
+    try:
+        e = ymerge.Engine(0)
+    finally:
+        if old is None:
+            del os.environ["YMERGE_PLANNER"]
+        else:
+            os.environ["YMERGE_PLANNER"] = old
     yield e
     e.close()
 

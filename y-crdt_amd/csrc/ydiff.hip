@@ -505,7 +505,9 @@ constexpr uint32_t RING_STRIDE = RING + 16; // LDS bytes per lane (16-byte align
 constexpr uint32_t RING_G = RING % 128 == 0 ? 8 : 4; // 16-byte loads per refill group
 constexpr uint32_t RING_NT = 256;       // lanes (documents) per workgroup
 constexpr uint32_t RING_STEPS = 10;     // item steps between refill points
-constexpr uint32_t LP_SLOW = 16;        // k_plan_lane: lanes that wait for a full step before the wave runs it
+constexpr uint32_t LP_SLOW = 6;         // k_plan_lane: lanes that wait for a full step before the wave runs it
+constexpr uint32_t LP_STEPS = 8;        // k_plan_lane: item steps between refill points (C5 sweep: 8 steps with
+                                        // LP_SLOW 6 best, profiles/r04/r04n_lane_sweep.txt)
 constexpr uint8_t PLAN_REDO = 3;
 constexpr uint8_t PLAN_WAVE = 4;         // planned by k_plan_wave (k_plan_lane's long documents)
 constexpr uint64_t PW_MIN = 64 * 1024;   // update bytes from which a document gets a wavefront
@@ -1708,9 +1710,11 @@ __global__ void __launch_bounds__(64 * PW_WPB) k_plan_wave(DiffBatch b, PlanScra
 //     the content length's end as the n-th terminator, the canonical-varint checks as mask
 //     algebra, the ASCII check as one mask test.  Everything else -- section headers,
 //     parent-form or re-encoded blocks, blocks longer than the window, a section's last block,
-//     the client's first diff block -- takes the full step (one field-program loop).
-//   * A lane stops at its DeleteSet; the wavefront then reads its documents' DeleteSets in
-//     turn, all 64 lanes on one (pw_deleteset).
+//     the client's first diff block, an entry's last range -- takes the full step (one
+//     field-program loop).
+//   * A DeleteSet range (two varints) likewise, from a 16-byte window.
+//   * The full step is batched: a lane that needs it waits until LP_SLOW lanes of its wave do
+//     (or none can take a fast step), so the wave runs it once for many lanes.
 // Same shapes, records and plans as the ring planner.
 template <bool DIFF>
 __global__ void __launch_bounds__(RING_NT) k_plan_lane(DiffBatch b, PlanScratch ps) {
@@ -1782,9 +1786,13 @@ __global__ void __launch_bounds__(RING_NT) k_plan_lane(DiffBatch b, PlanScratch 
   // current section (plan_doc's per-client record, kept in registers while the section runs)
   uint32_t e = 0, nstored = 0, lkind = 0, lclock = 0, llen = 0, remote = 0, found = 0, count = 0, kb = 0, pure = 1,
            ssize = 0, nsec = 0;
-  uint32_t nds = 0;
+  // DeleteSet
+  uint32_t nds = 0, ids = 0, dclient = 0, cpos = 0, nr = 0, kr = 0, prev_e = 0, dsz = 0;
+  bool dcanon = true, dsq = true;
   RingRd R{row, (uint64_t)up, 0, 0, (uint64_t)up + un, un, F_OK, 0, 0};
   bool have = false, wait = false, need_slow = false;
+  const uint32_t lp_slow = (ps.lane_dbg >> 8) & 0xFF ? (ps.lane_dbg >> 8) & 0xFF : LP_SLOW; // (diagnostic overrides)
+  const uint32_t ring_steps = (ps.lane_dbg >> 16) & 0xFF ? (ps.lane_dbg >> 16) & 0xFF : LP_STEPS;
 
   // diagnostic stamps (wave time): refill, steps, finish; refill rounds, step iterations
   uint64_t t_ref = 0, t_stp = 0, n_ref = 0, n_stp = 0, tq = ps.stamps ? __builtin_amdgcn_s_memtime() : 0;
@@ -1822,7 +1830,7 @@ __global__ void __launch_bounds__(RING_NT) k_plan_lane(DiffBatch b, PlanScratch 
       tq = now;
       n_ref++;
     }
-    for (uint32_t step = 0; step < RING_STEPS; step++) {
+    for (uint32_t step = 0; step < ring_steps; step++) {
       const bool can = active && !wait;
       if (!__any(can)) break;
       if (ps.stamps) n_stp++;
@@ -1906,7 +1914,48 @@ __global__ void __launch_bounds__(RING_NT) k_plan_lane(DiffBatch b, PlanScratch 
             need_slow = true;
           }
         }
-      } else if (can && st != R_BLOCK) {
+      } else if (can && !need_slow && st == R_DRANGE && kr + 1 < nr && !(ps.lane_dbg & 1)) {
+        // ---- fast step: one DeleteSet range (start, length), two varints of a 16-byte window
+        const int32_t o = (int32_t)pos - R.rbq;
+        if (!(o >= 0 && o + 20 <= (int32_t)RING_STRIDE && ((int32_t)pos + 16 <= R.rendq || R.rendq == (int32_t)un))) {
+          wait = true;
+        } else {
+          const uint32_t *wr = row + (o >> 2);
+          const uint32_t sh = (uint32_t)o & 3;
+          const uint32_t a0 = wr[0], a1 = wr[1], a2 = wr[2], a3 = wr[3], a4 = wr[4];
+          const uint32_t x0 = __builtin_amdgcn_alignbyte(a1, a0, sh), x1 = __builtin_amdgcn_alignbyte(a2, a1, sh);
+          const uint32_t x2 = __builtin_amdgcn_alignbyte(a3, a2, sh), x3 = __builtin_amdgcn_alignbyte(a4, a3, sh);
+          const uint64_t lo = (uint64_t)x0 | ((uint64_t)x1 << 32), hi = (uint64_t)x2 | ((uint64_t)x3 << 32);
+          const uint64_t tl = ~lo & 0x8080808080808080ull, th = ~hi & 0x8080808080808080ull;
+          const uint32_t e1 = (uint32_t)__builtin_ctzll(tl | (1ull << 63)) >> 3; // 7: none in the low 8 bytes
+          const uint32_t s2 = e1 + 1;                                             // second varint's start (<= 8)
+          const uint64_t y = s2 >= 8 ? hi : (lo >> (8 * s2)) | (s2 ? hi << (64 - 8 * s2) : 0ull);
+          const uint64_t ty = ~y & 0x8080808080808080ull;
+          const uint32_t n2 = ((uint32_t)__builtin_ctzll(ty | (1ull << 63)) >> 3) + 1;
+          const uint32_t n1 = e1 + 1;
+          auto dec = [](uint64_t x, uint32_t n) -> uint32_t {
+            const uint64_t xm = x & (n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1));
+            return (uint32_t)((xm & 0x7F) | ((xm >> 1) & 0x3F80) | ((xm >> 2) & 0x1FC000) | ((xm >> 3) & 0xFE00000) |
+                              ((xm >> 4) & 0x7F0000000ull));
+          };
+          const uint32_t rs = dec(lo, n1), rl = dec(y, n2);
+          const uint32_t l1 = (uint32_t)(lo >> (8 * (n1 - 1))) & 0xFF, l2 = (uint32_t)(y >> (8 * (n2 - 1))) & 0xFF;
+          const bool c1 = n1 == 1 || (l1 != 0 && (n1 < 5 || l1 < 16)), c2 = n2 == 1 || (l2 != 0 && (n2 < 5 || l2 < 16));
+          const bool fine = n1 <= 5 && n2 <= 5 && n1 + n2 <= un - pos;
+          const bool fast = fine && (uint64_t)rs + rl <= 0xFFFFFFFFull && (kr == 0 || rs >= prev_e || !DIFF);
+          if (fast) {
+            pos += n1 + n2;
+            dcanon &= c1 && c2;
+            if (kr > 0 && rs < prev_e) dsq = false;
+            prev_e = rs + rl;
+            dsz += varlen(rs) + varlen(rl);
+            kr++;
+            fast_done = true;
+          } else {
+            need_slow = true;
+          }
+        }
+      } else if (can && st != R_BLOCK && !need_slow) {
         need_slow = true;
       } else if (can && (ps.lane_dbg & 1)) {
         need_slow = true;
@@ -1916,11 +1965,11 @@ __global__ void __launch_bounds__(RING_NT) k_plan_lane(DiffBatch b, PlanScratch 
       //      lane made progress, so a wave pays for it once per LP_SLOW lanes, not once per step
       const uint64_t slow_m = __ballot(can && need_slow);
       if (!slow_m) continue;
-      if ((uint32_t)__builtin_popcountll(slow_m) < LP_SLOW && __ballot(fast_done)) continue;
+      if ((uint32_t)__builtin_popcountll(slow_m) < lp_slow && __ballot(fast_done)) continue;
       if (!(can && need_slow)) continue;
       need_slow = false;
       R.fail = F_OK;
-      bool cn, sec_end = false;
+      bool cn, sec_end = false, entry_end = false;
       // ---- the item's field program: one loop reads the varints of every item kind (lanes of
       //      a wave sit on different kinds -- string blocks, DeleteSet ranges, headers -- and run
       //      the same instructions); 2 bits per field, low end first: 0 varint, 1 varint + that
@@ -2102,12 +2151,47 @@ __global__ void __launch_bounds__(RING_NT) k_plan_lane(DiffBatch b, PlanScratch 
           if (nb) st = R_BLOCK;
           else sec_end = true;
         }
+      } else if (st == R_DRANGE) {
+        // ---- one DeleteSet range (start, len)
+        const uint32_t rs = f0, rl = f1;
+        if (!R.fail && (uint64_t)rs + rl > 0xFFFFFFFFull) R.fail = F_BAIL;
+        if (!R.fail) {
+          pos = q;
+          dcanon &= (ncan & 3) == 0;
+          if (kr > 0 && rs < prev_e) dsq = false;
+          prev_e = rs + rl;
+          dsz += varlen(rs) + varlen(rl);
+          if (++kr == nr) entry_end = true;
+        }
+      } else if (st == R_DENT) {
+        // ---- DeleteSet entry header: client, range count
+        dclient = f0;
+        nr = f1;
+        if (!R.fail) {
+          pos = q;
+          cpos = p1;
+          dcanon = (ncan & 2) == 0;
+          dsq = true;
+          prev_e = 0;
+          dsz = varlen(nr);
+          kr = 0;
+          if (nr) st = R_DRANGE;
+          else entry_end = true;
+        }
       } else if (st == R_NCL) {
         ncl = f0;
         if (!R.fail && ncl > cap.C) R.fail = F_BAIL;
         if (!R.fail) {
           pos = q;
           st = ncl ? R_SEC : R_NDS;
+        }
+      } else { // R_NDS
+        nds = f0;
+        if (!R.fail && DIFF && nds > cap.E) R.fail = F_BAIL;
+        if (!R.fail) {
+          pos = q;
+          ids = 0;
+          st = nds ? R_DENT : R_DONE;
         }
       }
       if (R.fail == F_SHORT) { // nothing consumed: the item is read again after the refill
@@ -2136,37 +2220,30 @@ __global__ void __launch_bounds__(RING_NT) k_plan_lane(DiffBatch b, PlanScratch 
         cr[10] = count;
         st = ++isec < ncl ? R_SEC : R_NDS;
       }
-      if (st == R_NDS) active = false; // the DeleteSet: read by the whole wavefront below
+      if (entry_end) {
+        if (DIFF) {
+          if (!dsq) { // squash of a clone: general planner
+            bail = true;
+            active = false;
+            continue;
+          }
+          uint32_t *r = de + DEW * ids;
+          r[0] = dclient;
+          r[1] = cpos;
+          r[2] = pos;
+          r[3] = nr;
+          r[4] = 1u | (dcanon ? 2u : 0u);
+          r[7] = varlen(dclient) + dsz;
+        }
+        st = ++ids < nds ? R_DENT : R_DONE;
+      }
+      if (st == R_DONE) active = false;
     }
     if (ps.stamps) t_stp += __builtin_amdgcn_s_memtime() - tq;
   }
   const uint64_t tf0 = ps.stamps ? __builtin_amdgcn_s_memtime() : 0;
-  // ---- DeleteSets: the wavefront reads each of its documents' DeleteSet in turn (pw_deleteset,
-  //      the wave planner's parse) in its lanes' ring rows, free by now
-  bool ds_ok = true;
-  {
-    uint64_t dm = __ballot(d < b.n_docs && !bail && st == R_NDS && !(ps.lane_dbg & 2));
-    if (ps.lane_dbg & 2) ds_ok = false;
-    uint32_t *wl = ring_lds + (t & ~63u) * (RING_STRIDE / 4);
-    const uint32_t lane = t & 63;
-    while (dm) {
-      const uint32_t lx = (uint32_t)__builtin_ctzll(dm);
-      dm &= dm - 1;
-      const uint8_t *upx = (const uint8_t *)rdlane64((uint64_t)up, lx);
-      uint32_t *scx = (uint32_t *)rdlane64((uint64_t)scr, lx);
-      uint32_t ndx = 0;
-      const bool okx = pw_deleteset<DIFF>(wl, scx + L.de, upx, rdlane(un, lx), rdlane(pos, lx), lane, cap.E, ndx);
-      if (lane == lx) {
-        ds_ok = okx;
-        nds = ndx;
-      }
-    }
-    __threadfence(); // lane 0's DeleteSet records, read by every lane's plan below
-  }
-  // ---- after the walk (out of the step loop: the calls below do not hold its registers):
-  // hash tables replayed in yrs' insertion order, re-encoded slice sizes, the output plan
   if (d >= b.n_docs) return;
-  if (!bail && st == R_NDS && ds_ok) {
+  if (!bail && st == R_DONE) {
     if (ncl && !ct.reserve(ncl, scr + L.ct_tmp)) bail = true;
     for (uint32_t f = 0; f < nclients && !bail; f++) {
       if (!ct.reserve(1, scr + L.ct_tmp)) bail = true;
@@ -2202,7 +2279,7 @@ __global__ void __launch_bounds__(RING_NT) k_plan_lane(DiffBatch b, PlanScratch 
       }
     }
   }
-  if (bail || (st == R_NDS && !ds_ok)) ps.big[d] = PLAN_REDO;
+  if (bail) ps.big[d] = PLAN_REDO;
   if (ps.stamps) {
     uint64_t *o = ps.stamps + (size_t)d * 16;
     o[0] = t_ref;

@@ -88,8 +88,9 @@ struct ymerge_ctx {
   uint32_t giant_min = ym::GS_MIN_U; // updates of a document for the grid-wide path (env YMERGE_GIANT_MIN, 0: off)
   int lean_order = -1; // k_lean longest-first dispatch: env YMERGE_LEAN_ORDER 0/1, default for >= 8192 small docs
   // diff / SV common-shape planner (env YMERGE_PLANNER): 0 "lane" k_plan_lane + k_plan_wave for
-  // long updates, 1 "ring" k_plan_ring (default: fastest measured on C5 so far), 2 "wave"
-  uint32_t planner = 1;
+  // long updates (default: C5 k_plan 4.24 -> 3.3 ms against the ring planner), 1 "ring"
+  // k_plan_ring, 2 "wave" k_plan_wave for every document
+  uint32_t planner = 0;
   uint32_t compact_lpw = 16; // k_compact documents per wavefront (env YMERGE_COMPACT_LPW; C2: 16 best)
   // host staging: two pinned buffers (double-buffered H2D / D2H of caller memory)
   uint8_t *stage[2] = {nullptr, nullptr};
@@ -122,7 +123,7 @@ static bool ctx_init(ymerge_ctx *c, int device) {
   if (const char *v = getenv("YMERGE_GIANT_MIN")) c->giant_min = (uint32_t)atoi(v);
   if (const char *v = getenv("YMERGE_LEAN_ORDER")) c->lean_order = atoi(v);
   if (const char *v = getenv("YMERGE_PLANNER"))
-    c->planner = strcmp(v, "lane") == 0 ? 0u : strcmp(v, "wave") == 0 ? 2u : 1u;
+    c->planner = strcmp(v, "ring") == 0 ? 1u : strcmp(v, "wave") == 0 ? 2u : 0u;
   if (const char *v = getenv("YMERGE_LEAN_SCR_MAX")) c->lean_scr_max = strtoull(v, nullptr, 10);
   // the fast kernel's LDS layout must fit one workgroup (160 KB on gfx950)
   int lds_max = 0;
