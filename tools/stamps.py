@@ -33,6 +33,9 @@ def main_big(n, kind="c3"):
     tot = d.sum(axis=1)
     print(f"tiled docs: {ok.sum()}, updates/doc mean {U.mean():.0f}, cycles/doc mean {tot.mean():.0f}, "
           f"cycles/update {(tot / U).mean():.0f}")
+    g = st[ok][:, 8:12].astype(np.float64)
+    print(f"  gather sub-phases (thread 0): records+walks {g[:, 0].mean():.0f}, scans {g[:, 1].mean():.0f}, "
+          f"writes {g[:, 2].mean():.0f}; rounds with a REC_SLOW update {g[:, 3].mean():.1f}")
     for i, nm in enumerate(BIG_NAMES):
         print(f"  {nm:10s} {d[:, i].mean():10.0f} cycles  {100 * d[:, i].mean() / tot.mean():5.1f}%")
     for lo, hi in ((0, 2000), (2000, 4000), (4000, 10001)):

@@ -540,7 +540,9 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
   //      or a walk of the update for the shapes k_decode left to a later pass)
   {
     uint32_t NBr = 0, NEr = 0, NRr = 0;
+    uint64_t g_rec = 0, g_scan = 0, g_write = 0, g_slow = 0; // diagnostic sub-phase sums (thread 0, stamps only)
     for (uint32_t r0 = 0; r0 < U; r0 += NT) {
+      const uint64_t tg0 = o.stamps ? __builtin_amdgcn_s_memtime() : 0;
       const uint32_t i = r0 + t;
       uint32_t ubase = 0, ulen = 0, shape = 0, w0 = 0, w1 = 0, w2 = 0, w3 = 0, w4 = 0, w5 = 0;
       uint32_t snb = 0, sne = 0, snr = 0;
@@ -579,6 +581,11 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
           walk = !(w0 & REC_OVF);
         }
       }
+      if (o.stamps) {
+        g_slow += __ballot(i < U && (w0 & REC_SLOW)) ? 1 : 0;
+        __syncthreads();
+      }
+      const uint64_t tg1 = o.stamps ? __builtin_amdgcn_s_memtime() : 0;
       uint64_t T0, T1;
       const uint64_t p0 = bscan_sum64<NT>((uint64_t)snb | ((uint64_t)sne << 32), S.ws64, T0);
       const uint64_t p1 = bscan_sum64<NT>((uint64_t)snr, S.ws64, T1);
@@ -586,7 +593,12 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
       NBr += (uint32_t)T0;
       NEr += (uint32_t)(T0 >> 32);
       NRr += (uint32_t)T1;
-      if (i >= U) continue;
+      const uint64_t tg2 = o.stamps ? __builtin_amdgcn_s_memtime() : 0;
+      if (o.stamps) {
+        g_rec += tg1 - tg0;
+        g_scan += tg2 - tg1;
+      }
+      if (i < U) {
       if (shape == REC_BLOCK) {
         m.bc[pb] = w1;
         m.bk[pb] = w2;
@@ -630,6 +642,17 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
         FastFill f{m.bc, m.bk, m.bl, m.bp, m.bm, m.ec, m.et, m.rs, m.re, m.ri, i, ubase, pb, pe, pr, 0};
         fill_hbm(in + ubase, ulen, &f);
       }
+      }
+      if (o.stamps) {
+        __syncthreads();
+        g_write += __builtin_amdgcn_s_memtime() - tg2;
+      }
+    }
+    if (o.stamps && t == 0) {
+      o.stamps[(size_t)d * 16 + 8] = g_rec;
+      o.stamps[(size_t)d * 16 + 9] = g_scan;
+      o.stamps[(size_t)d * 16 + 10] = g_write;
+      o.stamps[(size_t)d * 16 + 11] = g_slow;
     }
   }
   __syncthreads();
