@@ -35,7 +35,10 @@ def main_big(n, kind="c3"):
           f"cycles/update {(tot / U).mean():.0f}")
     g = st[ok][:, 8:12].astype(np.float64)
     print(f"  gather sub-phases (thread 0): records+walks {g[:, 0].mean():.0f}, scans {g[:, 1].mean():.0f}, "
-          f"writes {g[:, 2].mean():.0f}; rounds with a REC_SLOW update {g[:, 3].mean():.1f}")
+          f"writes {g[:, 2].mean():.0f}; REC_SLOW updates walked {g[:, 3].mean():.1f}")
+    r = st[ok][:, 12:16].astype(np.float64)
+    print(f"  per round: records round0 {r[:, 0].mean():.0f} / slowest later {r[:, 1].mean():.0f}; "
+          f"writes round0 {r[:, 2].mean():.0f} / slowest later {r[:, 3].mean():.0f}")
     for i, nm in enumerate(BIG_NAMES):
         print(f"  {nm:10s} {d[:, i].mean():10.0f} cycles  {100 * d[:, i].mean() / tot.mean():5.1f}%")
     for lo, hi in ((0, 2000), (2000, 4000), (4000, 10001)):

@@ -5,10 +5,11 @@
 // decodes its own update from LDS.  Varints are read branch-free: two dword reads
 // (ds_read2_b32) cover the <= 5 bytes of a u32 LEB128, the terminator is found with
 // a ctz over the continuation bits, so lanes stay converged whatever the varint
-// lengths.  The shapes handled are the ones a text editor emits (one client section
-// with one GC / Skip / Deleted / String block, any DeleteSet); anything else, and any
-// malformed input, bails out (-1) and the caller runs the exact walk (ysm.h), which
-// also owns the error codes.  Semantics follow Update::decode_v1
+// lengths.  The shapes handled are the ones a text editor emits: client sections of
+// GC / Skip / Deleted / ASCII String blocks (one block per update for an editor's
+// transactions, many for a snapshot), any DeleteSet; anything else, and any malformed
+// input, bails out (-1) and the caller runs the exact walk (ysm.h), which also owns the
+// error codes.  Semantics follow Update::decode_v1
 // (yrs/src/update.rs:714-749, 433-488), ItemContent::decode (yrs/src/block.rs:1786-1835)
 // and IdSet::decode (yrs/src/id_set.rs:412-426), exactly as ysm.h restates them.
 #pragma once
@@ -54,13 +55,15 @@ template <class S> YM_INLINE int fast_walk(const uint32_t *w, uint32_t start, ui
   bool cn;
   uint32_t ncl, nds;
   if (!lvar(c, ncl, cn)) return -1;
-  if (ncl > 1) return -1;
-  if (ncl == 1) {
+  // every section and block takes >= 1 byte: larger counts cannot decode (the exact walk
+  // reports them, including yrs' try_reserve errors for absurd counts)
+  if (ncl > n) return -1;
+  for (uint32_t sec = 0; sec < ncl; sec++) {
     uint32_t nb, client, clock;
     if (!lvar(c, nb, cn) || !lvar(c, client, cn) || !lvar(c, clock, cn)) return -1;
-    if (nb > 1) return -1;
+    if (nb > n) return -1;
     s.on_section(client);
-    if (nb == 1) {
+    for (uint32_t j = 0; j < nb; j++) {
       const uint32_t bpos = c.p;
       if (c.p >= c.end) return -1;
       const uint32_t info = lds_byte(w, c.p++);
@@ -138,9 +141,10 @@ template <class S> YM_INLINE int fast_walk(const uint32_t *w, uint32_t start, ui
           return -1;
         }
       }
-      if (!(bi.kind == BK_ITEM && bi.len == 0)) {
+      if (!(bi.kind == BK_ITEM && bi.len == 0)) { // Item::new -> None: dropped
         if ((uint64_t)clock + bi.len > 0xFFFFFFFFull) return -1;
         YM_TRY(s.on_block(client, clock, bi, bpos - start, c.p - bpos));
+        clock += bi.len;
       }
     }
   }

@@ -541,6 +541,7 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
   {
     uint32_t NBr = 0, NEr = 0, NRr = 0;
     uint64_t g_rec = 0, g_scan = 0, g_write = 0, g_slow = 0; // diagnostic sub-phase sums (thread 0, stamps only)
+    uint64_t g_r0 = 0, g_w0 = 0, g_rmax = 0, g_wmax = 0;      // round 0 / slowest later round
     for (uint32_t r0 = 0; r0 < U; r0 += NT) {
       const uint64_t tg0 = o.stamps ? __builtin_amdgcn_s_memtime() : 0;
       const uint32_t i = r0 + t;
@@ -560,6 +561,7 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
         w4 = x2.x;
         w5 = x2.y;
         if (w0 & REC_SLOW) {
+          if (o.stamps) atomicAdd((unsigned long long *)&o.stamps[(size_t)d * 16 + 11], 1ull);
           uint32_t w[6];
           walk_record_hbm(in + ubase, ulen, w);
           w0 = w[0];
@@ -582,7 +584,6 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
         }
       }
       if (o.stamps) {
-        g_slow += __ballot(i < U && (w0 & REC_SLOW)) ? 1 : 0;
         __syncthreads();
       }
       const uint64_t tg1 = o.stamps ? __builtin_amdgcn_s_memtime() : 0;
@@ -597,6 +598,8 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
       if (o.stamps) {
         g_rec += tg1 - tg0;
         g_scan += tg2 - tg1;
+        if (r0 == 0) g_r0 = tg1 - tg0;
+        else g_rmax = g_rmax > tg1 - tg0 ? g_rmax : tg1 - tg0;
       }
       if (i < U) {
       if (shape == REC_BLOCK) {
@@ -645,14 +648,20 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
       }
       if (o.stamps) {
         __syncthreads();
-        g_write += __builtin_amdgcn_s_memtime() - tg2;
+        const uint64_t gw = __builtin_amdgcn_s_memtime() - tg2;
+        g_write += gw;
+        if (r0 == 0) g_w0 = gw;
+        else g_wmax = g_wmax > gw ? g_wmax : gw;
       }
     }
     if (o.stamps && t == 0) {
       o.stamps[(size_t)d * 16 + 8] = g_rec;
       o.stamps[(size_t)d * 16 + 9] = g_scan;
       o.stamps[(size_t)d * 16 + 10] = g_write;
-      o.stamps[(size_t)d * 16 + 11] = g_slow;
+      o.stamps[(size_t)d * 16 + 12] = g_r0;
+      o.stamps[(size_t)d * 16 + 13] = g_rmax;
+      o.stamps[(size_t)d * 16 + 14] = g_w0;
+      o.stamps[(size_t)d * 16 + 15] = g_wmax;
     }
   }
   __syncthreads();
