@@ -33,12 +33,16 @@ def main_big(n, kind="c3"):
     tot = d.sum(axis=1)
     print(f"tiled docs: {ok.sum()}, updates/doc mean {U.mean():.0f}, cycles/doc mean {tot.mean():.0f}, "
           f"cycles/update {(tot / U).mean():.0f}")
-    g = st[ok][:, 8:12].astype(np.float64)
-    print(f"  gather sub-phases (thread 0): records+walks {g[:, 0].mean():.0f}, scans {g[:, 1].mean():.0f}, "
-          f"writes {g[:, 2].mean():.0f}; REC_SLOW updates walked {g[:, 3].mean():.1f}")
-    r = st[ok][:, 12:16].astype(np.float64)
-    print(f"  per round: records round0 {r[:, 0].mean():.0f} / slowest later {r[:, 1].mean():.0f}; "
-          f"writes round0 {r[:, 2].mean():.0f} / slowest later {r[:, 3].mean():.0f}")
+    s = st[ok].astype(np.int64)
+    om = s[:, 8] > 0
+    if om.any():
+        print(f"  classify: {om.sum()} docs in overlap mode: pass 0 {(s[om, 8] - s[om, 2]).mean():.0f}, "
+              f"run order {(s[om, 9] - s[om, 8]).mean():.0f}, pass 1 {(s[om, 3] - s[om, 9]).mean():.0f}")
+        print(f"  run order: runs {(s[om, 6] - s[om, 8]).mean():.0f}, predecessors {(s[om, 13] - s[om, 6]).mean():.0f}, "
+              f"sort {(s[om, 14] - s[om, 13]).mean():.0f}, tie rounds {(s[om, 15] - s[om, 14]).mean():.0f}, "
+              f"GC ties + positions {(s[om, 9] - s[om, 15]).mean():.0f}")
+    print(f"  deleteset: table+order {(s[:, 10] - s[:, 4]).mean():.0f}, range sort {(s[:, 11] - s[:, 10]).mean():.0f}, "
+          f"union {(s[:, 12] - s[:, 11]).mean():.0f}, write {(s[:, 5] - s[:, 12]).mean():.0f}")
     for i, nm in enumerate(BIG_NAMES):
         print(f"  {nm:10s} {d[:, i].mean():10.0f} cycles  {100 * d[:, i].mean() / tot.mean():5.1f}%")
     for lo, hi in ((0, 2000), (2000, 4000), (4000, 10001)):

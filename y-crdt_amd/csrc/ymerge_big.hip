@@ -28,6 +28,7 @@ namespace ym {
 constexpr uint32_t BIG_DCAP = 1024;   // distinct DeleteSet clients per document
 constexpr uint32_t BIG_DTAB = 2048;   // LDS hash slots for them (u64)
 constexpr uint32_t BIG_CHUNK = 2048;  // LDS bitonic chunk of the sort (key u64 + value u32)
+constexpr uint32_t BIG_LU_LDS = 8192; // overlap mode: updates / runs whose last-rank histogram stays in LDS
 // LDS union region (phase-local): sort chunk (24 KB) / output stage / DeleteSet tables:
 //   [0, 16K) client hash table  [16K, 44K) 7 per-client arrays  [44K, 68K) sort chunk / slots
 constexpr uint32_t BIG_OFF_DARR = 8 * BIG_DTAB, BIG_OFF_SCR = BIG_OFF_DARR + 7 * 4 * BIG_DCAP;
@@ -183,6 +184,100 @@ __global__ void __launch_bounds__(NT) k_big_count(BatchIn b, uint8_t *path, uint
   atomicAdd(n_big, 1u);
 }
 
+// ------------------------------------------------------------------ register bitonic
+// Ascending sort of BIG_CHUNK (key u64, value u32) pairs by (key, value) held in registers,
+// E = BIG_CHUNK / NT consecutive elements per lane: strides below E are exchanged inside the
+// lane, strides below 64 E across the wavefront by lane shuffles, and only the strides of
+// 64 E and more (6 of the 66 stages for NT = 512) go through LDS with two barriers each (the
+// LDS-only bitonic paid a barrier on every stage).  Positions at or past n are padding
+// (~0, ~0), sorted last; k / v hold the input and receive the first n results.
+template <int NT> __device__ void bitonic_reg(uint64_t *k, uint32_t *v, uint32_t n) {
+  constexpr uint32_t E = BIG_CHUNK / NT;
+  static_assert(E >= 1 && E * NT == BIG_CHUNK, "one chunk per workgroup");
+  const uint32_t t = threadIdx.x;
+  uint64_t x[E];
+  uint32_t y[E];
+#pragma unroll
+  for (uint32_t r = 0; r < E; r++) {
+    const uint32_t e = t * E + r;
+    x[r] = e < n ? k[e] : ~0ull;
+    y[r] = e < n ? v[e] : 0xFFFFFFFFu;
+  }
+  // element e at the lower position of its pair keeps the minimum in an ascending block
+  auto pick = [](uint64_t &a, uint32_t &av, uint64_t b, uint32_t bv, bool want_min) {
+    const bool g = a > b || (a == b && av > bv);
+    if (g == want_min) {
+      a = b;
+      av = bv;
+    }
+  };
+  for (uint32_t size = 2; size <= BIG_CHUNK; size <<= 1) {
+    for (uint32_t st = size >> 1; st > 0; st >>= 1) {
+      if (st >= 64 * E) {
+        __syncthreads();
+#pragma unroll
+        for (uint32_t r = 0; r < E; r++) {
+          k[t * E + r] = x[r];
+          v[t * E + r] = y[r];
+        }
+        __syncthreads();
+        uint64_t px[E];
+        uint32_t py[E];
+#pragma unroll
+        for (uint32_t r = 0; r < E; r++) {
+          const uint32_t e = t * E + r;
+          px[r] = k[e ^ st];
+          py[r] = v[e ^ st];
+        }
+#pragma unroll
+        for (uint32_t r = 0; r < E; r++) {
+          const uint32_t e = t * E + r;
+          pick(x[r], y[r], px[r], py[r], !(e & st) == !(e & size));
+        }
+      } else if (st >= E) {
+        const int ls = (int)(st / E);
+#pragma unroll
+        for (uint32_t r = 0; r < E; r++) {
+          const uint32_t e = t * E + r;
+          const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)x[r], ls, 64);
+          const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(x[r] >> 32), ls, 64);
+          const uint32_t pv = (uint32_t)__shfl_xor((int)y[r], ls, 64);
+          pick(x[r], y[r], ((uint64_t)hi << 32) | lo, pv, !(e & st) == !(e & size));
+        }
+      } else {
+#pragma unroll
+        for (uint32_t ss = 1; ss < E; ss <<= 1)
+          if (ss == st) {
+#pragma unroll
+            for (uint32_t r = 0; r < E; r++)
+              if (!(r & ss)) {
+                const uint32_t e = t * E + r;
+                const uint64_t a = x[r], b = x[r | ss];
+                const uint32_t av = y[r], bv = y[r | ss];
+                const bool g = a > b || (a == b && av > bv);
+                if (g == !(e & size)) {
+                  x[r] = b;
+                  y[r] = bv;
+                  x[r | ss] = a;
+                  y[r | ss] = av;
+                }
+              }
+          }
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t r = 0; r < E; r++) {
+    const uint32_t e = t * E + r;
+    if (e < n) {
+      k[e] = x[r];
+      v[e] = y[r];
+    }
+  }
+  __syncthreads();
+}
+
 // ------------------------------------------------------------------ workgroup sort
 // Stable sort of (key, value) pairs in HBM by key; values are distinct and ascending in
 // input order.  Chunks of BIG_CHUNK pairs are bitonic-sorted in LDS by (key, value) —
@@ -202,7 +297,7 @@ __device__ int wg_sort(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1, u
       cv[j] = g < n ? v0[g] : 0xFFFFFFFFu;
     }
     __syncthreads();
-    bitonic<NT>(ck, cv, CH);
+    bitonic_reg<NT>(ck, cv, CH);
     for (uint32_t j = threadIdx.x; j < CH; j += NT) {
       const uint32_t g = c0 + j;
       if (g < n) {
@@ -215,7 +310,19 @@ __device__ int wg_sort(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1, u
   uint64_t *ka = k0, *kb = k1;
   uint32_t *va = v0, *vb = v1;
   int which = 0;
+  // Merge passes.  The partner-run search runs over an LDS copy of every `stride`-th key
+  // (BIG_CHUNK samples, the chunk area is free now) and finishes over HBM in log2(stride)
+  // steps: a 4096-range DeleteSet (two chunks) merges with LDS reads only, instead of a
+  // dependent chain of 11 HBM loads per element.
+  uint64_t *smp = (uint64_t *)lds;
+  uint32_t stride = 1;
+  while ((n + stride - 1) / stride > BIG_CHUNK) stride <<= 1;
   for (uint32_t w = CH; w < n; w <<= 1) {
+    const bool sampled = stride <= w; // runs start at multiples of w: samples align with them
+    if (sampled) {
+      for (uint32_t q = threadIdx.x; q * stride < n; q += NT) smp[q] = ka[q * stride];
+      __syncthreads();
+    }
     for (uint32_t j = threadIdx.x; j < n; j += NT) {
       const uint64_t kj = ka[j];
       const uint32_t run = j / w, i = j - run * w;
@@ -225,6 +332,25 @@ __device__ int wg_sort(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1, u
       if (lo > n) lo = n;
       if (hi > n) hi = n;
       const uint32_t b0 = lo;
+      if (sampled && lo < hi) {
+        // samples q in [lo / stride, ceil(hi / stride)): the predicate holds on a prefix of the
+        // run, so the count of true samples s brackets the count: ((s-1) stride, s stride]
+        uint32_t qa = lo / stride, qb = (hi + stride - 1) / stride, q0 = qa;
+        while (qa < qb) {
+          const uint32_t mid = (qa + qb) >> 1;
+          const uint64_t km = smp[mid];
+          if (left ? (km < kj) : (km <= kj)) qa = mid + 1;
+          else qb = mid;
+        }
+        const uint32_t sn = qa - q0;
+        if (sn == 0) {
+          hi = lo;
+        } else {
+          const uint32_t nlo = b0 + (sn - 1) * stride + 1, nhi = b0 + sn * stride;
+          lo = nlo;
+          if (nhi < hi) hi = nhi;
+        }
+      }
       while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
         const uint64_t km = ka[mid];
@@ -313,22 +439,16 @@ __device__ __noinline__ bool big_splice_ok(const uint8_t *p, uint32_t n, uint32_
 // block at sorted position j (runs in order, blocks in run order).
 template <int NT>
 __device__ __noinline__ bool big_run_order(const BatchIn &b, uint64_t u0, uint32_t U, uint64_t B0, uint32_t NB,
-                                           BigMem &m, uint32_t *ws, uint32_t *sc, uint8_t *lds) {
+                                           BigMem &m, uint32_t *ws, uint32_t *sc, uint8_t *lds, uint64_t *stp) {
   const uint32_t t = threadIdx.x;
   constexpr uint32_t NONE = 0xFFFFFFFFu;
-  // 1 update of every block (the records keep the byte position), run heads and ids
-  const uint64_t *uo = b.upd_off + u0;
-  for (uint32_t j = t; j < NB; j += NT) {
-    const uint64_t x = B0 + m.bp[j];
-    uint32_t lo = 0, hi = U; // last update with uo[u] <= x
-    while (lo + 1 < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (uo[mid] <= x) lo = mid;
-      else hi = mid;
+  auto mark = [&](uint32_t k) { // diagnostic builds only (stp = this document's stamps)
+    if (stp) {
+      __syncthreads();
+      if (t == 0) stp[k] = __builtin_amdgcn_s_memtime();
     }
-    m.bu[j] = lo;
-  }
-  __syncthreads();
+  };
+  // 1 run heads and ids (m.bu: the update of every block, written by the gather)
   uint32_t NRun = 0;
   for (uint32_t base = 0; base < NB; base += NT) {
     const uint32_t j = base + t;
@@ -352,6 +472,7 @@ __device__ __noinline__ bool big_run_order(const BatchIn &b, uint64_t u0, uint32
   }
   __syncthreads();
   for (uint32_t r = t; r < NRun; r += NT) m.Rn[r] = (r + 1 < NRun ? m.Rb[r + 1] : NB) - m.Rb[r];
+  mark(6);
   // 2 predecessor of every run in its update's stream (clients descending): sort by
   //   (update, client desc); a repeated (update, client) -> exact engine
   uint32_t bad = 0;
@@ -377,6 +498,7 @@ __device__ __noinline__ bool big_run_order(const BatchIn &b, uint64_t u0, uint32
     m.Rp[r] = pr;
   }
   if (__syncthreads_or(bad)) return false;
+  mark(13);
   // 3 runs by (client desc, start asc, run id): run ids ascend with the update index
   for (uint32_t r = t; r < NRun; r += NT) {
     m.k0[r] = ((uint64_t)(uint32_t)~m.Rc[r] << 32) | m.Rs[r];
@@ -396,6 +518,7 @@ __device__ __noinline__ bool big_run_order(const BatchIn &b, uint64_t u0, uint32
     m.Rpos[r] = j;
   }
   __syncthreads();
+  mark(14);
   auto key = [&](uint32_t r) -> uint64_t { return ((uint64_t)m.Rc[r] << 32) | m.Rs[r]; };
   // 4 tie groups: one lane per group re-sorts it by the predecessors' current ranks
   for (uint32_t round = 0;; round++) {
@@ -435,20 +558,55 @@ __device__ __noinline__ bool big_run_order(const BatchIn &b, uint64_t u0, uint32
     }
     __syncthreads();
   }
+  mark(15);
   // 5 Item-vs-GC ties consumed while <= 20 decoders are live: last rank (+1) per update,
   //   V = the smallest v with #{u : lu[u] >= v} <= 20, tail = ranks >= V - 1
-  for (uint32_t u = t; u < U; u += NT) m.lu[u] = 0;
-  __syncthreads();
-  for (uint32_t j = t; j < NRun; j += NT) atomicMax(&m.lu[m.Ru[m.Rord[j]]], j + 1);
-  __syncthreads();
-  uint32_t lo = 1, hi = NRun + 1;
-  while (lo < hi) { // uniform
-    const uint32_t mid = (lo + hi) >> 1;
-    uint32_t c = 0, T;
-    for (uint32_t u = t; u < U; u += NT) c += m.lu[u] >= mid;
-    bscan_sum<NT>(c, ws, T);
-    if (T <= 20) hi = mid;
-    else lo = mid + 1;
+  uint32_t lo = 1;
+  if (U <= BIG_LU_LDS && NRun + 1 <= BIG_LU_LDS) {
+    // in LDS: lu per update, then a histogram of lu; #{lu >= v} <= 20 <=> #{lu < v} >= U - 20,
+    // so V is the first v >= 1 where the histogram's prefix reaches U - 20
+    uint32_t *llu = (uint32_t *)lds, *hist = llu + BIG_LU_LDS;
+    for (uint32_t u = t; u < BIG_LU_LDS; u += NT) {
+      llu[u] = 0;
+      hist[u] = 0;
+    }
+    if (t == 0) sc[4] = NRun + 1;
+    __syncthreads();
+    for (uint32_t j = t; j < NRun; j += NT) atomicMax(&llu[m.Ru[m.Rord[j]]], j + 1);
+    __syncthreads();
+    for (uint32_t u = t; u < U; u += NT) atomicAdd(&hist[llu[u]], 1u);
+    __syncthreads();
+    constexpr uint32_t C = BIG_LU_LDS / NT; // histogram slots per lane, contiguous
+    uint32_t csum = 0;
+    for (uint32_t q = 0; q < C; q++) csum += hist[t * C + q];
+    uint32_t T;
+    uint32_t pre = bscan_sum<NT>(csum, ws, T);
+    const uint32_t goal = U > 20 ? U - 20 : 0;
+    for (uint32_t q = 0; q < C; q++) {
+      const uint32_t v = t * C + q; // prefix(v) = pre = #{lu < v}
+      if (v >= 1 && v <= NRun + 1 && pre >= goal) {
+        atomicMin(&sc[4], v);
+        break;
+      }
+      pre += hist[v];
+    }
+    __syncthreads();
+    lo = sc[4];
+    __syncthreads();
+  } else {
+    for (uint32_t u = t; u < U; u += NT) m.lu[u] = 0;
+    __syncthreads();
+    for (uint32_t j = t; j < NRun; j += NT) atomicMax(&m.lu[m.Ru[m.Rord[j]]], j + 1);
+    __syncthreads();
+    uint32_t hi = NRun + 1;
+    while (lo < hi) { // uniform
+      const uint32_t mid = (lo + hi) >> 1;
+      uint32_t c = 0, T;
+      for (uint32_t u = t; u < U; u += NT) c += m.lu[u] >= mid;
+      bscan_sum<NT>(c, ws, T);
+      if (T <= 20) hi = mid;
+      else lo = mid + 1;
+    }
   }
   const uint32_t V = lo;
   for (uint32_t j = t; j < NRun; j += NT) {
@@ -520,6 +678,13 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
     }
   };
   stamp(0);
+  // sub-phase marks (slots 8..12): classify pass 0 / run order, DeleteSet table / range sort / union
+  auto mark = [&](uint32_t k) {
+    if (o.stamps) {
+      __syncthreads();
+      if (t == 0) o.stamps[(size_t)d * 16 + k] = __builtin_amdgcn_s_memtime();
+    }
+  };
   auto finish = [&](uint8_t p, uint8_t st, uint64_t len) {
     if (t == 0) {
       if (p == 1) {
@@ -561,7 +726,6 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
         w4 = x2.x;
         w5 = x2.y;
         if (w0 & REC_SLOW) {
-          if (o.stamps) atomicAdd((unsigned long long *)&o.stamps[(size_t)d * 16 + 11], 1ull);
           uint32_t w[6];
           walk_record_hbm(in + ubase, ulen, w);
           w0 = w[0];
@@ -608,6 +772,7 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
         m.bl[pb] = w3;
         m.bp[pb] = ubase + w4;
         m.bm[pb] = w5;
+        m.bu[pb] = i;
       } else if (shape == REC_DS) {
         m.ec[pe] = w1;
         m.et[pe] = 0x80000000u | (i << 8);
@@ -629,6 +794,7 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
           m.bl[pb + k] = ov[5 * k + 2];
           m.bp[pb + k] = ubase + ov[5 * k + 3];
           m.bm[pb + k] = ov[5 * k + 4];
+          m.bu[pb + k] = i;
         }
         ov += 5 * snb;
         for (uint32_t k = 0; k < sne; k++) {
@@ -644,6 +810,7 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
       } else if (shape == REC_COMPLEX) {
         FastFill f{m.bc, m.bk, m.bl, m.bp, m.bm, m.ec, m.et, m.rs, m.re, m.ri, i, ubase, pb, pe, pr, 0};
         fill_hbm(in + ubase, ulen, &f);
+        for (uint32_t k = 0; k < snb; k++) m.bu[pb + k] = i;
       }
       }
       if (o.stamps) {
@@ -655,13 +822,13 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
       }
     }
     if (o.stamps && t == 0) {
-      o.stamps[(size_t)d * 16 + 8] = g_rec;
-      o.stamps[(size_t)d * 16 + 9] = g_scan;
-      o.stamps[(size_t)d * 16 + 10] = g_write;
-      o.stamps[(size_t)d * 16 + 12] = g_r0;
-      o.stamps[(size_t)d * 16 + 13] = g_rmax;
-      o.stamps[(size_t)d * 16 + 14] = g_w0;
-      o.stamps[(size_t)d * 16 + 15] = g_wmax;
+      (void)g_rec;
+      (void)g_scan;
+      (void)g_write;
+      (void)g_r0;
+      (void)g_rmax;
+      (void)g_w0;
+      (void)g_wmax;
     }
   }
   __syncthreads();
@@ -892,7 +1059,10 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
       return;
     }
     if (vp & 1) { // partial overlap / same-clock mismatch: the run order of the yrs loop
-      if (!big_run_order<NT>(b, u0, U, B0, NB, m, ws, sc, S.un)) {
+      mark(8);
+      const bool ro = big_run_order<NT>(b, u0, U, B0, NB, m, ws, sc, S.un, o.stamps ? o.stamps + (size_t)d * 16 : nullptr);
+      mark(9);
+      if (!ro) {
         finish(1, 0, 0);
         return;
       }
@@ -1078,7 +1248,7 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
       uint32_t *tv = (uint32_t *)lscr; // values (unused by the order)
       for (uint32_t j = t; j < BIG_DTAB; j += NT) tv[j] = j;
       __syncthreads();
-      bitonic<NT>(dtab, tv, BIG_DTAB);
+      bitonic_reg<NT>(dtab, tv, BIG_DTAB);
     }
     for (uint32_t j = t; j < D; j += NT) {
       d_client[j] = (uint32_t)(dtab[j] >> 32);
@@ -1091,7 +1261,7 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
       uint32_t *tv = (uint32_t *)lscr;
       for (uint32_t j = t; j < BIG_DTAB; j += NT) tv[j] = j;
       __syncthreads();
-      bitonic<NT>(dtab, tv, BIG_DTAB);
+      bitonic_reg<NT>(dtab, tv, BIG_DTAB);
     }
   }
   // hashbrown emulation (single lane; D <= BIG_DCAP): slots hold rank + 1
@@ -1143,31 +1313,68 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
       if (slot_arr[q]) d_ord[k++] = slot_arr[q] - 1;
   }
   __syncthreads();
-  // live ranges sorted by (client, start, index)
+  mark(10);
+  // live ranges sorted by (client, start, index).  One pass builds the keys, counts the
+  // live ones and checks the order; four ranges per lane per trip with every load of the
+  // trip issued before the first use (the loop was a chain of dependent HBM round trips)
   const uint64_t *dkey = m.k0;
   const uint32_t *dval = m.v0;
+  uint32_t NL;
   {
-    uint32_t bad = 0;
-    for (uint32_t j = t; j < NR; j += NT) {
-      const bool live = m.et[m.ri[j]] & 0x80000000u;
-      m.k0[j] = live ? (((uint64_t)m.ec[m.ri[j]] << 32) | m.rs[j]) : ~0ull;
-      m.v0[j] = j;
+    const uint32_t *__restrict__ g_ri = m.ri, *__restrict__ g_rs = m.rs, *__restrict__ g_et = m.et,
+                   *__restrict__ g_ec = m.ec;
+    uint64_t *__restrict__ g_k0 = m.k0;
+    uint32_t *__restrict__ g_v0 = m.v0;
+    const uint32_t lane = t & 63;
+    uint32_t bad = 0, live_n = 0;
+    constexpr uint32_t RB = 4;
+    for (uint32_t j0 = t; j0 < NR; j0 += RB * NT) {
+      uint32_t xi[RB], xs[RB], pi[RB], ps[RB];
+#pragma unroll
+      for (uint32_t q = 0; q < RB; q++) {
+        const uint32_t j = j0 + q * NT;
+        xi[q] = j < NR ? g_ri[j] : 0;
+        xs[q] = j < NR ? g_rs[j] : 0;
+        // lane 0 also builds the key of j - 1 (the previous lane's key belongs to another wave)
+        const bool pv = lane == 0 && j > 0 && j <= NR;
+        pi[q] = pv ? g_ri[j - 1] : 0;
+        ps[q] = pv ? g_rs[j - 1] : 0;
+      }
+      uint32_t xt[RB], xc[RB], pt[RB], pc[RB];
+#pragma unroll
+      for (uint32_t q = 0; q < RB; q++) {
+        const uint32_t j = j0 + q * NT;
+        xt[q] = j < NR ? g_et[xi[q]] : 0;
+        xc[q] = j < NR ? g_ec[xi[q]] : 0;
+        const bool pv = lane == 0 && j > 0 && j <= NR;
+        pt[q] = pv ? g_et[pi[q]] : 0;
+        pc[q] = pv ? g_ec[pi[q]] : 0;
+      }
+#pragma unroll
+      for (uint32_t q = 0; q < RB; q++) {
+        const uint32_t j = j0 + q * NT;
+        const bool live = xt[q] & 0x80000000u;
+        const uint64_t key = live ? (((uint64_t)xc[q] << 32) | xs[q]) : ~0ull;
+        if (j < NR) {
+          g_k0[j] = key;
+          g_v0[j] = j;
+          live_n += live;
+        }
+        const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)key, 1, 64);
+        const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)(key >> 32), 1, 64);
+        uint64_t prev = ((uint64_t)hi << 32) | lo;
+        if (lane == 0) prev = (pt[q] & 0x80000000u) ? (((uint64_t)pc[q] << 32) | ps[q]) : ~0ull;
+        if (j < NR && j > 0 && prev > key) bad = 1;
+      }
     }
-    __syncthreads();
-    for (uint32_t j = t; j + 1 < NR; j += NT)
-      if (m.k0[j] > m.k0[j + 1]) bad = 1;
+    bscan_sum<NT>(live_n, ws, NL);
     if (__syncthreads_or(bad) && wg_sort<NT>(m.k0, m.v0, m.k1, m.v1, NR, lscr)) {
       dkey = m.k1;
       dval = m.v1;
     }
   }
+  mark(11);
   uint64_t *dk = (uint64_t *)dkey; // the component starts are stashed in the keys' low halves
-  uint32_t NL;
-  {
-    uint32_t c = 0;
-    for (uint32_t j = t; j < NR; j += NT) c += dkey[j] != ~0ull;
-    bscan_sum<NT>(c, ws, NL);
-  }
   // union pass 1: component heads (start after the running end of the client) and the
   // inclusive running end; pass 2: component starts, sizes, offsets, head prefix counts
   {
@@ -1235,6 +1442,7 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
     }
   }
   __syncthreads();
+  mark(12);
   // per distinct client (rank r, ascending client): [a, b) of the sorted live ranges
   for (uint32_t r = t; r < D; r += NT) {
     const uint32_t c = d_client[r];
