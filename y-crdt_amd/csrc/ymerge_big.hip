@@ -323,43 +323,86 @@ __device__ int wg_sort(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1, u
       for (uint32_t q = threadIdx.x; q * stride < n; q += NT) smp[q] = ka[q * stride];
       __syncthreads();
     }
-    for (uint32_t j = threadIdx.x; j < n; j += NT) {
-      const uint64_t kj = ka[j];
-      const uint32_t run = j / w, i = j - run * w;
-      const bool left = !(run & 1);
-      const uint32_t base = (left ? run : run - 1) * w;
-      uint32_t lo = left ? base + w : base, hi = left ? base + 2 * w : base + w;
-      if (lo > n) lo = n;
-      if (hi > n) hi = n;
-      const uint32_t b0 = lo;
-      if (sampled && lo < hi) {
-        // samples q in [lo / stride, ceil(hi / stride)): the predicate holds on a prefix of the
-        // run, so the count of true samples s brackets the count: ((s-1) stride, s stride]
-        uint32_t qa = lo / stride, qb = (hi + stride - 1) / stride, q0 = qa;
-        while (qa < qb) {
-          const uint32_t mid = (qa + qb) >> 1;
-          const uint64_t km = smp[mid];
-          if (left ? (km < kj) : (km <= kj)) qa = mid + 1;
-          else qb = mid;
+    // four elements per lane per trip, each step's loads issued together (the chain per
+    // element is key -> LDS samples -> log2(stride) HBM steps -> value)
+    constexpr uint32_t MB = 4;
+    for (uint32_t j0 = threadIdx.x; j0 < n; j0 += MB * NT) {
+      uint64_t kj[MB];
+      uint32_t lo[MB], hi[MB], b0[MB], base[MB];
+      bool left[MB];
+#pragma unroll
+      for (uint32_t q = 0; q < MB; q++) {
+        const uint32_t j = j0 + q * NT;
+        kj[q] = j < n ? ka[j] : 0;
+      }
+#pragma unroll
+      for (uint32_t q = 0; q < MB; q++) {
+        const uint32_t j = j0 + q * NT < n ? j0 + q * NT : n - 1;
+        const uint32_t run = j / w;
+        left[q] = !(run & 1);
+        base[q] = (left[q] ? run : run - 1) * w;
+        uint32_t l = left[q] ? base[q] + w : base[q], h = left[q] ? base[q] + 2 * w : base[q] + w;
+        if (l > n) l = n;
+        if (h > n) h = n;
+        b0[q] = l;
+        if (sampled && l < h) {
+          // samples q in [l / stride, ceil(h / stride)): the predicate holds on a prefix of
+          // the run, so the count of true samples sn brackets the count: ((sn-1) stride, sn stride]
+          uint32_t qa = l / stride, qb = (h + stride - 1) / stride;
+          const uint32_t q0 = qa;
+          while (qa < qb) {
+            const uint32_t mid = (qa + qb) >> 1;
+            const uint64_t km = smp[mid];
+            if (left[q] ? (km < kj[q]) : (km <= kj[q])) qa = mid + 1;
+            else qb = mid;
+          }
+          const uint32_t sn = qa - q0;
+          if (sn == 0) {
+            h = l;
+          } else {
+            const uint32_t nh = l + sn * stride;
+            l = l + (sn - 1) * stride + 1;
+            if (nh < h) h = nh;
+          }
         }
-        const uint32_t sn = qa - q0;
-        if (sn == 0) {
-          hi = lo;
-        } else {
-          const uint32_t nlo = b0 + (sn - 1) * stride + 1, nhi = b0 + sn * stride;
-          lo = nlo;
-          if (nhi < hi) hi = nhi;
+        lo[q] = l;
+        hi[q] = h;
+      }
+      // HBM steps in lockstep over the four searches
+      for (;;) {
+        bool any = false;
+        uint64_t km[MB];
+#pragma unroll
+        for (uint32_t q = 0; q < MB; q++) {
+          const bool act = lo[q] < hi[q];
+          any |= act;
+          km[q] = act ? ka[(lo[q] + hi[q]) >> 1] : 0;
+        }
+        if (!any) break;
+#pragma unroll
+        for (uint32_t q = 0; q < MB; q++) {
+          if (lo[q] < hi[q]) {
+            const uint32_t mid = (lo[q] + hi[q]) >> 1;
+            if (left[q] ? (km[q] < kj[q]) : (km[q] <= kj[q])) lo[q] = mid + 1;
+            else hi[q] = mid;
+          }
         }
       }
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        const uint64_t km = ka[mid];
-        if (left ? (km < kj) : (km <= kj)) lo = mid + 1;
-        else hi = mid;
+      uint32_t vj[MB];
+#pragma unroll
+      for (uint32_t q = 0; q < MB; q++) {
+        const uint32_t j = j0 + q * NT;
+        vj[q] = j < n ? va[j] : 0;
       }
-      const uint32_t dst = base + i + (lo - b0);
-      kb[dst] = kj;
-      vb[dst] = va[j];
+#pragma unroll
+      for (uint32_t q = 0; q < MB; q++) {
+        const uint32_t j = j0 + q * NT;
+        if (j < n) {
+          const uint32_t dst = base[q] + (j - (j / w) * w) + (lo[q] - b0[q]);
+          kb[dst] = kj[q];
+          vb[dst] = vj[q];
+        }
+      }
     }
     __syncthreads();
     uint64_t *tk = ka;
