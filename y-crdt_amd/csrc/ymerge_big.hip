@@ -93,6 +93,23 @@ __device__ inline BigMem big_carve(uint32_t *w, uint32_t NB, uint32_t NE, uint32
   m.lu = take(U);
   return m;
 }
+// The tables' addresses are per document, so wave-uniform: pinned to scalar registers (the
+// compiler otherwise kept several of them as VGPR pairs, a large part of the kernel's spills)
+template <class T> __device__ __forceinline__ T *uni_ptr(T *p) {
+  const uint64_t x = (uint64_t)p;
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
+  return (T *)(((uint64_t)hi << 32) | lo);
+}
+__device__ inline void big_uniform(BigMem &m) {
+  uint32_t **p32[] = {&m.bc, &m.bk, &m.bl, &m.bp, &m.bm, &m.v0, &m.v1, &m.fE, &m.fF, &m.sseg, &m.fO, &m.ec, &m.et,
+                      &m.rs, &m.re, &m.ri, &m.chead, &m.cend, &m.coff, &m.cpre, &m.bu, &m.rr, &m.sord, &m.Rb, &m.Rn,
+                      &m.Rc, &m.Rs, &m.Ru, &m.Rk, &m.Rp, &m.Rpos, &m.Rord, &m.Rord2, &m.Roff, &m.lu};
+#pragma unroll
+  for (uint32_t i = 0; i < sizeof(p32) / sizeof(p32[0]); i++) *p32[i] = uni_ptr(*p32[i]);
+  m.k0 = uni_ptr(m.k0);
+  m.k1 = uni_ptr(m.k1);
+}
 
 // ------------------------------------------------------------------ k_big_count
 // One workgroup per document with path == 2 (handed over by k_fast_merge for capacity):
@@ -703,6 +720,7 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
   const uint64_t u0 = b.doc_upd[d], u1 = b.doc_upd[d + 1];
   const uint32_t U = (uint32_t)(u1 - u0);
   BigMem m = big_carve(scratch + scr_off[d], NB, NE, NR, U);
+  big_uniform(m);
   const uint64_t B0 = b.upd_off[u0];
   const uint32_t nbytes = (uint32_t)(b.upd_off[u1] - B0);
   const uint8_t *in = b.bytes + B0;
@@ -1103,7 +1121,10 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
     }
     if (vp & 1) { // partial overlap / same-clock mismatch: the run order of the yrs loop
       mark(8);
-      const bool ro = big_run_order<NT>(b, u0, U, B0, NB, m, ws, sc, S.un, o.stamps ? o.stamps + (size_t)d * 16 : nullptr);
+      // (a copy: the callee takes the tables by reference, which would otherwise keep the
+      // kernel's own BigMem in scratch memory for every access of every phase)
+      BigMem mc = m;
+      const bool ro = big_run_order<NT>(b, u0, U, B0, NB, mc, ws, sc, S.un, o.stamps ? o.stamps + (size_t)d * 16 : nullptr);
       mark(9);
       if (!ro) {
         finish(1, 0, 0);
