@@ -1181,7 +1181,7 @@ YM_INLINE uint32_t pw_spec(const uint32_t *w, uint32_t p, uint32_t cs, uint32_t 
 // (no u32 overflow; DIFF: squashed, canonical), its plan record written to de (DEW words, lane
 // 0).  false: a shape for k_plan (malformed, unsquashed, more than capE entries).
 template <bool DIFF>
-__device__ __noinline__ bool pw_deleteset(uint32_t *u, uint32_t *de, const uint8_t *up, uint32_t un, uint32_t P,
+__device__ __forceinline__ bool pw_deleteset(uint32_t *u, uint32_t *de, const uint8_t *up, uint32_t un, uint32_t P,
                                           uint32_t lane, uint32_t capE, uint32_t &nds) {
   const uintptr_t A0 = (uintptr_t)up;
   int32_t wb = 0;
@@ -1318,7 +1318,7 @@ __device__ __noinline__ bool pw_deleteset(uint32_t *u, uint32_t *de, const uint8
 
 // One document on one wavefront (all 64 lanes call it with the same d).
 template <bool DIFF>
-__device__ __noinline__ void pw_plan_doc(const DiffBatch &b, const PlanScratch &ps, PwLds &S, uint32_t lane,
+__device__ __forceinline__ void pw_plan_doc(const DiffBatch &b, const PlanScratch &ps, PwLds &S, uint32_t lane,
                                          uint32_t d) {
   if (b.pre_status && b.pre_status[d]) { // e.g. a y-sync message that is not SyncStep1
     if (lane == 0) {

@@ -19,12 +19,16 @@
 //   k_gs_ds     lane per run: the (start, length) varints
 //   k_gs_final  section header, DeleteSet header, length / status / path of the document.
 // Documents outside the shape keep path 2 and go to the tiled kernel as before.
+#include <algorithm>
 #include "ycodec.h"
 #include "ykernels.h"
 
 namespace ym {
 
-enum : uint32_t { GS_BAD = 0, GS_CMIN, GS_CMAX, GS_MAXEND, GS_FIRST = 4 /* u64 at words 4-5 */, GS_WORDS = 8 };
+enum : uint32_t {
+  GS_BAD = 0, GS_CMIN, GS_CMAX, GS_MAXEND, GS_FIRST = 4 /* u64 at words 4-5 */, GS_NW = 6 /* bitmap words */,
+  GS_K = 7 /* squashed ranges */, GS_WORDS = 8
+};
 enum : uint32_t {
   GSB_SLOW = 1,      // an update k_decode did not decode (exact walk needed)
   GSB_BLOCK = 2,     // a block that is not copied verbatim (re-encoded / panics)
@@ -114,6 +118,12 @@ __global__ void __launch_bounds__(256) k_gs_pre(GsArgs a) {
   }
 }
 
+// the document's output slot and its capacity (2 x its bytes + 64, as every path's slot)
+__device__ __forceinline__ uint8_t *gs_out(const GsArgs &a) { return a.out + 2 * a.upd_off[a.u0] + 64ull * a.d; }
+__device__ __forceinline__ uint64_t gs_cap(const GsArgs &a) {
+  return 2 * (a.upd_off[a.u0 + a.U] - a.upd_off[a.u0]) + 64;
+}
+
 __device__ __forceinline__ uint32_t gs_hdr(const GsArgs &a) { // bytes of the one-section header
   const uint32_t nbt = (uint32_t)a.s_cnt[a.U];
   return varlen(1) + varlen(nbt) + varlen(a.g[GS_CMIN]) + varlen((uint32_t)*(const uint64_t *)(a.g + GS_FIRST));
@@ -124,9 +134,14 @@ __global__ void __launch_bounds__(256) k_gs_write(GsArgs a) {
   if (i >= a.U) return;
   const uint32_t clock0 = (uint32_t)*(const uint64_t *)(a.g + GS_FIRST);
   uint64_t expect = clock0 + (a.s_bl[i] & 0xFFFFFFFFu);
-  uint8_t *dst = a.out + gs_hdr(a) + (a.s_bl[i] >> 32);
+  uint8_t *dst = gs_out(a) + gs_hdr(a) + (a.s_bl[i] >> 32);
   const uint8_t *src = a.bytes + a.upd_off[a.u0 + i];
   uint32_t bad = 0;
+  if (i == 0) { // bitmap words in use (the last one stays clear: run ends); over the buffer: bad
+    const uint32_t nw = a.g[GS_MAXEND] / 32 + 2;
+    a.g[GS_NW] = nw <= a.nwords ? nw : 0;
+    if (nw > a.nwords) bad |= GSB_RANGE;
+  }
   gs_visit(
       a, i,
       [&](uint32_t, uint32_t k, uint32_t len, uint32_t pos, uint32_t meta) {
@@ -160,17 +175,30 @@ __device__ __forceinline__ uint32_t gs_starts(const GsArgs &a, uint32_t j) {
   return w & ~((w << 1) | prev);
 }
 
+// kernels over the bitmap / the runs: grid-stride up to the counts on the device (the grid is
+// sized for the buffers' capacity, so no host round trip sits between the stages)
 __global__ void __launch_bounds__(256) k_gs_runs(GsArgs a) {
-  const uint32_t j = blockIdx.x * 256 + threadIdx.x;
-  if (j >= a.nwords) return;
-  a.w_cnt[j] = a.g[GS_BAD] ? 0 : __popc(gs_starts(a, j));
+  const uint32_t nw = a.g[GS_NW];
+  for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < nw; j += gridDim.x * 256)
+    a.w_cnt[j] = a.g[GS_BAD] ? 0 : __popc(gs_starts(a, j));
 }
 
 __global__ void __launch_bounds__(256) k_gs_comp(GsArgs a) {
-  const uint32_t j = blockIdx.x * 256 + threadIdx.x;
-  if (j >= a.nwords || a.g[GS_BAD]) return;
+  const uint32_t nw = a.g[GS_NW];
+  if (a.g[GS_BAD]) return;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    // (32-bit halves: this hipcc miscompiled the 64-bit uniform compare feeding a select,
+    // testing SCC after a VALU compare that set VCC)
+    const uint64_t K = a.w_scan[nw];
+    const uint32_t kl = (uint32_t)K, kh = (uint32_t)(K >> 32);
+    const uint32_t over = (kh != 0) | (kl > a.kcap);
+    a.g[GS_K] = kl & (over - 1u);
+    if (over) atomicOr(&a.g[GS_BAD], GSB_RANGE);
+  }
+  for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < nw; j += gridDim.x * 256) {
   uint32_t st = gs_starts(a, j);
   uint64_t k = a.w_scan[j];
+  if (k + __popc(st) > a.kcap) continue; // (the count check above makes the document bad)
   while (st) {
     const uint32_t b = __builtin_ctz(st);
     st &= st - 1;
@@ -184,35 +212,40 @@ __global__ void __launch_bounds__(256) k_gs_comp(GsArgs a) {
     a.k_size[k] = varlen(s) + varlen(e - s);
     k++;
   }
+  }
 }
 
 __device__ __forceinline__ uint64_t gs_ds_base(const GsArgs &a) {
-  const uint32_t K = (uint32_t)a.w_scan[a.nwords];
+  const uint32_t K = a.g[GS_K];
   return gs_hdr(a) + (a.s_bl[a.U] >> 32) + (K ? varlen(1) + varlen(a.g[GS_CMIN]) + varlen(K) : varlen(0));
 }
 
 __global__ void __launch_bounds__(256) k_gs_ds(GsArgs a) {
-  const uint32_t k = blockIdx.x * 256 + threadIdx.x;
-  if (a.g[GS_BAD] || k >= a.w_scan[a.nwords]) return;
-  Writer w{a.out + gs_ds_base(a) + a.k_off[k], 0};
-  w_var(w, a.k_start[k]);
-  w_var(w, a.k_len[k]);
+  if (a.g[GS_BAD]) return;
+  const uint32_t K = a.g[GS_K];
+  uint8_t *base = gs_out(a) + gs_ds_base(a);
+  for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < K; k += gridDim.x * 256) {
+    Writer w{base + a.k_off[k], 0};
+    w_var(w, a.k_start[k]);
+    w_var(w, a.k_len[k]);
+  }
 }
 
 __global__ void k_gs_final(GsArgs a, FastOut o) {
   if (threadIdx.x) return;
-  const uint32_t K = a.g[GS_BAD] ? 0 : (uint32_t)a.w_scan[a.nwords];
+  const uint32_t K = a.g[GS_BAD] ? 0 : a.g[GS_K];
   const uint64_t total = a.g[GS_BAD] ? 0 : gs_ds_base(a) + a.k_off[K];
-  if (a.g[GS_BAD] || total > a.cap) { // not the shape after all: the tiled kernel writes it
+  o.out_start[a.d] = 2 * a.upd_off[a.u0] + 64ull * a.d;
+  if (a.g[GS_BAD] || total > gs_cap(a)) { // not the shape after all: the tiled kernel writes it
     o.path[a.d] = 2;
     return;
   }
-  Writer w{a.out, 0};
+  Writer w{gs_out(a), 0};
   w_var(w, 1);
   w_var(w, (uint32_t)a.s_cnt[a.U]);
   w_var(w, a.g[GS_CMIN]);
   w_var(w, (uint32_t)*(const uint64_t *)(a.g + GS_FIRST));
-  Writer v{a.out + gs_hdr(a) + (a.s_bl[a.U] >> 32), 0};
+  Writer v{gs_out(a) + gs_hdr(a) + (a.s_bl[a.U] >> 32), 0};
   if (K) {
     w_var(v, 1);
     w_var(v, a.g[GS_CMIN]);
@@ -253,13 +286,14 @@ void launch_gs_find(const BatchIn &b, uint8_t *path, uint32_t min_u, uint64_t *l
 void launch_gs_pre(const GsArgs &a, hipStream_t s) {
   hipLaunchKernelGGL(k_gs_pre, dim3((a.U + 255) / 256), dim3(256), 0, s, a);
 }
-void launch_gs_rest(const GsArgs &a, const FastOut &o, uint32_t n_ranges, uint64_t *scan_tmp, hipStream_t s) {
+void launch_gs_rest(const GsArgs &a, const FastOut &o, uint64_t *scan_tmp, hipStream_t s) {
+  const uint32_t gw = std::min<uint32_t>((a.nwords + 255) / 256, 1024u), gk = std::min<uint32_t>((a.kcap + 255) / 256, 1024u);
   hipLaunchKernelGGL(k_gs_write, dim3((a.U + 255) / 256), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(k_gs_runs, dim3((a.nwords + 255) / 256), dim3(256), 0, s, a);
-  launch_scan_u64(a.w_cnt, a.w_scan, a.nwords, scan_tmp, s);
-  hipLaunchKernelGGL(k_gs_comp, dim3((a.nwords + 255) / 256), dim3(256), 0, s, a);
-  launch_scan_u64(a.k_size, a.k_off, n_ranges + 1, scan_tmp, s);
-  hipLaunchKernelGGL(k_gs_ds, dim3((n_ranges + 256) / 256), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_gs_runs, dim3(gw), dim3(256), 0, s, a);
+  launch_scan_u64(a.w_cnt, a.w_scan, a.nwords, scan_tmp, s, a.g + GS_NW);
+  hipLaunchKernelGGL(k_gs_comp, dim3(gw), dim3(256), 0, s, a);
+  launch_scan_u64(a.k_size, a.k_off, a.kcap, scan_tmp, s, a.g + GS_K);
+  hipLaunchKernelGGL(k_gs_ds, dim3(gk), dim3(256), 0, s, a);
   hipLaunchKernelGGL(k_gs_final, dim3(1), dim3(64), 0, s, a, o);
 }
 

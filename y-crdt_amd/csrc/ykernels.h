@@ -76,20 +76,20 @@ struct GsArgs {
   const uint32_t *rec, *ovf;
   uint64_t u0;
   uint32_t U, d;
-  uint8_t *out; // the document's slot
-  uint64_t cap;
+  uint8_t *out; // the output arena (the document's slot is 2 x its first byte + 64 x d, on the device)
   uint64_t *cnt, *bl;    // [U]: blocks | ranges << 32, block bytes << 32 | clock lengths
   uint64_t *s_cnt, *s_bl; // [U + 1] exclusive scans
   uint32_t *g;                         // flags / client min, max / max range end / first block key
   uint32_t *bm;                        // deleted-clock bitmap [nwords]
-  uint32_t nbits, nwords;
+  uint32_t nbits, nwords;              // bitmap capacity (bits, words); the words in use are on the device
+  uint32_t kcap;                       // squashed-range capacity
   uint64_t *w_cnt, *w_scan;            // run starts per word, scan [nwords + 1]
   uint32_t *k_start, *k_len;           // runs = squashed ranges
   uint64_t *k_size, *k_off;
 };
 void launch_gs_find(const BatchIn &b, uint8_t *path, uint32_t min_u, uint64_t *list, hipStream_t s);
 void launch_gs_pre(const GsArgs &a, hipStream_t s);
-void launch_gs_rest(const GsArgs &a, const FastOut &o, uint32_t n_ranges, uint64_t *scan_tmp, hipStream_t s);
+void launch_gs_rest(const GsArgs &a, const FastOut &o, uint64_t *scan_tmp, hipStream_t s);
 
 // store-based compaction (ycompact.hip): one lane per document applies its updates to a
 // device block store; documents outside the device shape get status E_UNSUPPORTED.
@@ -114,7 +114,9 @@ void launch_seq_merge(bool write, const BatchIn &b, const uint8_t *path, const u
                       uint8_t *out, uint64_t out_base, uint64_t *out_start, uint64_t *out_len, uint8_t *status_out,
                       hipStream_t s);
 // exclusive scan: out[0..n] (out[n] = total); tmp needs >= (n/2048 + 2) u64
-void launch_scan_u64(const uint64_t *in, uint64_t *out, uint32_t n, uint64_t *tmp, hipStream_t s);
+// n_dev: optional device-side element count (<= n, the count the grid is sized for)
+void launch_scan_u64(const uint64_t *in, uint64_t *out, uint32_t n, uint64_t *tmp, hipStream_t s,
+                     const uint32_t *n_dev = nullptr);
 size_t scan_tmp_elems(uint32_t n);
 void launch_pack(const uint8_t *src, const uint64_t *start, const uint64_t *len, const uint64_t *pack_off,
                  uint8_t *dst, uint32_t n_docs, hipStream_t s);

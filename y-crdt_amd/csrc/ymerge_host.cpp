@@ -86,6 +86,7 @@ struct ymerge_ctx {
   bool lean = true; // k_lean first (env YMERGE_LEAN=0: every document through k_decode + k_fast_merge)
   bool pack_stale = false; // pack_off not computed for the last merge (all documents on k_lean)
   uint32_t giant_min = ym::GS_MIN_U; // updates of a document for the grid-wide path (env YMERGE_GIANT_MIN, 0: off)
+  bool giant_lane = true; // a batch of one such document skips the per-document routing (env YMERGE_GIANT_LANE=0: off)
   int lean_order = -1; // k_lean longest-first dispatch: env YMERGE_LEAN_ORDER 0/1, default for >= 8192 small docs
   // diff / SV common-shape planner (env YMERGE_PLANNER): 0 "lane" k_plan_lane + k_plan_wave for
   // long updates (default: C5 k_plan 4.24 -> 3.3 ms against the ring planner), 1 "ring"
@@ -121,6 +122,7 @@ static bool ctx_init(ymerge_ctx *c, int device) {
   if (const char *v = getenv("YMERGE_LEAN")) c->lean = atoi(v) != 0;
   if (const char *v = getenv("YMERGE_COMPACT_LPW")) c->compact_lpw = (uint32_t)atoi(v);
   if (const char *v = getenv("YMERGE_GIANT_MIN")) c->giant_min = (uint32_t)atoi(v);
+  if (const char *v = getenv("YMERGE_GIANT_LANE")) c->giant_lane = atoi(v) != 0;
   if (const char *v = getenv("YMERGE_LEAN_ORDER")) c->lean_order = atoi(v);
   if (const char *v = getenv("YMERGE_PLANNER"))
     c->planner = strcmp(v, "ring") == 0 ? 1u : strcmp(v, "wave") == 0 ? 2u : 0u;
@@ -279,23 +281,31 @@ static bool ensure_keep(ymerge_ctx *c, DevBuf &b, size_t bytes, size_t keep) {
   return true;
 }
 
-// One long single-client document over the whole GPU (ygiant.hip); leaves it on path 2 (tiled
-// kernel) when it is not that shape.  e = (document, updates, ranges, first update, first
-// byte, bytes) from k_gs_find.
-static int run_giant(ymerge_ctx *c, const ym::BatchIn &b, const ym::FastOut &fo, const uint64_t *e) {
-  const uint32_t d = (uint32_t)e[0], U = (uint32_t)e[1];
+// One long single-client document over the whole GPU (ygiant.hip), queued without a host
+// round trip: buffers are sized from host-known bounds (updates, bytes), the kernels read the
+// counts they produce on the device, and k_gs_final leaves the document on path 2 (tiled kernel)
+// when it is not that shape or outgrows a bound.  The deleted-clock bitmap holds 8 bits per input
+// byte, the squashed ranges one per 2 input bytes.
+static int run_giant(ymerge_ctx *c, const ym::BatchIn &b, const ym::FastOut &fo, uint32_t d, uint32_t U, uint64_t u0,
+                     uint64_t doc_bytes) {
   ym::GsArgs a{};
   a.bytes = b.bytes;
   a.upd_off = b.upd_off;
   a.rec = b.rec;
   a.ovf = b.ovf;
-  a.u0 = e[3];
+  a.u0 = u0;
   a.U = U;
   a.d = d;
-  a.out = fo.out + 2 * e[4] + 64ull * d;
-  a.cap = 2 * e[5] + 64;
+  a.out = fo.out;
   const size_t nu = (size_t)U + 1;
-  if (!c->gs1.ensure((4 * nu + 4) * 8) || !c->scan_tmp.ensure(ym::scan_tmp_elems((uint32_t)nu) * 8 + 64))
+  const uint64_t nwc = std::min<uint64_t>(std::max<uint64_t>(doc_bytes / 4 + 2, 1024), 1ull << 26);
+  a.nwords = (uint32_t)nwc;
+  a.nbits = (uint32_t)((nwc - 2) * 32);
+  a.kcap = (uint32_t)std::min<uint64_t>(nwc * 16, doc_bytes / 2 + 2);
+  const size_t nw = a.nwords, kc = (size_t)a.kcap + 2;
+  if (!c->gs1.ensure((4 * nu + 4) * 8) ||
+      !c->scan_tmp.ensure(ym::scan_tmp_elems((uint32_t)std::max<size_t>(std::max<size_t>(nu, nw), kc)) * 8 + 64) ||
+      !c->gs2.ensure(nw * 4 + (2 * nw + 1) * 8 + 2 * kc * 4 + 2 * kc * 8 + 64))
     return YMERGE_ERR_DEVICE;
   uint64_t *w = c->gs1.as<uint64_t>();
   a.cnt = w;
@@ -303,38 +313,22 @@ static int run_giant(ymerge_ctx *c, const ym::BatchIn &b, const ym::FastOut &fo,
   a.s_cnt = w + 2 * nu;
   a.s_bl = w + 3 * nu;
   a.g = (uint32_t *)(w + 4 * nu);
-  hipMemsetAsync(a.g, 0, 32, c->s);
-  hipMemsetAsync(a.g + 1, 0xFF, 4, c->s);  // client min
-  hipMemsetAsync(a.g + 4, 0xFF, 8, c->s);  // first block key
-  ym::launch_gs_pre(a, c->s);
-  ym::launch_scan_u64(a.cnt, a.s_cnt, U, c->scan_tmp.as<uint64_t>(), c->s);
-  ym::launch_scan_u64(a.bl, a.s_bl, U, c->scan_tmp.as<uint64_t>(), c->s);
-  uint64_t *hp = c->h_pinned + 64; // flags, client min / max, max range end, first key, block count
-  hipMemcpyAsync(hp, a.g, 32, hipMemcpyDeviceToHost, c->s);
-  hipMemcpyAsync(hp + 4, a.s_cnt + U, 8, hipMemcpyDeviceToHost, c->s);
-  if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
-  const uint32_t *g = (const uint32_t *)hp;
-  const uint32_t nb_total = (uint32_t)(hp[4] & 0xFFFFFFFFu), NR = (uint32_t)(hp[4] >> 32);
-  if (g[0] || g[1] != g[2] || nb_total == 0) { // not the shape: back to the tiled kernel
-    hipMemsetAsync(fo.path + d, 2, 1, c->s);
-    return 0;
-  }
-  a.nbits = g[3];
-  a.nwords = a.nbits / 32 + 2; // the last word stays clear (run ends)
-  const size_t nw = a.nwords;
-  if (!c->gs2.ensure(nw * 4 + (2 * nw + 1) * 8 + 2 * ((size_t)NR + 2) * 4 + 2 * ((size_t)NR + 2) * 8 + 64) ||
-      !c->scan_tmp.ensure(ym::scan_tmp_elems((uint32_t)std::max<size_t>(nw, NR + 2)) * 8 + 64))
-    return YMERGE_ERR_DEVICE;
   uint8_t *q = c->gs2.as<uint8_t>();
   a.w_cnt = (uint64_t *)q;
   a.w_scan = a.w_cnt + nw;
   a.k_size = a.w_scan + nw + 1;
-  a.k_off = a.k_size + NR + 2;
-  a.bm = (uint32_t *)(a.k_off + NR + 2);
+  a.k_off = a.k_size + kc;
+  a.bm = (uint32_t *)(a.k_off + kc);
   a.k_start = a.bm + nw;
-  a.k_len = a.k_start + NR + 2;
+  a.k_len = a.k_start + kc;
+  hipMemsetAsync(a.g, 0, 32, c->s);
+  hipMemsetAsync(a.g + 1, 0xFF, 4, c->s);  // client min
+  hipMemsetAsync(a.g + 4, 0xFF, 8, c->s);  // first block key
   hipMemsetAsync(a.bm, 0, nw * 4, c->s);
-  ym::launch_gs_rest(a, fo, NR, c->scan_tmp.as<uint64_t>(), c->s);
+  ym::launch_gs_pre(a, c->s);
+  ym::launch_scan_u64(a.cnt, a.s_cnt, U, c->scan_tmp.as<uint64_t>(), c->s);
+  ym::launch_scan_u64(a.bl, a.s_bl, U, c->scan_tmp.as<uint64_t>(), c->s);
+  ym::launch_gs_rest(a, fo, c->scan_tmp.as<uint64_t>(), c->s);
   return hipGetLastError() == hipSuccess ? 0 : YMERGE_ERR_DEVICE;
 }
 
@@ -379,6 +373,46 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   // k_decode + k_fast_merge, which are skipped when k_lean wrote every document
   const bool lean = c->lean && c->fast_threads;
   uint32_t n_rej = n;
+  // One long document alone in the batch (C1: an editing trace as per-op updates): k_decode,
+  // then the grid-wide kernels, with one host round trip at the end instead of the hand-over
+  // reads of k_lean, k_fast_merge and the listing.  Not that shape: the batch takes the
+  // general route below (which recomputes everything).
+  if (n == 1 && c->giant_min && n_updates >= c->giant_min && n_updates < (1ull << 31) && c->fast_threads &&
+      !c->want_stamps && c->giant_lane) {
+    hipEventRecord(c->ev[7], c->s);
+    hipEventRecord(c->ev[0], c->s);
+    ym::launch_decode(d_bytes, d_upd_off, n_updates, c->rec.as<uint32_t>(), c->ovf.as<uint32_t>(), c->s);
+    hipEventRecord(c->ev[5], c->s);
+    const int rc = run_giant(c, b, fo, 0, (uint32_t)n_updates, 0, n_bytes);
+    if (rc) return rc;
+    hipEventRecord(c->ev[1], c->s);
+    hipMemcpyAsync(c->h_pinned + 20, path, 1, hipMemcpyDeviceToHost, c->s);
+    hipMemcpyAsync(c->h_pinned + 21, olen, 8, hipMemcpyDeviceToHost, c->s);
+    if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
+    if ((c->h_pinned[20] & 0xFF) == 0) {
+      float t05 = 0, t51 = 0, t71 = 0;
+      hipEventElapsedTime(&t05, c->ev[0], c->ev[5]);
+      hipEventElapsedTime(&t51, c->ev[5], c->ev[1]);
+      hipEventElapsedTime(&t71, c->ev[7], c->ev[1]);
+      c->stats = ymerge_stats{};
+      c->stats.n_docs = n_docs;
+      c->stats.bytes_in = n_bytes;
+      c->stats.bytes_out = c->h_pinned[21];
+      c->stats.docs_big = 1;
+      c->stats.docs_giant = 1;
+      c->stats.ms_decode = t05;
+      c->stats.ms_big = t51;
+      c->stats.ms_total = t71;
+      c->pack_stale = true; // pack_off is the one document's length: computed when a host copy asks
+      res->d_out = arena;
+      res->d_out_start = ostart;
+      res->d_out_len = olen;
+      res->d_status = status;
+      res->arena_bytes = c->arena.cap;
+      res->out_bytes = c->h_pinned[21];
+      return 0;
+    }
+  }
   hipEventRecord(c->ev[7], c->s);
   if (lean) {
     // BIG k_lean documents keep their size-proportional tables in HBM (untouched otherwise)
@@ -465,8 +499,9 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
       uint64_t ent[GSL];
       memcpy(ent, c->h_pinned + 128, sizeof ent);
       const uint64_t ng = std::min<uint64_t>(ent[0], ym::GS_LIST);
-      for (uint64_t k = 0; k < ng; k++) {
-        const int rc = run_giant(c, b, fo, ent + 1 + 6 * k);
+      for (uint64_t k = 0; k < ng; k++) { // e = (document, updates, ranges, first update, first byte, bytes)
+        const uint64_t *e = ent + 1 + 6 * k;
+        const int rc = run_giant(c, b, fo, (uint32_t)e[0], (uint32_t)e[1], e[3], e[5]);
         if (rc) return rc;
       }
     }

@@ -31,8 +31,17 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t *sh, ui
   return r;
 }
 
-__global__ void __launch_bounds__(256) k_scan_tiles(const uint64_t *in, uint32_t n, uint64_t *tile_sum) {
+// n_dev (optional): the element count is read on the device (<= the n the grid was sized
+// for), so a scan can follow the kernel that produces its length without a host round trip
+__device__ __forceinline__ uint32_t scan_n(uint32_t n, const uint32_t *n_dev) {
+  const uint32_t m = n_dev ? *n_dev : n;
+  return m < n ? m : n;
+}
+__global__ void __launch_bounds__(256) k_scan_tiles(const uint64_t *in, uint32_t n, uint64_t *tile_sum,
+                                                   const uint32_t *n_dev) {
   __shared__ uint64_t sh[SCAN_NT / 64 + 1];
+  n = scan_n(n, n_dev);
+  if (blockIdx.x * SCAN_TILE >= n && blockIdx.x) return; // (uniform)
   uint32_t base = blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_IT;
   uint64_t s = 0;
   for (uint32_t i = 0; i < SCAN_IT; i++)
@@ -41,8 +50,13 @@ __global__ void __launch_bounds__(256) k_scan_tiles(const uint64_t *in, uint32_t
   block_excl_scan(s, sh, tot);
   if (threadIdx.x == 0) tile_sum[blockIdx.x] = tot;
 }
-__global__ void __launch_bounds__(256) k_scan_top(uint64_t *tile_sum, uint32_t ntiles) {
+__global__ void __launch_bounds__(256) k_scan_top(uint64_t *tile_sum, uint32_t ntiles, uint32_t n,
+                                                 const uint32_t *n_dev) {
   __shared__ uint64_t sh[SCAN_NT / 64 + 1];
+  if (n_dev) {
+    const uint32_t m = scan_n(n, n_dev);
+    ntiles = m ? (m + SCAN_TILE - 1) / SCAN_TILE : 1;
+  }
   uint64_t carry = 0;
   for (uint32_t b0 = 0; b0 < ntiles; b0 += SCAN_NT) {
     uint32_t i = b0 + threadIdx.x;
@@ -54,8 +68,11 @@ __global__ void __launch_bounds__(256) k_scan_top(uint64_t *tile_sum, uint32_t n
   if (threadIdx.x == 0) tile_sum[ntiles] = carry;
 }
 __global__ void __launch_bounds__(256) k_scan_final(const uint64_t *in, uint32_t n, const uint64_t *tile_off,
-                                                   uint64_t *out) {
+                                                   uint64_t *out, const uint32_t *n_dev) {
   __shared__ uint64_t sh[SCAN_NT / 64 + 1];
+  n = scan_n(n, n_dev);
+  const uint32_t ntiles = n ? (n + SCAN_TILE - 1) / SCAN_TILE : 1;
+  if (blockIdx.x >= ntiles) return; // (uniform)
   uint32_t base = blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_IT;
   uint64_t v[SCAN_IT], s = 0;
   for (uint32_t i = 0; i < SCAN_IT; i++) {
@@ -68,19 +85,20 @@ __global__ void __launch_bounds__(256) k_scan_final(const uint64_t *in, uint32_t
     if (base + i < n) out[base + i] = e;
     e += v[i];
   }
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = tile_off[gridDim.x];
+  if (blockIdx.x == ntiles - 1 && threadIdx.x == 0) out[n] = tile_off[ntiles];
 }
 
 size_t scan_tmp_elems(uint32_t n) { return n / SCAN_TILE + 2; }
-void launch_scan_u64(const uint64_t *in, uint64_t *out, uint32_t n, uint64_t *tmp, hipStream_t s) {
+void launch_scan_u64(const uint64_t *in, uint64_t *out, uint32_t n, uint64_t *tmp, hipStream_t s,
+                     const uint32_t *n_dev) {
   uint32_t ntiles = (n + SCAN_TILE - 1) / SCAN_TILE;
   if (ntiles == 0) {
     hipMemsetAsync(out, 0, sizeof(uint64_t), s);
     return;
   }
-  hipLaunchKernelGGL(k_scan_tiles, dim3(ntiles), dim3(SCAN_NT), 0, s, in, n, tmp);
-  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_NT), 0, s, tmp, ntiles);
-  hipLaunchKernelGGL(k_scan_final, dim3(ntiles), dim3(SCAN_NT), 0, s, in, n, tmp, out);
+  hipLaunchKernelGGL(k_scan_tiles, dim3(ntiles), dim3(SCAN_NT), 0, s, in, n, tmp, n_dev);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_NT), 0, s, tmp, ntiles, n, n_dev);
+  hipLaunchKernelGGL(k_scan_final, dim3(ntiles), dim3(SCAN_NT), 0, s, in, n, tmp, out, n_dev);
 }
 } // namespace ym
 
