@@ -11,10 +11,11 @@
 //   (scans)     block and range counts, block bytes, clock lengths (k_scan)
 //   k_gs_write  lane per update: the clock-contiguity check, block bytes copied to their
 //               scanned offsets, deleted ranges set in a bitmap over the clock space
-//   k_gs_runs   lane per bitmap word: run starts (a run = one squashed DeleteSet range:
+//   k_gs_runs   lane per bitmap word: run starts and ends (a run = one squashed DeleteSet range:
 //               union of overlapping and adjacent ranges, as IdRange::squash merges them)
 //   (scan)      run offsets
-//   k_gs_comp   lane per word: each run's start and length, its varint bytes
+//   k_gs_comp   lane per word: the starts and ends of the runs in it, at their scanned ranks
+//   k_gs_size   lane per run: length, varint bytes
 //   (scan)      range byte offsets
 //   k_gs_ds     lane per run: the (start, length) varints
 //   k_gs_final  section header, DeleteSet header, length / status / path of the document.
@@ -75,6 +76,7 @@ __device__ __forceinline__ uint32_t gs_visit(const GsArgs &a, uint32_t i, FB blk
 
 __global__ void __launch_bounds__(256) k_gs_pre(GsArgs a) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  for (uint32_t j = i; j < a.nwords; j += gridDim.x * 256) a.bm[j] = 0; // (k_gs_write sets it)
   uint32_t nb = 0, nr = 0, bad = 0, cmin = 0xFFFFFFFFu, cmax = 0, maxend = 0;
   uint64_t bytes = 0, lens = 0, first = ~0ull;
   if (i < a.U) bad |= gs_visit(
@@ -99,7 +101,8 @@ __global__ void __launch_bounds__(256) k_gs_pre(GsArgs a) {
     a.cnt[i] = nb | ((uint64_t)nr << 32);
     a.bl[i] = (bytes << 32) | lens;
   } // block bytes (< 2^31 per document) | clock lengths (< 2^32)
-  // one atomic per wave for each global (a lane per update would serialise 10^5 atomics)
+  // workgroup partials (wave shuffles, then LDS), reduced by k_gs_reduce: atomics from every
+  // wave on the same five words serialised at one L2 channel (165 us for the C1 trace)
   for (int o = 32; o > 0; o >>= 1) {
     bad |= __shfl_xor(bad, o, 64);
     const uint32_t c0 = __shfl_xor(cmin, o, 64), c1 = __shfl_xor(cmax, o, 64), m = __shfl_xor(maxend, o, 64);
@@ -109,12 +112,84 @@ __global__ void __launch_bounds__(256) k_gs_pre(GsArgs a) {
     const uint64_t f = __shfl_xor(first, o, 64);
     first = f < first ? f : first;
   }
+  __shared__ uint32_t part[4][6];
+  const uint32_t wv = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
-    if (bad) atomicOr(&a.g[GS_BAD], bad);
-    if (cmin != 0xFFFFFFFFu) atomicMin(&a.g[GS_CMIN], cmin);
-    if (cmax) atomicMax(&a.g[GS_CMAX], cmax);
-    if (maxend) atomicMax(&a.g[GS_MAXEND], maxend);
-    if (first != ~0ull) atomicMin((unsigned long long *)(a.g + GS_FIRST), (unsigned long long)first);
+    part[wv][0] = bad;
+    part[wv][1] = cmin;
+    part[wv][2] = cmax;
+    part[wv][3] = maxend;
+    part[wv][4] = (uint32_t)first;
+    part[wv][5] = (uint32_t)(first >> 32);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (uint32_t q = 1; q < 4; q++) {
+      bad |= part[q][0];
+      cmin = part[q][1] < cmin ? part[q][1] : cmin;
+      cmax = part[q][2] > cmax ? part[q][2] : cmax;
+      maxend = part[q][3] > maxend ? part[q][3] : maxend;
+      const uint64_t f = ((uint64_t)part[q][5] << 32) | part[q][4];
+      first = f < first ? f : first;
+    }
+    uint32_t *gp = a.gp + 6 * blockIdx.x;
+    gp[0] = bad;
+    gp[1] = cmin;
+    gp[2] = cmax;
+    gp[3] = maxend;
+    gp[4] = (uint32_t)first;
+    gp[5] = (uint32_t)(first >> 32);
+  }
+}
+
+// one workgroup: the k_gs_pre partials -> the document's flags / client range / max range end /
+// first block key
+__global__ void __launch_bounds__(1024) k_gs_reduce(GsArgs a, uint32_t nparts) {
+  uint32_t bad = 0, cmin = 0xFFFFFFFFu, cmax = 0, maxend = 0;
+  uint64_t first = ~0ull;
+  for (uint32_t q = threadIdx.x; q < nparts; q += 1024) {
+    const uint32_t *gp = a.gp + 6 * q;
+    bad |= gp[0];
+    cmin = gp[1] < cmin ? gp[1] : cmin;
+    cmax = gp[2] > cmax ? gp[2] : cmax;
+    maxend = gp[3] > maxend ? gp[3] : maxend;
+    const uint64_t f = ((uint64_t)gp[5] << 32) | gp[4];
+    first = f < first ? f : first;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    bad |= __shfl_xor(bad, o, 64);
+    const uint32_t c0 = __shfl_xor(cmin, o, 64), c1 = __shfl_xor(cmax, o, 64), m = __shfl_xor(maxend, o, 64);
+    cmin = c0 < cmin ? c0 : cmin;
+    cmax = c1 > cmax ? c1 : cmax;
+    maxend = m > maxend ? m : maxend;
+    const uint64_t f = __shfl_xor(first, o, 64);
+    first = f < first ? f : first;
+  }
+  __shared__ uint32_t part[16][6];
+  const uint32_t wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    part[wv][0] = bad;
+    part[wv][1] = cmin;
+    part[wv][2] = cmax;
+    part[wv][3] = maxend;
+    part[wv][4] = (uint32_t)first;
+    part[wv][5] = (uint32_t)(first >> 32);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (uint32_t q = 1; q < 16; q++) {
+      bad |= part[q][0];
+      cmin = part[q][1] < cmin ? part[q][1] : cmin;
+      cmax = part[q][2] > cmax ? part[q][2] : cmax;
+      maxend = part[q][3] > maxend ? part[q][3] : maxend;
+      const uint64_t f = ((uint64_t)part[q][5] << 32) | part[q][4];
+      first = f < first ? f : first;
+    }
+    a.g[GS_BAD] = bad;
+    a.g[GS_CMIN] = cmin;
+    a.g[GS_CMAX] = cmax;
+    a.g[GS_MAXEND] = maxend;
+    *(uint64_t *)(a.g + GS_FIRST) = first;
   }
 }
 
@@ -174,44 +249,57 @@ __device__ __forceinline__ uint32_t gs_starts(const GsArgs &a, uint32_t j) {
   const uint32_t w = a.bm[j], prev = j ? a.bm[j - 1] >> 31 : 0u;
   return w & ~((w << 1) | prev);
 }
+// last bits of runs (the bitmap's last word in use is clear, so every run ends)
+__device__ __forceinline__ uint32_t gs_ends(const GsArgs &a, uint32_t j) {
+  const uint32_t w = a.bm[j], next = a.bm[j + 1] & 1u;
+  return w & ~((w >> 1) | (next << 31));
+}
 
 // kernels over the bitmap / the runs: grid-stride up to the counts on the device (the grid is
 // sized for the buffers' capacity, so no host round trip sits between the stages)
 __global__ void __launch_bounds__(256) k_gs_runs(GsArgs a) {
   const uint32_t nw = a.g[GS_NW];
   for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < nw; j += gridDim.x * 256)
-    a.w_cnt[j] = a.g[GS_BAD] ? 0 : __popc(gs_starts(a, j));
+    a.w_cnt[j] = a.g[GS_BAD] || j + 1 >= nw ? 0 : __popc(gs_starts(a, j)) | ((uint64_t)__popc(gs_ends(a, j)) << 32);
 }
 
+// run k: its first bit from the k-th start, its end from the k-th end (scanned per word), so no
+// lane walks a long run word by word
 __global__ void __launch_bounds__(256) k_gs_comp(GsArgs a) {
   const uint32_t nw = a.g[GS_NW];
   if (a.g[GS_BAD]) return;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     // (32-bit halves: this hipcc miscompiled the 64-bit uniform compare feeding a select,
     // testing SCC after a VALU compare that set VCC)
-    const uint64_t K = a.w_scan[nw];
-    const uint32_t kl = (uint32_t)K, kh = (uint32_t)(K >> 32);
-    const uint32_t over = (kh != 0) | (kl > a.kcap);
+    const uint32_t kl = (uint32_t)a.w_scan[nw];
+    const uint32_t over = kl > a.kcap;
     a.g[GS_K] = kl & (over - 1u);
     if (over) atomicOr(&a.g[GS_BAD], GSB_RANGE);
   }
-  for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < nw; j += gridDim.x * 256) {
-  uint32_t st = gs_starts(a, j);
-  uint64_t k = a.w_scan[j];
-  if (k + __popc(st) > a.kcap) continue; // (the count check above makes the document bad)
-  while (st) {
-    const uint32_t b = __builtin_ctz(st);
-    st &= st - 1;
-    const uint32_t s = 32 * j + b;
-    // end: the first clear bit after s (the bitmap's last word is always clear)
-    uint32_t q = j, inv = ~a.bm[j] & (b == 31 ? 0u : 0xFFFFFFFFu << (b + 1));
-    while (!inv) inv = ~a.bm[++q];
-    const uint32_t e = 32 * q + __builtin_ctz(inv);
-    a.k_start[k] = s;
-    a.k_len[k] = e - s;
-    a.k_size[k] = varlen(s) + varlen(e - s);
-    k++;
+  for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j + 1 < nw; j += gridDim.x * 256) {
+    const uint64_t sc = a.w_scan[j];
+    uint32_t ks = (uint32_t)sc, ke = (uint32_t)(sc >> 32);
+    uint32_t st = gs_starts(a, j), en = gs_ends(a, j);
+    if (ks + __popc(st) > a.kcap || ke + __popc(en) > a.kcap) continue; // (then the document is bad)
+    while (st) {
+      a.k_start[ks++] = 32 * j + __builtin_ctz(st);
+      st &= st - 1;
+    }
+    while (en) {
+      a.k_len[ke++] = 32 * j + __builtin_ctz(en) + 1; // end (exclusive) for now: k_gs_size subtracts
+      en &= en - 1;
+    }
   }
+}
+
+// per run: length and varint bytes
+__global__ void __launch_bounds__(256) k_gs_size(GsArgs a) {
+  if (a.g[GS_BAD]) return;
+  const uint32_t K = a.g[GS_K];
+  for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < K; k += gridDim.x * 256) {
+    const uint32_t s = a.k_start[k], n = a.k_len[k] - s;
+    a.k_len[k] = n;
+    a.k_size[k] = varlen(s) + varlen(n);
   }
 }
 
@@ -284,7 +372,9 @@ void launch_gs_find(const BatchIn &b, uint8_t *path, uint32_t min_u, uint64_t *l
   hipLaunchKernelGGL(k_gs_find, dim3((b.n_docs + 255) / 256), dim3(256), 0, s, b, path, min_u, list);
 }
 void launch_gs_pre(const GsArgs &a, hipStream_t s) {
-  hipLaunchKernelGGL(k_gs_pre, dim3((a.U + 255) / 256), dim3(256), 0, s, a);
+  const uint32_t nb = (a.U + 255) / 256;
+  hipLaunchKernelGGL(k_gs_pre, dim3(nb), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_gs_reduce, dim3(1), dim3(1024), 0, s, a, nb);
 }
 void launch_gs_rest(const GsArgs &a, const FastOut &o, uint64_t *scan_tmp, hipStream_t s) {
   const uint32_t gw = std::min<uint32_t>((a.nwords + 255) / 256, 1024u), gk = std::min<uint32_t>((a.kcap + 255) / 256, 1024u);
@@ -292,6 +382,7 @@ void launch_gs_rest(const GsArgs &a, const FastOut &o, uint64_t *scan_tmp, hipSt
   hipLaunchKernelGGL(k_gs_runs, dim3(gw), dim3(256), 0, s, a);
   launch_scan_u64(a.w_cnt, a.w_scan, a.nwords, scan_tmp, s, a.g + GS_NW);
   hipLaunchKernelGGL(k_gs_comp, dim3(gw), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_gs_size, dim3(gk), dim3(256), 0, s, a);
   launch_scan_u64(a.k_size, a.k_off, a.kcap, scan_tmp, s, a.g + GS_K);
   hipLaunchKernelGGL(k_gs_ds, dim3(gk), dim3(256), 0, s, a);
   hipLaunchKernelGGL(k_gs_final, dim3(1), dim3(64), 0, s, a, o);

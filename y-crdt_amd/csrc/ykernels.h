@@ -80,6 +80,7 @@ struct GsArgs {
   uint64_t *cnt, *bl;    // [U]: blocks | ranges << 32, block bytes << 32 | clock lengths
   uint64_t *s_cnt, *s_bl; // [U + 1] exclusive scans
   uint32_t *g;                         // flags / client min, max / max range end / first block key
+  uint32_t *gp;                        // k_gs_pre's per-workgroup partials of g (6 words each)
   uint32_t *bm;                        // deleted-clock bitmap [nwords]
   uint32_t nbits, nwords;              // bitmap capacity (bits, words); the words in use are on the device
   uint32_t kcap;                       // squashed-range capacity

@@ -284,8 +284,9 @@ static bool ensure_keep(ymerge_ctx *c, DevBuf &b, size_t bytes, size_t keep) {
 // One long single-client document over the whole GPU (ygiant.hip), queued without a host
 // round trip: buffers are sized from host-known bounds (updates, bytes), the kernels read the
 // counts they produce on the device, and k_gs_final leaves the document on path 2 (tiled kernel)
-// when it is not that shape or outgrows a bound.  The deleted-clock bitmap holds 8 bits per input
-// byte, the squashed ranges one per 2 input bytes.
+// when it is not that shape or outgrows a bound.  The deleted-clock bitmap holds one bit per input
+// byte (at least 2^20: a clock unit of text is a byte of it), the squashed ranges one per 2 input
+// bytes.
 static int run_giant(ymerge_ctx *c, const ym::BatchIn &b, const ym::FastOut &fo, uint32_t d, uint32_t U, uint64_t u0,
                      uint64_t doc_bytes) {
   ym::GsArgs a{};
@@ -298,12 +299,13 @@ static int run_giant(ymerge_ctx *c, const ym::BatchIn &b, const ym::FastOut &fo,
   a.d = d;
   a.out = fo.out;
   const size_t nu = (size_t)U + 1;
-  const uint64_t nwc = std::min<uint64_t>(std::max<uint64_t>(doc_bytes / 4 + 2, 1024), 1ull << 26);
+  const uint64_t nwc = std::min<uint64_t>(std::max<uint64_t>(doc_bytes / 32 + 2, 32768), 1ull << 26);
   a.nwords = (uint32_t)nwc;
   a.nbits = (uint32_t)((nwc - 2) * 32);
   a.kcap = (uint32_t)std::min<uint64_t>(nwc * 16, doc_bytes / 2 + 2);
   const size_t nw = a.nwords, kc = (size_t)a.kcap + 2;
-  if (!c->gs1.ensure((4 * nu + 4) * 8) ||
+  const size_t nparts = ((size_t)U + 255) / 256;
+  if (!c->gs1.ensure((4 * nu + 4) * 8 + nparts * 24 + 64) ||
       !c->scan_tmp.ensure(ym::scan_tmp_elems((uint32_t)std::max<size_t>(std::max<size_t>(nu, nw), kc)) * 8 + 64) ||
       !c->gs2.ensure(nw * 4 + (2 * nw + 1) * 8 + 2 * kc * 4 + 2 * kc * 8 + 64))
     return YMERGE_ERR_DEVICE;
@@ -313,6 +315,7 @@ static int run_giant(ymerge_ctx *c, const ym::BatchIn &b, const ym::FastOut &fo,
   a.s_cnt = w + 2 * nu;
   a.s_bl = w + 3 * nu;
   a.g = (uint32_t *)(w + 4 * nu);
+  a.gp = a.g + 8;
   uint8_t *q = c->gs2.as<uint8_t>();
   a.w_cnt = (uint64_t *)q;
   a.w_scan = a.w_cnt + nw;
@@ -321,10 +324,7 @@ static int run_giant(ymerge_ctx *c, const ym::BatchIn &b, const ym::FastOut &fo,
   a.bm = (uint32_t *)(a.k_off + kc);
   a.k_start = a.bm + nw;
   a.k_len = a.k_start + kc;
-  hipMemsetAsync(a.g, 0, 32, c->s);
-  hipMemsetAsync(a.g + 1, 0xFF, 4, c->s);  // client min
-  hipMemsetAsync(a.g + 4, 0xFF, 8, c->s);  // first block key
-  hipMemsetAsync(a.bm, 0, nw * 4, c->s);
+  // (no memsets: k_gs_pre zeroes the bitmap, k_gs_reduce / k_gs_write / k_gs_comp write g)
   ym::launch_gs_pre(a, c->s);
   ym::launch_scan_u64(a.cnt, a.s_cnt, U, c->scan_tmp.as<uint64_t>(), c->s);
   ym::launch_scan_u64(a.bl, a.s_bl, U, c->scan_tmp.as<uint64_t>(), c->s);
