@@ -85,6 +85,7 @@ struct ymerge_ctx {
   int fast_threads = 256;
   bool lean = true; // k_lean first (env YMERGE_LEAN=0: every document through k_decode + k_fast_merge)
   bool pack_stale = false; // pack_off not computed for the last merge (all documents on k_lean)
+  bool times_pending = false; // the last merge's stage times wait on its events (resolve_times)
   uint32_t giant_min = ym::GS_MIN_U; // updates of a document for the grid-wide path (env YMERGE_GIANT_MIN, 0: off)
   bool giant_lane = true; // a batch of one such document skips the per-document routing (env YMERGE_GIANT_LANE=0: off)
   int lean_order = -1; // k_lean longest-first dispatch: env YMERGE_LEAN_ORDER 0/1, default for >= 8192 small docs
@@ -281,6 +282,21 @@ static bool ensure_keep(ymerge_ctx *c, DevBuf &b, size_t bytes, size_t keep) {
   return true;
 }
 
+// Stage times of a merge whose documents were all written by k_lean: its one host round trip
+// (hand-over count and output bytes) is taken right after k_lean, so the events recorded after
+// it are read here -- by the stats getter, or before the next call records the events again --
+// instead of in a second synchronisation per batch.
+static void resolve_times(ymerge_ctx *c) {
+  if (!c->times_pending) return;
+  c->times_pending = false;
+  if (hipEventSynchronize(c->ev[3]) != hipSuccess) return;
+  float t70 = 0, t03 = 0;
+  hipEventElapsedTime(&t70, c->ev[7], c->ev[0]);
+  hipEventElapsedTime(&t03, c->ev[7], c->ev[3]);
+  c->stats.ms_lean = t70;
+  c->stats.ms_total = t03;
+}
+
 // One long single-client document over the whole GPU (ygiant.hip), queued without a host
 // round trip: buffers are sized from host-known bounds (updates, bytes), the kernels read the
 // counts they produce on the device, and k_gs_final leaves the document on path 2 (tiled kernel)
@@ -335,6 +351,7 @@ static int run_giant(ymerge_ctx *c, const ym::BatchIn &b, const ym::FastOut &fo,
 // One batch: fast path for every document, exact engine for the documents it hands over.
 static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes, const uint64_t *d_upd_off,
                         uint64_t n_updates, const uint64_t *d_doc_upd, uint64_t n_docs, ymerge_device_result *res) {
+  resolve_times(c);
   if (hipSetDevice(c->device) != hipSuccess) return YMERGE_ERR_DEVICE;
   if (n_docs > 0xFFFFFFFFull) return YMERGE_ERR_OTHER;
   const uint32_t n = (uint32_t)n_docs;
@@ -345,7 +362,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   if (!c->status.ensure(nn) || !c->path.ensure(nn) || !c->out_start.ensure(nn * 8) || !c->out_len.ensure(nn * 8) ||
       !c->pack_off.ensure(nn * 8) || !c->counts.ensure(4 * nn * 4) || !c->need.ensure(nn * 8) ||
       !c->scr_off.ensure(nn * 8) || !c->sizes.ensure(nn * 8) || !c->spill_off.ensure(nn * 8) ||
-      !c->scan_tmp.ensure(ym::scan_tmp_elems(n) * 8 + 64) || !c->counter.ensure(128) ||
+      !c->scan_tmp.ensure(ym::scan_tmp_elems(n) * 8 + 64) || !c->counter.ensure(128 + 64 * 64) ||
       !ensure_keep(c, c->arena, slots + slots / 8 + 4096, 0) ||
       (c->fast_threads && (!c->rec.ensure((n_updates + 1) * ym::REC_WORDS * 4) ||
                            !c->ovf.ensure(((n_updates + ym::DEC_NT - 1) / ym::DEC_NT + 1) * ym::DEC_OVF * 4))))
@@ -355,7 +372,8 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   uint8_t *arena = c->arena.as<uint8_t>();
   uint64_t *ostart = c->out_start.as<uint64_t>(), *olen = c->out_len.as<uint64_t>();
   uint8_t *status = c->status.as<uint8_t>(), *path = c->path.as<uint8_t>();
-  hipMemsetAsync(c->counter.p, 0, 128, c->s);
+  // counters [128 B] then k_lean's 64 output-byte partial sums [4 KB]: one memset, one copy back
+  hipMemsetAsync(c->counter.p, 0, 128 + 64 * 64, c->s);
   uint64_t *stamps = nullptr;
   if (c->want_stamps) {
     if (!c->stamps.ensure(nn * 16 * 8)) return YMERGE_ERR_DEVICE;
@@ -422,9 +440,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     uint32_t *lscr = nullptr;
     if (lw * 4 + 64 <= c->lean_scr_max && c->lean_scr.ensure(lw * 4 + 64)) lscr = c->lean_scr.as<uint32_t>();
     (void)hipGetLastError();
-    if (!c->lean_tot.ensure(64 * 64)) return YMERGE_ERR_DEVICE;
-    hipMemsetAsync(c->lean_tot.p, 0, 64 * 64, c->s);
-    fo.lean_total = c->lean_tot.as<unsigned long long>();
+    fo.lean_total = (unsigned long long *)(c->counter.as<uint8_t>() + 128);
     // large batches: long documents dispatched first (a skewed batch otherwise ends on the
     // last long document to start)
     ym::BatchIn bl = b;
@@ -438,11 +454,12 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     }
     ym::launch_lean(bl, fo, lscr, c->s);
     if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
-    // hand-over count and k_lean's output bytes (npath[6], the 64 partial sums) in one sync
-    hipMemcpyAsync(c->h_pinned + 16, c->counter.as<uint32_t>() + 10, 4, hipMemcpyDeviceToHost, c->s);
-    hipMemcpyAsync(c->h_pinned + 512, c->lean_tot.p, 64 * 64, hipMemcpyDeviceToHost, c->s);
+    // hand-over count and k_lean's output bytes (npath[6] at counter byte 40, the 64 partial
+    // sums from byte 128) in one copy and one sync: byte 128 lands on h_pinned[512]
+    hipMemcpyAsync((uint8_t *)(c->h_pinned + 512) - 88, c->counter.as<uint8_t>() + 40, 88 + 64 * 64,
+                   hipMemcpyDeviceToHost, c->s);
     if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
-    n_rej = (uint32_t)(c->h_pinned[16] & 0xFFFFFFFFu);
+    n_rej = (uint32_t)(c->h_pinned[501] & 0xFFFFFFFFu);
     b.only_path3 = 1;
     if (n_rej && getenv("YMERGE_LEAN_DEBUG")) {
       uint32_t why[7];
@@ -561,7 +578,20 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   if (c->pack_stale) {
     for (int q = 0; q < 64; q++) total += c->h_pinned[512 + 8 * q];
     hipEventRecord(c->ev[3], c->s);
-    if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
+    if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
+    c->stats = ymerge_stats{};
+    c->stats.n_docs = n_docs;
+    c->stats.bytes_in = n_bytes;
+    c->stats.docs_lean = n_docs;
+    c->stats.bytes_out = total;
+    c->times_pending = true; // ms_lean / ms_total: resolve_times
+    res->d_out = arena;
+    res->d_out_start = ostart;
+    res->d_out_len = olen;
+    res->d_status = status;
+    res->arena_bytes = c->arena.cap;
+    res->out_bytes = total;
+    return 0;
   } else {
     ym::launch_scan_u64(olen, c->pack_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
     hipEventRecord(c->ev[3], c->s);
@@ -620,6 +650,7 @@ extern "C" int ymerge_updates_v1_batch_device(ymerge_ctx *c, const uint8_t *d_by
 static int plan_exec(ymerge_ctx *c, bool diff, const uint8_t *d_bytes, const uint64_t *d_upd_off,
                      const uint8_t *d_sv, const uint64_t *d_sv_off, uint64_t n_docs, ymerge_device_result *res,
                      uint32_t frame = 0, const uint64_t *sv_end = nullptr, const uint8_t *pre_status = nullptr) {
+  resolve_times(c);
   if (hipSetDevice(c->device) != hipSuccess) return YMERGE_ERR_DEVICE;
   if (n_docs > 0xFFFFFFFFull) return YMERGE_ERR_OTHER;
   const uint32_t n = (uint32_t)n_docs;
@@ -744,6 +775,7 @@ extern "C" int ydiff_updates_v1_batch_device(ymerge_ctx *c, const uint8_t *d_byt
 // offsets by a scan of the lengths.
 static int compact_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes, const uint64_t *d_upd_off,
                           uint64_t n_updates, const uint64_t *d_doc_upd, uint64_t n_docs, ymerge_device_result *res) {
+  resolve_times(c);
   if (hipSetDevice(c->device) != hipSuccess) return YMERGE_ERR_DEVICE;
   if (n_docs > 0xFFFFFFFFull) return YMERGE_ERR_OTHER;
   const uint32_t n = (uint32_t)n_docs;
@@ -977,6 +1009,7 @@ extern "C" int ymerge_debug_stamps(ymerge_ctx *c, uint64_t n_docs, uint64_t *dst
 extern "C" void ymerge_last_stats(ymerge_ctx *c, ymerge_stats *st) {
   if (!c || !st) return;
   std::lock_guard<std::mutex> g(c->mu);
+  resolve_times(c);
   *st = c->stats;
 }
 
