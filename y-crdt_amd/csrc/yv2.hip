@@ -523,14 +523,14 @@ __global__ void k_v2_sv_parse(const uint8_t *sv, const uint64_t *sv_off, const u
 template <class W> struct IEnc {
   uint32_t last = 0, count = 0;
   int32_t diff = 0;
-  __device__ void flush(W &w) {
+  __device__ __forceinline__ void flush(W &w) {
     if (count > 0) {
       const int32_t ed = (int32_t)((uint32_t)diff << 1) | (count == 1 ? 0 : 1);
       w_var_i64(w, ed);
       if (count > 1) w_var(w, count - 2);
     }
   }
-  __device__ void put(W &w, uint32_t v) {
+  __device__ __forceinline__ void put(W &w, uint32_t v) {
     const int32_t df = (int32_t)(v - last);
     if (diff == df) {
       last = v;
@@ -554,7 +554,7 @@ template <class W> __device__ __forceinline__ void w_signed(W &w, uint64_t mag, 
 template <class W> struct UEnc {
   uint64_t last = 0;
   uint32_t count = 0;
-  __device__ void flush(W &w) {
+  __device__ __forceinline__ void flush(W &w) {
     if (count == 1) {
       w_var_i64(w, (int64_t)last);
     } else if (count > 1) {
@@ -562,7 +562,7 @@ template <class W> struct UEnc {
       w_var(w, count - 2);
     }
   }
-  __device__ void put(W &w, uint64_t v) {
+  __device__ __forceinline__ void put(W &w, uint64_t v) {
     if (last == v) {
       count++;
     } else {
@@ -576,7 +576,7 @@ template <class W> struct REnc {
   bool has = false;
   uint8_t last = 0;
   uint32_t count = 0;
-  __device__ void put(W &w, uint8_t v) {
+  __device__ __forceinline__ void put(W &w, uint8_t v) {
     if (has && last == v) {
       count++;
     } else {
@@ -601,11 +601,11 @@ template <class W> struct V2Enc {
   UEnc<W> cli, tref, len, slen;
   REnc<W> info, pinfo;
   uint32_t seq = 0, ds_cur = 0;
-  __device__ void string(const uint8_t *p, uint32_t n) {
+  __device__ __forceinline__ void string(const uint8_t *p, uint32_t n) {
     s[S_SBUF].bytes(p, n);
     slen.put(s[S_SLEN], utf16_count(p, n));
   }
-  __device__ void finish() {
+  __device__ __forceinline__ void finish() {
     keyc.flush(s[S_KEY]);
     cli.flush(s[S_CLI]);
     lclk.flush(s[S_LCLK]);
@@ -630,7 +630,9 @@ __device__ __forceinline__ uint64_t rv64(Cur &c) {
 // copies one (validated) Any value / raw byte range of the v1x document into the rest stream
 template <class W> __device__ __forceinline__ void copy_any(Cur &c, W &rest) {
   const uint32_t st = c.i;
-  any_skip(c);
+  Cur cc = c; // (the out-of-line skip takes its cursor by reference: a copy keeps c in registers)
+  any_skip(cc);
+  c.i = cc.i;
   rest.bytes(c.p + st, c.i - st);
 }
 template <class W> __device__ __forceinline__ void e_str(V2Enc<W> &e, Cur &c) {
@@ -640,7 +642,7 @@ template <class W> __device__ __forceinline__ void e_str(V2Enc<W> &e, Cur &c) {
 }
 // encode_diff with an empty state vector over EncoderV2 (update.rs:490-535, slice.rs:199-251,
 // block.rs:1711-1754), reading the canonical v1x bytes the engine wrote
-template <class W> __device__ __noinline__ void v1x_to_v2(const uint8_t *p, uint32_t n, V2Enc<W> &e) {
+template <class W> __device__ __forceinline__ void v1x_to_v2(const uint8_t *p, uint32_t n, V2Enc<W> &e) {
   Cur c{p, n, 0};
   W &rest = e.s[S_REST];
   const uint32_t ncl = rv(c);
@@ -771,6 +773,7 @@ template <class W> __device__ __noinline__ void v1x_to_v2(const uint8_t *p, uint
 }
 __device__ __forceinline__ uint64_t v2_total(const V2Enc<Counter> &e) {
   uint64_t t = 1;
+#pragma unroll
   for (int k = 0; k < S_N; k++) {
     if (k == S_SBUF || k == S_SLEN || k == S_REST) continue;
     t += varlen(e.s[k].n) + e.s[k].n;
@@ -781,8 +784,10 @@ __device__ __forceinline__ uint64_t v2_total(const V2Enc<Counter> &e) {
 
 // mode 0: full v2 update; mode 1: state vector (EncoderV2 header of empty columns + the
 // v1 state vector bytes, which the rest buffer holds unchanged)
+// (64 lanes per workgroup, a document per lane: a batch of 10^4 documents is ~160 waves, so
+// the encoder state may take the whole register file instead of scratch memory)
 template <bool WRITE>
-__global__ void k_v2_encode(const uint8_t *src, const uint64_t *src_start, const uint64_t *src_len,
+__global__ void __launch_bounds__(64) k_v2_encode(const uint8_t *src, const uint64_t *src_start, const uint64_t *src_len,
                             const uint8_t *status, uint32_t n_docs, uint64_t *sz_off, uint8_t *out, int mode) {
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= n_docs) return;
@@ -813,6 +818,7 @@ __global__ void k_v2_encode(const uint8_t *src, const uint64_t *src_start, const
   h.u8(0); // feature flag
   V2Enc<Writer> ew;
   uint64_t at = 1;
+#pragma unroll
   for (int k = 0; k < S_N; k++) {
     if (k == S_SBUF) {
       const uint64_t sc = varlen(ec.s[S_SBUF].n) + ec.s[S_SBUF].n + ec.s[S_SLEN].n;
