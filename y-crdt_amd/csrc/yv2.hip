@@ -65,7 +65,7 @@ __device__ __forceinline__ int rd_var_signed(Cur &c, uint64_t &mag, bool &neg) {
   return 0;
 }
 // IntDiffOptRleDecoder::read_u32 (decoder.rs:389-404)
-__device__ int icol_read(ICol &d, uint32_t &v) {
+__device__ __forceinline__ int icol_read(ICol &d, uint32_t &v) {
   if (d.count == 0) {
     int64_t x;
     YM_TRY(rd_var_i64(d.c, x));
@@ -90,7 +90,7 @@ __device__ int icol_read(ICol &d, uint32_t &v) {
   return 0;
 }
 // UIntOptRleDecoder::read_u64 (decoder.rs:422-437)
-__device__ int ucol_read(UCol &d, uint64_t &v) {
+__device__ __forceinline__ int ucol_read(UCol &d, uint64_t &v) {
   if (d.count == 0) {
     uint64_t mag;
     bool neg;
@@ -111,7 +111,7 @@ __device__ int ucol_read(UCol &d, uint64_t &v) {
   return 0;
 }
 // RleDecoder::read_u8 (decoder.rs:455-466)
-__device__ int rcol_read(RCol &d, uint8_t &v) {
+__device__ __forceinline__ int rcol_read(RCol &d, uint8_t &v) {
   if (d.count == 0) {
     YM_TRY(rd_u8(d.c, d.last));
     if (d.c.i < d.c.n) {
@@ -129,7 +129,7 @@ __device__ int rcol_read(RCol &d, uint8_t &v) {
   return 0;
 }
 // StringDecoder::read_str (decoder.rs:489-503): `remaining` UTF-16 units over chars()
-__device__ int scol_read(SCol &d, uint32_t &pos, uint32_t &len) {
+__device__ __forceinline__ int scol_read(SCol &d, uint32_t &pos, uint32_t &len) {
   uint64_t remaining;
   YM_TRY(ucol_read(d.lens, remaining));
   uint32_t i = 0, j = d.pos;
@@ -149,7 +149,7 @@ __device__ int scol_read(SCol &d, uint32_t &pos, uint32_t &len) {
   return 0;
 }
 // DecoderV2::read_usize + read_buf (decoder.rs:246-277)
-__device__ int usize_buf(const uint8_t *p, uint32_t n, uint32_t &idx, uint32_t &bp, uint32_t &bl) {
+__device__ __forceinline__ int usize_buf(const uint8_t *p, uint32_t n, uint32_t &idx, uint32_t &bp, uint32_t &bl) {
   if (idx >= n) return E_VARINT;
   uint64_t num = 0;
   uint32_t len = 0;
@@ -181,7 +181,7 @@ struct V2Dec {
   uint32_t kpos[V2_KCAP], klen[V2_KCAP];
 };
 // DecoderV2::new (decoder.rs:209-244)
-__device__ int v2_init(V2Dec &d, const uint8_t *p, uint32_t n) {
+__device__ __forceinline__ int v2_init(V2Dec &d, const uint8_t *p, uint32_t n) {
   uint32_t idx = n > 0 ? 1 : 0; // feature flag
   uint32_t bp[9], bl[9];
   for (int k = 0; k < 9; k++) YM_TRY(usize_buf(p, n, idx, bp[k], bl[k]));
@@ -221,7 +221,7 @@ template <class W> __device__ __forceinline__ int d2_string(V2Dec &d, W &w) {
 }
 // read_key (decoder.rs:355-364): a key clock inside the table reuses the key, else the
 // next string is read and appended
-template <class W> __device__ int d2_key(V2Dec &d, W &w) {
+template <class W> __device__ __forceinline__ int d2_key(V2Dec &d, W &w) {
   uint32_t kc;
   YM_TRY(icol_read(d.keyc, kc));
   uint32_t pos, len;
@@ -242,7 +242,7 @@ template <class W> __device__ int d2_key(V2Dec &d, W &w) {
   return 0;
 }
 // one Any value of the rest cursor, validated (Any::decode) and copied
-template <class W> __device__ int d2_any(V2Dec &d, W &w) {
+template <class W> __device__ __forceinline__ int d2_any(V2Dec &d, W &w) {
   const uint32_t st = d.r.i;
   Counter cnt;
   bool re = false;
@@ -260,7 +260,7 @@ template <class W> __device__ __forceinline__ int d2_client(V2Dec &d, W &w) {
 
 // Update::decode_block + ItemContent::decode over DecoderV2, emitted as v1x; `ilen` = the
 // block's clock length (0 for a dropped Item)
-template <class W> __device__ int v2_block(V2Dec &d, W &w, uint32_t &ilen) {
+template <class W> __device__ __forceinline__ int v2_block(V2Dec &d, W &w, uint32_t &ilen) {
   uint8_t info;
   bool cn;
   uint32_t v;
@@ -387,7 +387,7 @@ template <class W> __device__ int v2_block(V2Dec &d, W &w, uint32_t &ilen) {
 }
 
 // Update::decode over DecoderV2 (update.rs:714-749, id_set.rs:412-426) -> v1x
-template <class W> __device__ __noinline__ int v2_to_v1(const uint8_t *p, uint32_t n, W &w) {
+template <class W> __device__ __forceinline__ int v2_to_v1(const uint8_t *p, uint32_t n, W &w) {
   V2Dec d;
   YM_TRY(v2_init(d, p, n));
   bool cn;
@@ -471,7 +471,7 @@ __device__ int v2_sv_rest(const uint8_t *p, uint32_t n, uint32_t &rest) {
 // pass 0: sizes + status per update; pass 1: v1x bytes at the scanned offsets (an empty
 // update [0, 0] for a failed one, which the document's status reports)
 template <bool WRITE>
-__global__ void k_v2_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_upd, uint64_t *sz_off,
+__global__ void __launch_bounds__(64) k_v2_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_upd, uint64_t *sz_off,
                             uint8_t *out, uint8_t *ust) {
   const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= n_upd) return;
