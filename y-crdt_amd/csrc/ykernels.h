@@ -31,8 +31,11 @@ constexpr uint32_t DEC_NT = 256, DEC_STAGE = 16384, DEC_OVF = 1024; // overflow 
 constexpr uint32_t REC_WORDS = 6;
 constexpr uint32_t REC_UNSUP = 1u << 8, REC_BIGDS = 1u << 9, REC_SLOW = 1u << 14, REC_OVF = 1u << 15;
 constexpr uint32_t REC_EMPTY = 0, REC_BLOCK = 1, REC_DS = 2, REC_COMPLEX = 3;
+// huge: [count, bump, -, -, u64 list of HUGE_LIST update indices]; huge_cap: overflow words
+// after the k_decode workgroups' DEC_OVF words for the updates k_decode_huge decodes
+constexpr uint32_t HUGE_MIN = 2048, HUGE_LIST = 4096;
 void launch_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_updates, uint32_t *rec, uint32_t *ovf,
-                   hipStream_t s);
+                   uint32_t *huge, uint32_t huge_cap, hipStream_t s);
 
 // LDS capacities of the one-workgroup-per-document fast path (per document)
 struct FastCaps {

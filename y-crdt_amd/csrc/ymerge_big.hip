@@ -28,7 +28,8 @@ namespace ym {
 constexpr uint32_t BIG_DCAP = 1024;   // distinct DeleteSet clients per document
 constexpr uint32_t BIG_DTAB = 2048;   // LDS hash slots for them (u64)
 constexpr uint32_t BIG_CHUNK = 2048;  // LDS bitonic chunk of the sort (key u64 + value u32)
-constexpr uint32_t BIG_LU_LDS = 8192; // overlap mode: updates / runs whose last-rank histogram stays in LDS
+constexpr uint32_t BIG_LU_LDS = 8192;
+constexpr uint32_t BIG_COOP = 64;      // records of one update from which the gather copies them cooperatively // overlap mode: updates / runs whose last-rank histogram stays in LDS
 // LDS union region (phase-local): sort chunk (24 KB) / output stage / DeleteSet tables:
 //   [0, 16K) client hash table  [16K, 44K) 7 per-client arrays  [44K, 68K) sort chunk / slots
 constexpr uint32_t BIG_OFF_DARR = 8 * BIG_DTAB, BIG_OFF_SCR = BIG_OFF_DARR + 7 * 4 * BIG_DCAP;
@@ -766,6 +767,8 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
   //      or a walk of the update for the shapes k_decode left to a later pass)
   {
     uint32_t NBr = 0, NEr = 0, NRr = 0;
+    if (t == 0) sc[5] = 0;
+    __syncthreads();
     uint64_t g_rec = 0, g_scan = 0, g_write = 0, g_slow = 0; // diagnostic sub-phase sums (thread 0, stamps only)
     uint64_t g_r0 = 0, g_w0 = 0, g_rmax = 0, g_wmax = 0;      // round 0 / slowest later round
     for (uint32_t r0 = 0; r0 < U; r0 += NT) {
@@ -826,6 +829,7 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
         if (r0 == 0) g_r0 = tg1 - tg0;
         else g_rmax = g_rmax > tg1 - tg0 ? g_rmax : tg1 - tg0;
       }
+      uint32_t co = 0; // 1: this lane's record list is copied by the workgroup
       if (i < U) {
       if (shape == REC_BLOCK) {
         m.bc[pb] = w1;
@@ -847,7 +851,21 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
           m.re[pr + 1] = w5;
           m.ri[pr + 1] = pe;
         }
+      } else if (shape == REC_COMPLEX && !walk && snb + sne + snr > BIG_COOP && (co = atomicAdd(&sc[5], 1u)) < 8) {
+        // a long record list (k_decode_huge: thousands of blocks in one update) is copied by
+        // the whole workgroup after this round's writes instead of by this lane
+        uint32_t *ce = (uint32_t *)S.un + 8 * co;
+        ce[0] = i;
+        ce[1] = pb;
+        ce[2] = pe;
+        ce[3] = pr;
+        ce[4] = w4;
+        ce[5] = snb;
+        ce[6] = sne;
+        ce[7] = snr;
+        co = 1;
       } else if (shape == REC_COMPLEX && !walk) {
+        co = 0;
         const uint32_t *ov = b.ovf + w4;
         for (uint32_t k = 0; k < snb; k++) {
           m.bc[pb + k] = ov[5 * k];
@@ -873,6 +891,37 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
         fill_hbm(in + ubase, ulen, &f);
         for (uint32_t k = 0; k < snb; k++) m.bu[pb + k] = i;
       }
+      }
+      if (__syncthreads_or(co == 1)) { // the deferred long record lists, one after another
+        const uint32_t nco = sc[5] < 8 ? sc[5] : 8;
+        for (uint32_t q = 0; q < nco; q++) {
+          const uint32_t *ce = (const uint32_t *)S.un + 8 * q;
+          const uint32_t ci = ce[0], cb = ce[1], cE = ce[2], cr = ce[3], nb2 = ce[5], ne2 = ce[6], nr2 = ce[7];
+          const uint32_t cub = (uint32_t)(b.upd_off[u0 + ci] - B0);
+          const uint32_t *ov = b.ovf + ce[4];
+          for (uint32_t k = t; k < nb2; k += NT) {
+            m.bc[cb + k] = ov[5 * k];
+            m.bk[cb + k] = ov[5 * k + 1];
+            m.bl[cb + k] = ov[5 * k + 2];
+            m.bp[cb + k] = cub + ov[5 * k + 3];
+            m.bm[cb + k] = ov[5 * k + 4];
+            m.bu[cb + k] = ci;
+          }
+          const uint32_t *oe = ov + 5 * nb2;
+          for (uint32_t k = t; k < ne2; k += NT) {
+            m.ec[cE + k] = oe[k];
+            m.et[cE + k] = oe[ne2 + k] | (ci << 8);
+          }
+          const uint32_t *orr = oe + 2 * ne2;
+          for (uint32_t k = t; k < nr2; k += NT) {
+            m.rs[cr + k] = orr[3 * k];
+            m.re[cr + k] = orr[3 * k + 1];
+            m.ri[cr + k] = cE + orr[3 * k + 2];
+          }
+        }
+        __syncthreads();
+        if (t == 0) sc[5] = 0;
+        __syncthreads();
       }
       if (o.stamps) {
         __syncthreads();

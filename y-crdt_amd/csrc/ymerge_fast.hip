@@ -104,7 +104,7 @@ __host__ __device__ inline FastLayout fast_layout(const FastCaps &c) {
 // 8 workgroups per CU (8 waves per SIMD): <= 64 VGPRs and < 20 KB of LDS (the second-walk
 // list keeps 16-bit lane / count fields)
 __global__ void __launch_bounds__(DEC_NT, 8) k_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_upd,
-                                                      uint32_t *rec, uint32_t *ovf) {
+                                                      uint32_t *rec, uint32_t *ovf, uint32_t *huge) {
   __shared__ __align__(16) uint32_t stage[DEC_STAGE / 4 + 4];
   __shared__ uint32_t ovf_top, n_cx;
   ym_set_grammar(0); // fast_walk bails on every content it does not restate; v1 by construction
@@ -143,7 +143,12 @@ __global__ void __launch_bounds__(DEC_NT, 8) k_decode(const uint8_t *bytes, cons
     s.nb = s.ne = s.nr = 0;
     s.unsupported = s.big_ds = false;
     s.ubase = 0;
-    const int e = a1 - sbase <= 4 * nd ? fast_walk(stage, (uint32_t)(a0 - sbase), ulen, s) : -1;
+    const bool staged = a1 - sbase <= 4 * nd;
+    const int e = staged ? fast_walk(stage, (uint32_t)(a0 - sbase), ulen, s) : -1;
+    if (!staged && ulen >= HUGE_MIN) { // a long update: k_decode_huge walks it (a wavefront, LDS window)
+      const uint32_t k = atomicAdd(&huge[0], 1u);
+      if (k < HUGE_LIST) ((uint64_t *)(huge + 4))[k] = i;
+    }
     uint32_t w0 = REC_SLOW, w1 = 0, w2 = 0, w3 = 0, w4 = 0, w5 = 0;
     if (e >= 0) rec_pack(s, e, w0, w1, w2, w3, w4, w5);
     if (e == 0 && ((w0 >> 10) & 3) == REC_COMPLEX && !s.big_ds) {
@@ -180,11 +185,66 @@ __global__ void __launch_bounds__(DEC_NT, 8) k_decode(const uint8_t *bytes, cons
   }
 }
 
+// The updates k_decode could not stage and listed (>= HUGE_MIN bytes): a wavefront each walks
+// one through the LDS window of ylwin.h, all 64 lanes in lockstep (the exact walk of ysm.h, so
+// records and errors are those of walk_record_hbm), and writes its record.  A multi-record
+// update's overflow words come from a bump allocator over the tail of the overflow buffer
+// (words huge_base.. huge_base + huge_cap); one that does not fit stays REC_SLOW.  The merge
+// kernels then read records instead of walking the update over HBM, once per kernel, through
+// a 64-byte register window (b4-update.bin: ~1 s -> a few ms).
+__global__ void __launch_bounds__(64) k_decode_huge(const uint8_t *bytes, const uint64_t *upd_off, uint32_t *rec,
+                                                   uint32_t *ovf, uint32_t *huge, uint32_t huge_base, uint32_t huge_cap) {
+  __shared__ __align__(16) uint32_t win[LW_BYTES / 4];
+  ym_set_grammar(0);
+  const uint32_t lane = threadIdx.x;
+  const uint32_t n = huge[0] < HUGE_LIST ? huge[0] : HUGE_LIST;
+  for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
+    const uint64_t i = ((const uint64_t *)(huge + 4))[k];
+    const uint64_t a0 = upd_off[i], a1 = upd_off[i + 1];
+    const uint32_t ulen = (uint32_t)(a1 - a0);
+    RegSink s;
+    s.nb = s.ne = s.nr = 0;
+    s.unsupported = s.big_ds = false;
+    s.ubase = 0;
+    LWin c;
+    lw_init(c, bytes + a0, ulen, win);
+    const int e = smwalk_update(c, s);
+    uint32_t w0, w1, w2, w3, w4, w5;
+    rec_pack(s, e, w0, w1, w2, w3, w4, w5);
+    bool write = true;
+    if (e == 0 && ((w0 >> 10) & 3) == REC_COMPLEX && !s.big_ds) {
+      const uint32_t need = 5 * s.nb + 2 * s.ne + 3 * s.nr;
+      uint32_t off = 0;
+      if (lane == 0) off = atomicAdd(&huge[1], need);
+      off = (uint32_t)__builtin_amdgcn_readfirstlane((int)off);
+      if ((uint64_t)off + need <= huge_cap) {
+        OvfFill f{ovf + huge_base + off, s.nb, s.ne, 0, 0, 0};
+        LWin c2;
+        lw_init(c2, bytes + a0, ulen, win);
+        smwalk_update(c2, f);
+        w0 |= REC_OVF;
+        w4 = huge_base + off;
+      } else {
+        write = false; // no room: the record stays REC_SLOW
+      }
+    }
+    if (write && lane == 0) {
+      uint2 *o = (uint2 *)(rec + i * REC_WORDS);
+      o[0] = make_uint2(w0, w1);
+      o[1] = make_uint2(w2, w3);
+      o[2] = make_uint2(w4, w5);
+    }
+  }
+}
+
 void launch_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_updates, uint32_t *rec, uint32_t *ovf,
-                   hipStream_t s) {
+                   uint32_t *huge, uint32_t huge_cap, hipStream_t s) {
   if (!n_updates) return;
-  hipLaunchKernelGGL(k_decode, dim3((unsigned)((n_updates + DEC_NT - 1) / DEC_NT)), dim3(DEC_NT), 0, s, bytes, upd_off,
-                     n_updates, rec, ovf);
+  const uint64_t nwg = (n_updates + DEC_NT - 1) / DEC_NT;
+  hipMemsetAsync(huge, 0, 16, s);
+  hipLaunchKernelGGL(k_decode, dim3((unsigned)nwg), dim3(DEC_NT), 0, s, bytes, upd_off, n_updates, rec, ovf, huge);
+  hipLaunchKernelGGL(k_decode_huge, dim3(64), dim3(64), 0, s, bytes, upd_off, rec, ovf, huge,
+                     (uint32_t)(nwg * DEC_OVF), huge_cap);
 }
 
 // ------------------------------------------------------------------ the kernel

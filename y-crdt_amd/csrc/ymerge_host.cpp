@@ -67,6 +67,7 @@ struct ymerge_ctx {
   DevBuf status, path, out_start, out_len, pack_off, counts, need, scr_off, scratch, sizes, spill_off, scan_tmp;
   DevBuf arena, packed, counter, stamps, plan_small, plan_big, rec, ovf, big_scratch, lean_scr, lean_tot, cscr;
   DevBuf gs_list, gs1, gs2; // long single-client documents (ygiant.hip)
+  DevBuf huge;              // k_decode_huge's list and bump counter
   DevBuf lean_ord;          // k_lean dispatch order: 8 counters, then n_docs document indices
   DevBuf plan_wlist;        // diff / SV: documents k_plan_lane leaves to k_plan_wave
   DevBuf lean_dbg;          // YMERGE_LEAN_DEBUG hand-over reasons (this context's device only)
@@ -155,7 +156,7 @@ extern "C" void ymerge_ctx_destroy(ymerge_ctx *c) {
                     &c->sync_end, &c->sync_st, &c->rec, &c->ovf, &c->status, &c->path,
                     &c->out_start, &c->out_len, &c->pack_off, &c->counts, &c->need, &c->scr_off, &c->scratch,
                     &c->sizes, &c->spill_off, &c->scan_tmp, &c->arena, &c->packed, &c->counter, &c->stamps,
-                    &c->plan_small, &c->plan_big, &c->big_scratch, &c->lean_scr, &c->lean_tot, &c->cscr, &c->gs_list, &c->gs1, &c->gs2, &c->lean_ord, &c->lean_dbg, &c->plan_wlist, &c->v2x, &c->v2x_sz, &c->v2x_off, &c->v2_ust,
+                    &c->plan_small, &c->plan_big, &c->big_scratch, &c->lean_scr, &c->lean_tot, &c->cscr, &c->gs_list, &c->gs1, &c->gs2, &c->huge, &c->lean_ord, &c->lean_dbg, &c->plan_wlist, &c->v2x, &c->v2x_sz, &c->v2x_off, &c->v2_ust,
                     &c->v2_out, &c->v2_osz, &c->v2_ooff, &c->v2_svoff, &c->v2_svend, &c->v2_pre})
     b->release();
   if (c->h_pinned) hipHostFree(c->h_pinned);
@@ -282,6 +283,11 @@ static bool ensure_keep(ymerge_ctx *c, DevBuf &b, size_t bytes, size_t keep) {
   return true;
 }
 
+// overflow words for the long updates k_decode_huge decodes (5 per block, 2 per DeleteSet entry,
+// 3 per range: at most ~2.5 words per input byte; a batch that needs more leaves the rest on
+// the merge kernels' walk)
+static uint32_t huge_words(uint64_t n_bytes) { return (uint32_t)std::min<uint64_t>(n_bytes / 2 + 65536, 1u << 24); }
+
 // Stage times of a merge whose documents were all written by k_lean: its one host round trip
 // (hand-over count and output bytes) is taken right after k_lean, so the events recorded after
 // it are read here -- by the stats getter, or before the next call records the events again --
@@ -365,7 +371,9 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
       !c->scan_tmp.ensure(ym::scan_tmp_elems(n) * 8 + 64) || !c->counter.ensure(128 + 64 * 64) ||
       !ensure_keep(c, c->arena, slots + slots / 8 + 4096, 0) ||
       (c->fast_threads && (!c->rec.ensure((n_updates + 1) * ym::REC_WORDS * 4) ||
-                           !c->ovf.ensure(((n_updates + ym::DEC_NT - 1) / ym::DEC_NT + 1) * ym::DEC_OVF * 4))))
+                           !c->ovf.ensure(((n_updates + ym::DEC_NT - 1) / ym::DEC_NT + 1) * ym::DEC_OVF * 4 +
+                                          (uint64_t)huge_words(n_bytes) * 4) ||
+                           !c->huge.ensure(16 + 8 * ym::HUGE_LIST))))
     return YMERGE_ERR_DEVICE;
   b.rec = c->rec.as<uint32_t>();
   b.ovf = c->ovf.as<uint32_t>();
@@ -399,7 +407,8 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
       !c->want_stamps && c->giant_lane) {
     hipEventRecord(c->ev[7], c->s);
     hipEventRecord(c->ev[0], c->s);
-    ym::launch_decode(d_bytes, d_upd_off, n_updates, c->rec.as<uint32_t>(), c->ovf.as<uint32_t>(), c->s);
+    ym::launch_decode(d_bytes, d_upd_off, n_updates, c->rec.as<uint32_t>(), c->ovf.as<uint32_t>(), c->huge.as<uint32_t>(),
+                      huge_words(n_bytes), c->s);
     hipEventRecord(c->ev[5], c->s);
     const int rc = run_giant(c, b, fo, 0, (uint32_t)n_updates, 0, n_bytes);
     if (rc) return rc;
@@ -479,7 +488,8 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   hipEventRecord(c->ev[0], c->s);
   const bool fast = c->fast_threads && n_rej > 0;
   if (fast) {
-    ym::launch_decode(d_bytes, d_upd_off, n_updates, c->rec.as<uint32_t>(), c->ovf.as<uint32_t>(), c->s);
+    ym::launch_decode(d_bytes, d_upd_off, n_updates, c->rec.as<uint32_t>(), c->ovf.as<uint32_t>(), c->huge.as<uint32_t>(),
+                      huge_words(n_bytes), c->s);
     hipEventRecord(c->ev[5], c->s);
     ym::launch_fast_merge(b, c->caps, fo, c->fast_threads, c->s);
     if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;

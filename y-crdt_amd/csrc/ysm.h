@@ -10,6 +10,7 @@
 // the size of the fully inlined walk.
 #pragma once
 #include "ywin.h"
+#include "ylwin.h"
 
 namespace ym {
 
@@ -43,7 +44,7 @@ struct SmTrack {
   }
 };
 
-template <class S> YM_INLINE int smwalk_update(WCur &c, S &s) {
+template <class S, class C> YM_INLINE int smwalk_update(C &c, S &s) {
   uint32_t st = W_NCL;
   uint32_t ncl = 0, isec = 0, nb = 0, client = 0, clock = 0, j = 0, stored = 0, slot = 4;
   uint32_t nds = 0, ids = 0, dclient = 0, nr = 0, kr = 0, rst = 0;
