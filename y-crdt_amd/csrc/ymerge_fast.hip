@@ -207,7 +207,7 @@ __global__ void __launch_bounds__(64) k_decode_huge(const uint8_t *bytes, const 
     s.unsupported = s.big_ds = false;
     s.ubase = 0;
     LWin c;
-    lw_init(c, bytes + a0, ulen, win);
+    lw_init(c, bytes + a0, ulen, (lds_u32 *)win);
     const int e = smwalk_update(c, s);
     uint32_t w0, w1, w2, w3, w4, w5;
     rec_pack(s, e, w0, w1, w2, w3, w4, w5);
@@ -220,7 +220,7 @@ __global__ void __launch_bounds__(64) k_decode_huge(const uint8_t *bytes, const 
       if ((uint64_t)off + need <= huge_cap) {
         OvfFill f{ovf + huge_base + off, s.nb, s.ne, 0, 0, 0};
         LWin c2;
-        lw_init(c2, bytes + a0, ulen, win);
+        lw_init(c2, bytes + a0, ulen, (lds_u32 *)win);
         smwalk_update(c2, f);
         w0 |= REC_OVF;
         w4 = huge_base + off;

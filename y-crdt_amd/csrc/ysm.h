@@ -44,6 +44,34 @@ struct SmTrack {
   }
 };
 
+// one read of the walk: a raw byte (raw) or a LEB128 u32 with yrs' wrapping_shl (varint.rs:
+// 244-260; E_VARINT past 11 bytes); canon = re-encoding gives the same bytes
+template <class C> YM_INLINE int wc_read(C &c, bool raw, uint32_t &v, bool &canon) {
+  uint32_t sh = 0, nbytes = 0, b = 0;
+  v = 0;
+  for (;;) {
+    if (c.i >= c.n) return E_EOS;
+    b = wc_byte(c, c.i++);
+    if (raw) {
+      v = b;
+      return 0;
+    }
+    v |= (b & 0x7f) << (sh & 31);
+    sh += 7;
+    nbytes++;
+    if (b < 0x80) break;
+    if (sh > 70) return E_VARINT;
+  }
+  canon = nbytes == varlen(v) && (nbytes != 5 || b < 16);
+  return 0;
+}
+// OR of the bytes [s0, s0 + n) (the ASCII test of a string)
+template <class C> YM_INLINE uint32_t wc_or(C &c, uint32_t s0, uint32_t n) {
+  uint32_t hi = 0;
+  for (uint32_t q = 0; q < n; q++) hi |= wc_byte(c, s0 + q);
+  return hi;
+}
+
 template <class S, class C> YM_INLINE int smwalk_update(C &c, S &s) {
   uint32_t st = W_NCL;
   uint32_t ncl = 0, isec = 0, nb = 0, client = 0, clock = 0, j = 0, stored = 0, slot = 4;
@@ -69,21 +97,7 @@ template <class S, class C> YM_INLINE int smwalk_update(C &c, S &s) {
       } else if (st == W_DST) {
         wc_ensure(c, 20);
       }
-      uint32_t sh = 0, nbytes = 0, b = 0;
-      for (;;) {
-        if (c.i >= c.n) return E_EOS;
-        b = wc_byte(c, c.i++);
-        if (raw) {
-          v = b;
-          break;
-        }
-        v |= (b & 0x7f) << (sh & 31);
-        sh += 7;
-        nbytes++;
-        if (b < 0x80) break;
-        if (sh > 70) return E_VARINT;
-      }
-      if (!raw) canon = nbytes == varlen(v) && (nbytes != 5 || b < 16);
+      YM_TRY(wc_read(c, raw, v, canon));
     }
     // ---- state transition
     bool block_end = false, header_end = false;
@@ -178,8 +192,7 @@ template <class S, class C> YM_INLINE int smwalk_update(C &c, S &s) {
         bi.len = 1;
         break;
       }
-      uint32_t hi = 0;
-      for (uint32_t q = 0; q < v; q++) hi |= wc_byte(c, s0 + q);
+      const uint32_t hi = wc_or(c, s0, v);
       if (hi < 0x80) {
         bi.len = v;
         break;
