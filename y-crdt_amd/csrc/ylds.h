@@ -49,101 +49,105 @@ YM_INLINE bool lvar(LCur &c, uint32_t &v, bool &canon) {
   return true;
 }
 
-// One block at c.p (its info byte first): fills bi; false = bail.
-YM_INLINE bool fast_block(LCur &c, BlockInfo &bi) {
-  const uint32_t *w = c.w;
+// Decodes one staged update into the sink.  Returns 0, a sink error, or -1 (bail).
+template <class S> YM_INLINE int fast_walk(const uint32_t *w, uint32_t start, uint32_t n, S &s) {
+  LCur c{w, start, start + n};
   bool cn;
-  if (c.p >= c.end) return false;
-  const uint32_t info = lds_byte(w, c.p++);
-  bi.info = (uint8_t)info;
-  bi.reenc = bi.unsupported = bi.enc_panic = false;
-  bi.canon = 0;
-  uint32_t v;
-  if (info == 10 || info == 0) {
-    bi.kind = info == 10 ? BK_SKIP : BK_GC;
-    bi.ref = 0;
-    if (!lvar(c, bi.len, cn)) return false;
-    bi.reenc = !cn;
-    return true;
-  }
-  bi.kind = BK_ITEM;
-  uint32_t want = info & 0xCF;
-  bool ok = true;
-  if (info & 0x80) {
-    ok = lvar(c, v, cn) && (bi.reenc |= !cn, lvar(c, v, cn)) && (bi.reenc |= !cn, true);
-  }
-  if (ok && (info & 0x40)) {
-    ok = lvar(c, v, cn) && (bi.reenc |= !cn, lvar(c, v, cn)) && (bi.reenc |= !cn, true);
-  }
-  if (!ok) return false;
-  if ((info & 0xC0) == 0) {
-    uint32_t pi;
-    if (!lvar(c, pi, cn)) return false;
-    bi.reenc |= !cn || (pi != 1 && pi != 0);
-    if (!lvar(c, v, cn)) return false;
-    bi.reenc |= !cn;
-    if (pi == 1) {
-      if (v > c.end - c.p) return false;
-      c.p += v;
-    } else {
-      if (!lvar(c, v, cn)) return false;
-      bi.reenc |= !cn;
-    }
-    if (info & 0x20) {
-      want |= 0x20;
-      if (!lvar(c, v, cn)) return false;
-      bi.reenc |= !cn;
-      if (v > c.end - c.p) return false;
-      c.p += v;
-    }
-  }
-  if (want != info) bi.reenc = true;
-  const uint32_t ref = info & 15;
-  bi.ref = (uint8_t)ref;
-  if (ref == 1) {
-    if (!lvar(c, bi.len, cn)) return false;
-    bi.reenc |= !cn;
-  } else if (ref == 4) {
-    if (!lvar(c, v, cn)) return false;
-    bi.reenc |= !cn;
-    if (v > c.end - c.p) return false;
-    const uint32_t s0 = c.p;
-    c.p += v;
-    if (v == 1) {
-      bi.len = 1;
-    } else {
-      // any byte >= 0x80 in [s0, s0 + v)?  dword-wise: OR of the covering dwords,
-      // masked to the string's bytes in the first and last dword
-      uint32_t hi = 0;
-      const uint32_t e0 = s0 + v, q0 = s0 >> 2, q1 = (e0 - 1) >> 2;
-      for (uint32_t q = q0; q <= q1; q++) {
-        uint32_t x = w[q];
-        if (q == q0) x &= 0xFFFFFFFFu << (8 * (s0 & 3));
-        if (q == q1 && (e0 & 3)) x &= 0xFFFFFFFFu >> (8 * (4 - (e0 & 3)));
-        hi |= x;
+  uint32_t ncl, nds;
+  if (!lvar(c, ncl, cn)) return -1;
+  // every section and block takes >= 1 byte: larger counts cannot decode (the exact walk
+  // reports them, including yrs' try_reserve errors for absurd counts)
+  if (ncl > n) return -1;
+  for (uint32_t sec = 0; sec < ncl; sec++) {
+    uint32_t nb, client, clock;
+    if (!lvar(c, nb, cn) || !lvar(c, client, cn) || !lvar(c, clock, cn)) return -1;
+    if (nb > n) return -1;
+    s.on_section(client);
+    for (uint32_t j = 0; j < nb; j++) {
+      const uint32_t bpos = c.p;
+      if (c.p >= c.end) return -1;
+      const uint32_t info = lds_byte(w, c.p++);
+      BlockInfo bi;
+      bi.info = (uint8_t)info;
+      bi.reenc = bi.unsupported = bi.enc_panic = false;
+      bi.canon = 0;
+      uint32_t v;
+      if (info == 10 || info == 0) {
+        bi.kind = info == 10 ? BK_SKIP : BK_GC;
+        bi.ref = 0;
+        if (!lvar(c, bi.len, cn)) return -1;
+        bi.reenc = !cn;
+      } else {
+        bi.kind = BK_ITEM;
+        uint32_t want = info & 0xCF;
+        bool ok = true;
+        if (info & 0x80) {
+          ok = lvar(c, v, cn) && (bi.reenc |= !cn, lvar(c, v, cn)) && (bi.reenc |= !cn, true);
+        }
+        if (ok && (info & 0x40)) {
+          ok = lvar(c, v, cn) && (bi.reenc |= !cn, lvar(c, v, cn)) && (bi.reenc |= !cn, true);
+        }
+        if (!ok) return -1;
+        if ((info & 0xC0) == 0) {
+          uint32_t pi;
+          if (!lvar(c, pi, cn)) return -1;
+          bi.reenc |= !cn || (pi != 1 && pi != 0);
+          if (!lvar(c, v, cn)) return -1;
+          bi.reenc |= !cn;
+          if (pi == 1) {
+            if (v > c.end - c.p) return -1;
+            c.p += v;
+          } else {
+            if (!lvar(c, v, cn)) return -1;
+            bi.reenc |= !cn;
+          }
+          if (info & 0x20) {
+            want |= 0x20;
+            if (!lvar(c, v, cn)) return -1;
+            bi.reenc |= !cn;
+            if (v > c.end - c.p) return -1;
+            c.p += v;
+          }
+        }
+        if (want != info) bi.reenc = true;
+        const uint32_t ref = info & 15;
+        bi.ref = (uint8_t)ref;
+        if (ref == 1) {
+          if (!lvar(c, bi.len, cn)) return -1;
+          bi.reenc |= !cn;
+        } else if (ref == 4) {
+          if (!lvar(c, v, cn)) return -1;
+          bi.reenc |= !cn;
+          if (v > c.end - c.p) return -1;
+          const uint32_t s0 = c.p;
+          c.p += v;
+          if (v == 1) {
+            bi.len = 1;
+          } else {
+            // any byte >= 0x80 in [s0, s0 + v)?  dword-wise: OR of the covering dwords,
+            // masked to the string's bytes in the first and last dword
+            uint32_t hi = 0;
+            const uint32_t e0 = s0 + v, q0 = s0 >> 2, q1 = (e0 - 1) >> 2;
+            for (uint32_t q = q0; q <= q1; q++) {
+              uint32_t x = w[q];
+              if (q == q0) x &= 0xFFFFFFFFu << (8 * (s0 & 3));
+              if (q == q1 && (e0 & 3)) x &= 0xFFFFFFFFu >> (8 * (4 - (e0 & 3)));
+              hi |= x;
+            }
+            if (hi & 0x80808080u) return -1; // UTF-16 length of non-ASCII text: exact walk
+            bi.len = v;
+          }
+        } else {
+          return -1;
+        }
       }
-      if (hi & 0x80808080u) return false; // UTF-16 length of non-ASCII text: exact walk
-      bi.len = v;
+      if (!(bi.kind == BK_ITEM && bi.len == 0)) { // Item::new -> None: dropped
+        if ((uint64_t)clock + bi.len > 0xFFFFFFFFull) return -1;
+        YM_TRY(s.on_block(client, clock, bi, bpos - start, c.p - bpos));
+        clock += bi.len;
+      }
     }
-  } else {
-    return false;
   }
-  return true;
-}
-
-// block -> sink (Item::new drops a zero-length item); -1 = bail
-template <class S>
-YM_INLINE int fast_emit(S &s, uint32_t client, uint32_t &clock, const BlockInfo &bi, uint32_t rel, uint32_t blen) {
-  if (bi.kind == BK_ITEM && bi.len == 0) return 0;
-  if ((uint64_t)clock + bi.len > 0xFFFFFFFFull) return -1;
-  YM_TRY(s.on_block(client, clock, bi, rel, blen));
-  clock += bi.len;
-  return 0;
-}
-
-template <class S> YM_INLINE int fast_ds(LCur &c, uint32_t n, S &s) {
-  bool cn;
-  uint32_t nds;
   if (!lvar(c, nds, cn)) return -1;
   YM_TRY(s.on_ds_begin(nds));
   for (uint32_t i = 0; i < nds; i++) {
@@ -159,54 +163,6 @@ template <class S> YM_INLINE int fast_ds(LCur &c, uint32_t n, S &s) {
     }
   }
   return s.on_ds_done();
-}
-
-// Several client sections or blocks (a snapshot, a multi-block transaction): the same
-// grammar in loops.  fast_walk leaves these to the caller (-2), which walks them here after
-// its main pass, so the single-block path keeps its straight-line code and registers.
-// Every section and block takes >= 1 byte: larger counts cannot decode (the exact walk
-// reports them, including yrs' try_reserve errors for absurd counts).
-template <class S> YM_INLINE int fast_walk_multi(const uint32_t *w, uint32_t start, uint32_t n, S &s) {
-  LCur c{w, start, start + n};
-  bool cn;
-  uint32_t ncl;
-  if (!lvar(c, ncl, cn) || ncl > n) return -1;
-  for (uint32_t sec = 0; sec < ncl; sec++) {
-    uint32_t nb, client, clock;
-    if (!lvar(c, nb, cn) || !lvar(c, client, cn) || !lvar(c, clock, cn)) return -1;
-    if (nb > n) return -1;
-    s.on_section(client);
-    for (uint32_t j = 0; j < nb; j++) {
-      const uint32_t bpos = c.p;
-      BlockInfo bi;
-      if (!fast_block(c, bi)) return -1;
-      YM_TRY(fast_emit(s, client, clock, bi, bpos - start, c.p - bpos));
-    }
-  }
-  return fast_ds(c, n, s);
-}
-
-// Decodes one staged update into the sink.  Returns 0, a sink error, -1 (bail: the exact
-// walk) or -2 (several sections or blocks: fast_walk_multi; nothing reached the sink).
-template <class S> YM_INLINE int fast_walk(const uint32_t *w, uint32_t start, uint32_t n, S &s) {
-  LCur c{w, start, start + n};
-  bool cn;
-  uint32_t ncl;
-  if (!lvar(c, ncl, cn)) return -1;
-  if (ncl > 1) return -2;
-  if (ncl == 1) {
-    uint32_t nb, client, clock;
-    if (!lvar(c, nb, cn) || !lvar(c, client, cn) || !lvar(c, clock, cn)) return -1;
-    if (nb > 1) return -2;
-    s.on_section(client);
-    if (nb == 1) {
-      const uint32_t bpos = c.p;
-      BlockInfo bi;
-      if (!fast_block(c, bi)) return -1;
-      YM_TRY(fast_emit(s, client, clock, bi, bpos - start, c.p - bpos));
-    }
-  }
-  return fast_ds(c, n, s);
 }
 
 } // namespace ym

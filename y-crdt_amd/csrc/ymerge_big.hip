@@ -29,7 +29,11 @@ constexpr uint32_t BIG_DCAP = 1024;   // distinct DeleteSet clients per document
 constexpr uint32_t BIG_DTAB = 2048;   // LDS hash slots for them (u64)
 constexpr uint32_t BIG_CHUNK = 2048;  // LDS bitonic chunk of the sort (key u64 + value u32)
 constexpr uint32_t BIG_LU_LDS = 8192;
-constexpr uint32_t BIG_COOP = 64;      // records of one update from which the gather copies them cooperatively // overlap mode: updates / runs whose last-rank histogram stays in LDS
+constexpr uint32_t BIG_COOP = 64;
+#ifndef YM_DS_PACKED
+#define YM_DS_PACKED 1
+#endif
+constexpr bool BIG_DS_PACKED = YM_DS_PACKED; // DeleteSet range sort on packed keys (few clients)      // records of one update from which the gather copies them cooperatively // overlap mode: updates / runs whose last-rank histogram stays in LDS
 // LDS union region (phase-local): sort chunk (24 KB) / output stage / DeleteSet tables:
 //   [0, 16K) client hash table  [16K, 44K) 7 per-client arrays  [44K, 68K) sort chunk / slots
 constexpr uint32_t BIG_OFF_DARR = 8 * BIG_DTAB, BIG_OFF_SCR = BIG_OFF_DARR + 7 * 4 * BIG_DCAP;
@@ -209,7 +213,8 @@ __global__ void __launch_bounds__(NT) k_big_count(BatchIn b, uint8_t *path, uint
 // 64 E and more (6 of the 66 stages for NT = 512) go through LDS with two barriers each (the
 // LDS-only bitonic paid a barrier on every stage).  Positions at or past n are padding
 // (~0, ~0), sorted last; k / v hold the input and receive the first n results.
-template <int NT> __device__ void bitonic_reg(uint64_t *k, uint32_t *v, uint32_t n) {
+// KO: keys only (distinct keys, v unused): one 64-bit compare and no value moves per exchange
+template <int NT, bool KO = false> __device__ void bitonic_reg(uint64_t *k, uint32_t *v, uint32_t n) {
   constexpr uint32_t E = BIG_CHUNK / NT;
   static_assert(E >= 1 && E * NT == BIG_CHUNK, "one chunk per workgroup");
   const uint32_t t = threadIdx.x;
@@ -219,11 +224,11 @@ template <int NT> __device__ void bitonic_reg(uint64_t *k, uint32_t *v, uint32_t
   for (uint32_t r = 0; r < E; r++) {
     const uint32_t e = t * E + r;
     x[r] = e < n ? k[e] : ~0ull;
-    y[r] = e < n ? v[e] : 0xFFFFFFFFu;
+    y[r] = KO ? 0u : (e < n ? v[e] : 0xFFFFFFFFu);
   }
   // element e at the lower position of its pair keeps the minimum in an ascending block
   auto pick = [](uint64_t &a, uint32_t &av, uint64_t b, uint32_t bv, bool want_min) {
-    const bool g = a > b || (a == b && av > bv);
+    const bool g = a > b || (!KO && a == b && av > bv);
     if (g == want_min) {
       a = b;
       av = bv;
@@ -236,7 +241,7 @@ template <int NT> __device__ void bitonic_reg(uint64_t *k, uint32_t *v, uint32_t
 #pragma unroll
         for (uint32_t r = 0; r < E; r++) {
           k[t * E + r] = x[r];
-          v[t * E + r] = y[r];
+          if (!KO) v[t * E + r] = y[r];
         }
         __syncthreads();
         uint64_t px[E];
@@ -245,7 +250,7 @@ template <int NT> __device__ void bitonic_reg(uint64_t *k, uint32_t *v, uint32_t
         for (uint32_t r = 0; r < E; r++) {
           const uint32_t e = t * E + r;
           px[r] = k[e ^ st];
-          py[r] = v[e ^ st];
+          py[r] = KO ? 0u : v[e ^ st];
         }
 #pragma unroll
         for (uint32_t r = 0; r < E; r++) {
@@ -259,7 +264,7 @@ template <int NT> __device__ void bitonic_reg(uint64_t *k, uint32_t *v, uint32_t
           const uint32_t e = t * E + r;
           const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)x[r], ls, 64);
           const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(x[r] >> 32), ls, 64);
-          const uint32_t pv = (uint32_t)__shfl_xor((int)y[r], ls, 64);
+          const uint32_t pv = KO ? 0u : (uint32_t)__shfl_xor((int)y[r], ls, 64);
           pick(x[r], y[r], ((uint64_t)hi << 32) | lo, pv, !(e & st) == !(e & size));
         }
       } else {
@@ -272,7 +277,7 @@ template <int NT> __device__ void bitonic_reg(uint64_t *k, uint32_t *v, uint32_t
                 const uint32_t e = t * E + r;
                 const uint64_t a = x[r], b = x[r | ss];
                 const uint32_t av = y[r], bv = y[r | ss];
-                const bool g = a > b || (a == b && av > bv);
+                const bool g = a > b || (!KO && a == b && av > bv);
                 if (g == !(e & size)) {
                   x[r] = b;
                   y[r] = bv;
@@ -290,7 +295,7 @@ template <int NT> __device__ void bitonic_reg(uint64_t *k, uint32_t *v, uint32_t
     const uint32_t e = t * E + r;
     if (e < n) {
       k[e] = x[r];
-      v[e] = y[r];
+      if (!KO) v[e] = y[r];
     }
   }
   __syncthreads();
@@ -303,7 +308,8 @@ template <int NT> __device__ void bitonic_reg(uint64_t *k, uint32_t *v, uint32_t
 // base + i + (rank in the partner run): left-run elements count partner keys < k,
 // right-run elements count partner keys <= k (equal keys keep input order).
 // Returns the buffer pair holding the result (0: k0/v0, 1: k1/v1).
-template <int NT>
+// KO: keys only (distinct keys; v0 / v1 unused)
+template <int NT, bool KO = false>
 __device__ int wg_sort(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1, uint32_t n, uint8_t *lds) {
   uint64_t *ck = (uint64_t *)lds;
   uint32_t *cv = (uint32_t *)(lds + 8 * BIG_CHUNK);
@@ -312,15 +318,15 @@ __device__ int wg_sort(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1, u
     for (uint32_t j = threadIdx.x; j < CH; j += NT) {
       const uint32_t g = c0 + j;
       ck[j] = g < n ? k0[g] : ~0ull;
-      cv[j] = g < n ? v0[g] : 0xFFFFFFFFu;
+      if (!KO) cv[j] = g < n ? v0[g] : 0xFFFFFFFFu;
     }
     __syncthreads();
-    bitonic_reg<NT>(ck, cv, CH);
+    bitonic_reg<NT, KO>(ck, cv, CH);
     for (uint32_t j = threadIdx.x; j < CH; j += NT) {
       const uint32_t g = c0 + j;
       if (g < n) {
         k0[g] = ck[j];
-        v0[g] = cv[j];
+        if (!KO) v0[g] = cv[j];
       }
     }
     __syncthreads();
@@ -410,7 +416,7 @@ __device__ int wg_sort(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1, u
 #pragma unroll
       for (uint32_t q = 0; q < MB; q++) {
         const uint32_t j = j0 + q * NT;
-        vj[q] = j < n ? va[j] : 0;
+        vj[q] = !KO && j < n ? va[j] : 0;
       }
 #pragma unroll
       for (uint32_t q = 0; q < MB; q++) {
@@ -418,7 +424,7 @@ __device__ int wg_sort(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1, u
         if (j < n) {
           const uint32_t dst = base[q] + (j - (j / w) * w) + (lo[q] - b0[q]);
           kb[dst] = kj[q];
-          vb[dst] = vj[q];
+          if (!KO) vb[dst] = vj[q];
         }
       }
     }
@@ -1441,6 +1447,19 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
     const uint32_t lane = t & 63;
     uint32_t bad = 0, live_n = 0;
     constexpr uint32_t RB = 4;
+    // few clients (D <= 64, ranks in LDS ascending by client): keys packed as (client rank,
+    // start, index) in 6 + 32 + 26 bits -- distinct keys in the same order as (client, start,
+    // index), sorted keys-only (one 64-bit compare per exchange) and unpacked after
+    const bool pk = BIG_DS_PACKED && D <= 64 && NR < (1u << 26);
+    auto rank_of = [&](uint32_t c) -> uint64_t {
+      uint32_t lo = 0, hi = D;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (d_client[mid] < c) lo = mid + 1;
+        else hi = mid;
+      }
+      return lo;
+    };
     for (uint32_t j0 = t; j0 < NR; j0 += RB * NT) {
       uint32_t xi[RB], xs[RB], pi[RB], ps[RB];
 #pragma unroll
@@ -1467,23 +1486,44 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
       for (uint32_t q = 0; q < RB; q++) {
         const uint32_t j = j0 + q * NT;
         const bool live = xt[q] & 0x80000000u;
-        const uint64_t key = live ? (((uint64_t)xc[q] << 32) | xs[q]) : ~0ull;
+        const uint64_t key = !live ? ~0ull
+                             : pk  ? (rank_of(xc[q]) << 58) | ((uint64_t)xs[q] << 26) | j
+                                   : (((uint64_t)xc[q] << 32) | xs[q]);
         if (j < NR) {
           g_k0[j] = key;
-          g_v0[j] = j;
+          if (!pk) g_v0[j] = j;
           live_n += live;
         }
         const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)key, 1, 64);
         const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)(key >> 32), 1, 64);
         uint64_t prev = ((uint64_t)hi << 32) | lo;
-        if (lane == 0) prev = (pt[q] & 0x80000000u) ? (((uint64_t)pc[q] << 32) | ps[q]) : ~0ull;
+        if (lane == 0)
+          prev = !(pt[q] & 0x80000000u) ? ~0ull
+                 : pk ? (rank_of(pc[q]) << 58) | ((uint64_t)ps[q] << 26) | (j - 1)
+                      : (((uint64_t)pc[q] << 32) | ps[q]);
         if (j < NR && j > 0 && prev > key) bad = 1;
       }
     }
     bscan_sum<NT>(live_n, ws, NL);
-    if (__syncthreads_or(bad) && wg_sort<NT>(m.k0, m.v0, m.k1, m.v1, NR, lscr)) {
-      dkey = m.k1;
-      dval = m.v1;
+    const bool srt = __syncthreads_or(bad);
+    if (!pk) {
+      if (srt && wg_sort<NT>(m.k0, m.v0, m.k1, m.v1, NR, lscr)) {
+        dkey = m.k1;
+        dval = m.v1;
+      }
+    } else {
+      const int w = srt ? wg_sort<NT, true>(m.k0, m.v0, m.k1, m.v1, NR, lscr) : 0;
+      const uint64_t *src = w ? m.k1 : m.k0;
+      uint64_t *dst = w ? m.k0 : m.k1;
+      uint32_t *dv = w ? m.v0 : m.v1;
+      for (uint32_t j = t; j < NL; j += NT) {
+        const uint64_t k = src[j];
+        dst[j] = ((uint64_t)d_client[k >> 58] << 32) | (uint32_t)(k >> 26);
+        dv[j] = (uint32_t)k & 0x3FFFFFFu;
+      }
+      __syncthreads();
+      dkey = dst;
+      dval = dv;
     }
   }
   mark(11);

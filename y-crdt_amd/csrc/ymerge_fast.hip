@@ -106,10 +106,10 @@ __host__ __device__ inline FastLayout fast_layout(const FastCaps &c) {
 __global__ void __launch_bounds__(DEC_NT, 8) k_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_upd,
                                                       uint32_t *rec, uint32_t *ovf, uint32_t *huge) {
   __shared__ __align__(16) uint32_t stage[DEC_STAGE / 4 + 4];
-  __shared__ uint32_t ovf_top, n_cx, n_mx;
+  __shared__ uint32_t ovf_top, n_cx;
   ym_set_grammar(0); // fast_walk bails on every content it does not restate; v1 by construction
   __shared__ uint32_t cx_at[DEC_NT];
-  __shared__ uint16_t cx_lane[DEC_NT], cx_nb[DEC_NT], cx_ne[DEC_NT], mx_lane[DEC_NT];
+  __shared__ uint16_t cx_lane[DEC_NT], cx_nb[DEC_NT], cx_ne[DEC_NT];
   const uint64_t g0 = (uint64_t)blockIdx.x * DEC_NT;
   const uint32_t t = threadIdx.x;
   const uint64_t i = g0 + t;
@@ -134,7 +134,6 @@ __global__ void __launch_bounds__(DEC_NT, 8) k_decode(const uint8_t *bytes, cons
   if (t == 0) {
     ovf_top = 0;
     n_cx = 0;
-    n_mx = 0;
   }
   __syncthreads();
   if (i < n_upd) {
@@ -145,11 +144,7 @@ __global__ void __launch_bounds__(DEC_NT, 8) k_decode(const uint8_t *bytes, cons
     s.unsupported = s.big_ds = false;
     s.ubase = 0;
     const bool staged = a1 - sbase <= 4 * nd;
-    int e = staged ? fast_walk(stage, (uint32_t)(a0 - sbase), ulen, s) : -1;
-    if (e == -2) { // several sections / blocks: walked after this pass (REC_SLOW until then)
-      mx_lane[atomicAdd(&n_mx, 1u)] = (uint16_t)t;
-      e = -1;
-    }
+    const int e = staged ? fast_walk(stage, (uint32_t)(a0 - sbase), ulen, s) : -1;
     if (!staged && ulen >= HUGE_MIN) { // a long update: k_decode_huge walks it (a wavefront, LDS window)
       const uint32_t k = atomicAdd(&huge[0], 1u);
       if (k < HUGE_LIST) ((uint64_t *)(huge + 4))[k] = i;
@@ -187,35 +182,6 @@ __global__ void __launch_bounds__(DEC_NT, 8) k_decode(const uint8_t *bytes, cons
     const uint64_t a0 = upd_off[j], a1 = upd_off[j + 1];
     OvfFill f{ovf + cx_at[q], cx_nb[q], cx_ne[q], 0, 0, 0};
     fast_walk(stage, (uint32_t)(a0 - sbase), (uint32_t)(a1 - a0), f);
-  }
-  // updates of several sections / blocks (a GC'd snapshot heading a log), packed onto the
-  // first lanes: count walk, record, then the overflow words (after the pass above, whose
-  // allocations are done)
-  for (uint32_t q = t; q < n_mx; q += DEC_NT) {
-    const uint64_t j = g0 + mx_lane[q];
-    const uint64_t a0 = upd_off[j], a1 = upd_off[j + 1];
-    const uint32_t start = (uint32_t)(a0 - sbase), ulen = (uint32_t)(a1 - a0);
-    RegSink s;
-    s.nb = s.ne = s.nr = 0;
-    s.unsupported = s.big_ds = false;
-    s.ubase = 0;
-    const int e = fast_walk_multi(stage, start, ulen, s);
-    if (e < 0) continue; // the exact walk downstream (the record stays REC_SLOW)
-    uint32_t w0, w1, w2, w3, w4, w5;
-    rec_pack(s, e, w0, w1, w2, w3, w4, w5);
-    if (e == 0 && ((w0 >> 10) & 3) == REC_COMPLEX && !s.big_ds) {
-      const uint32_t need = 5 * s.nb + 2 * s.ne + 3 * s.nr;
-      const uint32_t off = need <= DEC_OVF ? atomicAdd(&ovf_top, need) : DEC_OVF;
-      if (off + need > DEC_OVF) continue; // no room: REC_SLOW
-      OvfFill f{ovf + blockIdx.x * DEC_OVF + off, s.nb, s.ne, 0, 0, 0};
-      fast_walk_multi(stage, start, ulen, f);
-      w0 |= REC_OVF;
-      w4 = blockIdx.x * DEC_OVF + off;
-    }
-    uint2 *o = (uint2 *)(rec + j * REC_WORDS);
-    o[0] = make_uint2(w0, w1);
-    o[1] = make_uint2(w2, w3);
-    o[2] = make_uint2(w4, w5);
   }
 }
 
