@@ -65,20 +65,41 @@ def test_b4_merge_gpu(oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("planner", ["ring", "lane", "wave"])
+@pytest.mark.parametrize("planner", ["grid", "ring", "lane", "wave"])
 def test_b4_sv_and_diff_gpu(oracle, planner):
-    """b4 and its merge through each planner (the merged form is canonical, 375 KB: under
-    "lane" it is a k_plan_wave document; b4 itself has 7-byte client varints, which the
-    common-shape planners hand to k_plan)."""
+    """b4 and its merge through the long-update grid path (ylong.hip: the parallel parse, then a
+    lane per block) and, with it turned off, through each planner (the merged form is canonical,
+    375 KB: under "lane" it is a k_plan_wave document; b4 itself has 7-byte client varints, which
+    the common-shape planners hand to k_plan)."""
     from test_gpu_diff import check_diff, check_sv
     from test_gpu_parity import engine_with
     u = corpus.b4_update()
     m = oracle.merge_updates_v1([u])
     (client, clock), = oracle.parse_sv(oracle.encode_state_vector_from_update_v1(u))
-    eng = engine_with(YMERGE_PLANNER=planner)
+    env = {} if planner == "grid" else {"YMERGE_PLANNER": planner, "YMERGE_LONG_GRID": 0}
+    eng = engine_with(**env)
     try:
         check_sv(eng, oracle, [u, m])
         svs = _remote_svs(client, clock)
         check_diff(eng, oracle, [u] * len(svs) + [m] * len(svs), svs + svs)
     finally:
         eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("grid", [1, 0])
+def test_b4_merge_paths(oracle, grid):
+    """merge_updates_v1([b4]) on the long-update grid path and, turned off, on the tiled kernel;
+    also with the parallel parse off (every long update walked by k_decode_huge)."""
+    import ymerge
+    from test_gpu_parity import engine_with
+    u = corpus.b4_update()
+    for env in ({"YMERGE_LONG_GRID": grid}, {"YMERGE_LONG_PARSE": grid}):
+        eng = engine_with(**env)
+        try:
+            check_batch(eng, oracle, batch_of([[u], [u[:5000]], [u], [u, b"\x00\x00"]]))
+            st = eng.stats()
+            if grid:
+                assert st["docs_giant"] >= 2, st  # the two [u] documents on the grid path
+        finally:
+            eng.close()

@@ -578,6 +578,7 @@ __global__ void __launch_bounds__(RING_NT) k_plan_ring(DiffBatch b, PlanScratch 
     ps.size[d] = 0;
     active = false;
   }
+  if (active && b.ls_done && b.ls_done[d]) active = false; // the long-update grid path's (ylong.hip)
   const uint8_t *up = nullptr, *svp = nullptr;
   uint32_t un = 0, svn = 0, nsv = 0;
   uint32_t *scr = nullptr;
@@ -1320,6 +1321,7 @@ __device__ __forceinline__ bool pw_deleteset(uint32_t *u, uint32_t *de, const ui
 template <bool DIFF>
 __device__ __forceinline__ void pw_plan_doc(const DiffBatch &b, const PlanScratch &ps, PwLds &S, uint32_t lane,
                                          uint32_t d) {
+  if (b.ls_done && b.ls_done[d]) return; // the long-update grid path's (ylong.hip)
   if (b.pre_status && b.pre_status[d]) { // e.g. a y-sync message that is not SyncStep1
     if (lane == 0) {
       ps.big[d] = 0;
@@ -1730,6 +1732,7 @@ __global__ void __launch_bounds__(RING_NT) k_plan_lane(DiffBatch b, PlanScratch 
     ps.size[d] = 0;
     active = false;
   }
+  if (active && b.ls_done && b.ls_done[d]) active = false; // the long-update grid path's (ylong.hip)
   if (active && ps.wave_list && b.upd_off[d + 1] - b.upd_off[d] >= PW_MIN) { // one long update: k_plan_wave
     ps.big[d] = PLAN_WAVE;
     ps.wave_list[atomicAdd(ps.wave_n, 1u)] = d;
@@ -2299,6 +2302,7 @@ __global__ void __launch_bounds__(64) k_plan(DiffBatch b, PlanScratch ps, int pa
   if (d >= b.n_docs) return;
   if (pass == 1 && !ps.big[d]) return;
   if (pass == 0 && ps.big[d] != PLAN_REDO) return; // planned by k_plan_ring
+  if (b.ls_done && b.ls_done[d]) return;
   if (b.pre_status && b.pre_status[d]) { // e.g. a y-sync message that is not SyncStep1
     ps.big[d] = 0;
     ps.status[d] = b.pre_status[d];
@@ -2444,7 +2448,7 @@ __global__ void __launch_bounds__(256) k_exec(DiffBatch b, PlanScratch ps, const
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t d = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   if (d >= b.n_docs) return;
-  if (ps.status[d] || ps.size[d] == 0) return;
+  if (ps.status[d] || ps.size[d] == 0 || (b.ls_done && b.ls_done[d])) return;
   const uint64_t o0 = b.upd_off[d], o1 = b.upd_off[d + 1];
   const uint8_t *up = b.bytes + o0;
   const uint32_t un = (uint32_t)(o1 - o0);
@@ -2514,7 +2518,7 @@ __global__ void __launch_bounds__(64) k_exec_cold(DiffBatch b, PlanScratch ps, c
   ym_set_grammar(b.v1x);
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= b.n_docs) return;
-  if (ps.status[d] || ps.size[d] == 0) return;
+  if (ps.status[d] || ps.size[d] == 0 || (b.ls_done && b.ls_done[d])) return;
   const uint64_t o0 = b.upd_off[d], o1 = b.upd_off[d + 1];
   const uint8_t *up = b.bytes + o0;
   const uint32_t un = (uint32_t)(o1 - o0);

@@ -5,6 +5,10 @@
 #include <stdint.h>
 
 namespace ym {
+// exclusive scan: out[0..n] (out[n] = total); tmp needs >= (n/2048 + 2) u64
+// n_dev: optional device-side element count (<= n, the count the grid is sized for)
+void launch_scan_u64(const uint64_t *in, uint64_t *out, uint32_t n, uint64_t *tmp, hipStream_t s,
+                     const uint32_t *n_dev = nullptr);
 // A batch of documents in HBM: doc d owns updates [doc_upd[d], doc_upd[d+1]);
 // update u owns bytes [upd_off[u], upd_off[u+1]) of `bytes`.
 struct BatchIn {
@@ -34,8 +38,78 @@ constexpr uint32_t REC_EMPTY = 0, REC_BLOCK = 1, REC_DS = 2, REC_COMPLEX = 3;
 // huge: [count, bump, -, -, u64 list of HUGE_LIST update indices]; huge_cap: overflow words
 // after the k_decode workgroups' DEC_OVF words for the updates k_decode_huge decodes
 constexpr uint32_t HUGE_MIN = 2048, HUGE_LIST = 4096;
+// REC_COMPLEX record written by the parallel long-update parse (ylong.hip) for an update of one
+// client section without Skips, zero-length GC blocks, panicking splits or unsupported content,
+// and <= 1 DeleteSet entry; w5 = its LP entry + 1 (grid paths for single-update documents)
+constexpr uint32_t REC_LONG = 1u << 16;
+
+// ---- parallel parse of long updates (ylong.hip)
+constexpr uint32_t LP_CH = 8192;  // bytes per chunk
+constexpr uint32_t LP_MW = 16;    // meta words per long update
+constexpr uint32_t LP_SEGW = 6;   // words per segment
+enum : uint32_t {                 // meta words
+  LPM_U = 0, LPM_L = 2, LPM_CB, LPM_NCH, LPM_PB, LPM_FLAGS, LPM_NBALL, LPM_NB, LPM_DS, LPM_SB, LPM_NCL, LPM_OB, LPM_OVF,
+  LPM_NE, LPM_NR
+};
+enum : uint32_t { // flags
+  LPF_FALLBACK = 1, LPF_UNSUP = 2, LPF_SKIP = 4, LPF_ZGC = 8, LPF_PANIC = 16, LPF_MSEC = 32, LPF_RICH = 64
+};
+enum : uint32_t { LPG_CHUNKS = 0, LPG_SEGS, LPG_ORDS, LPG_SECS, LPG_N, LPG_WORDS = 8 };
+struct LpArgs {
+  const uint8_t *bytes;
+  const uint64_t *upd_off;
+  uint32_t *rec, *ovf;
+  uint32_t *huge;            // k_decode's list: [0] count, [1] exact-walker count, [2..3] u64 overflow bump, list
+  uint32_t huge_base;        // first overflow word of the long-update region
+  uint64_t huge_cap;         // its words
+  uint32_t *meta, *g, *c2e;  // per long update, counters, chunk -> update
+  uint32_t *ext;             // [pcap] speculative block ends
+  uint64_t *jc;              // [pcap] (first boundary past the chunk, blocks | stored << 16)
+  uint32_t *seg, *sec;       // segments [scap], sections [seccap] (client, clock, first ordinal, update)
+  uint64_t *blen, *sblen;    // [ocap] clock lengths in block order, scan [ocap + 1]
+  uint32_t *omap;            // [ocap] record word + 1 of a stored block, 0 otherwise
+  uint64_t *fb;              // updates left to the exact walker (k_decode_huge)
+  uint64_t *scan_tmp;
+  uint32_t pcap, ccap, scap, seccap, ocap;
+  uint32_t v1x;
+};
+void launch_long_decode(const LpArgs &a, hipStream_t s);
+
+// ---- single long update documents on the grid (ylong.hip, after the parallel parse): merge_updates_v1
+// of a document that is one REC_LONG update, its diff_updates_v1 / state vector.  One document
+// per launch sequence; the list entries (LS_EW words) come from k_ls_find / k_ls_collect.
+constexpr uint32_t LS_LIST = 16, LS_EW = 8; // entry: doc, update lo, hi, L, NB, NE, NR, ovf base
+constexpr uint32_t LS_MIN_DIFF = 65536;     // diff / SV: documents of >= this many bytes (env YMERGE_LS_MIN)
+enum : uint32_t { LSG_BAD = 0, LSG_K0, LSG_OFF, LSG_HDR, LSG_DSH, LSG_K, LSG_CLIENT, LSG_CLOCK, LSG_END, LSG_WORDS = 16 };
+struct LsArgs {
+  const uint8_t *bytes;    // the update: bytes + upd_off[u]
+  uint32_t L, NB, NE, NR;
+  const uint32_t *ov;      // its records (OvfFill layout)
+  uint32_t d, mode;        // document; 0 merge, 1 diff, 2 state vector
+  uint32_t v1x, frame;     // grammar; y-sync framing (diff / SV)
+  const uint8_t *sv;       // diff: remote state vector bytes
+  const uint64_t *sv_off, *sv_end;
+  uint32_t *g;             // LSG_WORDS per document
+  uint64_t *bsz, *boff;    // [NB], [NB + 1]
+  uint64_t *rsz, *roff;    // [NR], [NR + 1]
+  uint64_t *scan_tmp;
+  // merge: the document's slot in the output arena; diff / SV: the packed output (after the scan)
+  uint8_t *out;
+  const uint64_t *upd_off; // (merge: the slot is 2 * upd_off[u] + 64 * d)
+  uint64_t u;
+  uint64_t *out_start, *out_len, *size;
+  uint8_t *status, *path, *done;
+  uint32_t *npath;
+  const uint64_t *pack_off;
+};
+void launch_ls_find(const BatchIn &b, const uint8_t *path, uint32_t *list, hipStream_t s);
+void launch_ls_list_diff(const uint64_t *upd_off, const uint8_t *pre_status, uint32_t n_docs, uint32_t min_len,
+                         uint32_t *huge, hipStream_t s);
+void launch_ls_collect(const LpArgs &a, uint32_t *list, hipStream_t s);
+// phase 0: checks, sizes, scans, totals (merge: also the write); phase 1 (diff / SV): the write
+void launch_ls_doc(const LsArgs &a, int phase, hipStream_t s);
 void launch_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_updates, uint32_t *rec, uint32_t *ovf,
-                   uint32_t *huge, uint32_t huge_cap, hipStream_t s);
+                   uint32_t *huge, uint32_t huge_cap, hipStream_t s, const LpArgs *lp = nullptr);
 
 // LDS capacities of the one-workgroup-per-document fast path (per document)
 struct FastCaps {
@@ -117,10 +191,6 @@ void launch_seq_merge(bool write, const BatchIn &b, const uint8_t *path, const u
                       const uint64_t *scr_off, uint32_t *scratch, uint64_t *sizes, const uint64_t *out_off,
                       uint8_t *out, uint64_t out_base, uint64_t *out_start, uint64_t *out_len, uint8_t *status_out,
                       hipStream_t s);
-// exclusive scan: out[0..n] (out[n] = total); tmp needs >= (n/2048 + 2) u64
-// n_dev: optional device-side element count (<= n, the count the grid is sized for)
-void launch_scan_u64(const uint64_t *in, uint64_t *out, uint32_t n, uint64_t *tmp, hipStream_t s,
-                     const uint32_t *n_dev = nullptr);
 size_t scan_tmp_elems(uint32_t n);
 void launch_pack(const uint8_t *src, const uint64_t *start, const uint64_t *len, const uint64_t *pack_off,
                  uint8_t *dst, uint32_t n_docs, hipStream_t s);
@@ -138,6 +208,7 @@ struct DiffBatch {
   const uint8_t *pre_status = nullptr;    // optional: nonzero = the document failed before planning
   uint32_t frame = 0;                     // y-sync framing: 0 none, 1 SyncStep2, 2 SyncStep1
   uint32_t v1x = 0;                       // bytes are the internal v1x grammar (lib0 v2 path)
+  const uint8_t *ls_done = nullptr;       // optional: nonzero = planned and written by the long-update grid path
 };
 // y-sync: parse one client message per document (must be Message::Sync(SyncStep1(sv)),
 // yrs/src/sync/protocol.rs:179-203, 245-272) -> SV slice [sv_off, sv_end) + status

@@ -193,13 +193,15 @@ __global__ void __launch_bounds__(DEC_NT, 8) k_decode(const uint8_t *bytes, cons
 // kernels then read records instead of walking the update over HBM, once per kernel, through
 // a 64-byte register window (b4-update.bin: ~1 s -> a few ms).
 __global__ void __launch_bounds__(64) k_decode_huge(const uint8_t *bytes, const uint64_t *upd_off, uint32_t *rec,
-                                                   uint32_t *ovf, uint32_t *huge, uint32_t huge_base, uint32_t huge_cap) {
+                                                   uint32_t *ovf, uint32_t *huge, const uint32_t *count,
+                                                   const uint64_t *list, uint32_t huge_base, uint64_t huge_cap,
+                                                   uint32_t v1x) {
   __shared__ __align__(16) uint32_t win[LW_BYTES / 4];
-  ym_set_grammar(0);
+  ym_set_grammar(v1x);
   const uint32_t lane = threadIdx.x;
-  const uint32_t n = huge[0] < HUGE_LIST ? huge[0] : HUGE_LIST;
+  const uint32_t n = *count < HUGE_LIST ? *count : HUGE_LIST;
   for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
-    const uint64_t i = ((const uint64_t *)(huge + 4))[k];
+    const uint64_t i = list[k];
     const uint64_t a0 = upd_off[i], a1 = upd_off[i + 1];
     const uint32_t ulen = (uint32_t)(a1 - a0);
     RegSink s;
@@ -213,17 +215,20 @@ __global__ void __launch_bounds__(64) k_decode_huge(const uint8_t *bytes, const 
     rec_pack(s, e, w0, w1, w2, w3, w4, w5);
     bool write = true;
     if (e == 0 && ((w0 >> 10) & 3) == REC_COMPLEX && !s.big_ds) {
-      const uint32_t need = 5 * s.nb + 2 * s.ne + 3 * s.nr;
-      uint32_t off = 0;
-      if (lane == 0) off = atomicAdd(&huge[1], need);
-      off = (uint32_t)__builtin_amdgcn_readfirstlane((int)off);
-      if ((uint64_t)off + need <= huge_cap) {
+      const uint64_t need = 5ull * s.nb + 2ull * s.ne + 3ull * s.nr;
+      uint64_t off = 0;
+      // 64-bit bump (shared with the parallel parse): a request that does not fit still advances
+      // it, but it cannot wrap onto words already handed out
+      if (lane == 0) off = atomicAdd((unsigned long long *)(huge + 2), (unsigned long long)need);
+      off = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(off >> 32)) << 32) |
+            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)off);
+      if (off + need <= huge_cap) {
         OvfFill f{ovf + huge_base + off, s.nb, s.ne, 0, 0, 0};
         LWin c2;
         lw_init(c2, bytes + a0, ulen, (lds_u32 *)win);
         smwalk_update(c2, f);
         w0 |= REC_OVF;
-        w4 = huge_base + off;
+        w4 = huge_base + (uint32_t)off;
       } else {
         write = false; // no room: the record stays REC_SLOW
       }
@@ -237,14 +242,32 @@ __global__ void __launch_bounds__(64) k_decode_huge(const uint8_t *bytes, const 
   }
 }
 
+// k_decode, then the long updates it listed: the parallel parse (ylong.hip) when its scratch is
+// given, the exact lockstep walk for the ones it leaves (errors, bounds); without it every listed
+// update takes the exact walk
 void launch_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_updates, uint32_t *rec, uint32_t *ovf,
-                   uint32_t *huge, uint32_t huge_cap, hipStream_t s) {
+                   uint32_t *huge, uint32_t huge_cap, hipStream_t s, const LpArgs *lp) {
   if (!n_updates) return;
   const uint64_t nwg = (n_updates + DEC_NT - 1) / DEC_NT;
   hipMemsetAsync(huge, 0, 16, s);
   hipLaunchKernelGGL(k_decode, dim3((unsigned)nwg), dim3(DEC_NT), 0, s, bytes, upd_off, n_updates, rec, ovf, huge);
-  hipLaunchKernelGGL(k_decode_huge, dim3(64), dim3(64), 0, s, bytes, upd_off, rec, ovf, huge,
-                     (uint32_t)(nwg * DEC_OVF), huge_cap);
+  const uint32_t base = (uint32_t)(nwg * DEC_OVF);
+  if (lp) {
+    LpArgs a = *lp;
+    a.bytes = bytes;
+    a.upd_off = upd_off;
+    a.rec = rec;
+    a.ovf = ovf;
+    a.huge = huge;
+    a.huge_base = base;
+    a.huge_cap = huge_cap;
+    launch_long_decode(a, s);
+    hipLaunchKernelGGL(k_decode_huge, dim3(64), dim3(64), 0, s, bytes, upd_off, rec, ovf, huge,
+                       (const uint32_t *)(huge + 1), (const uint64_t *)a.fb, base, (uint64_t)huge_cap, a.v1x);
+  } else {
+    hipLaunchKernelGGL(k_decode_huge, dim3(64), dim3(64), 0, s, bytes, upd_off, rec, ovf, huge, (const uint32_t *)huge,
+                       (const uint64_t *)(huge + 4), base, (uint64_t)huge_cap, 0u);
+  }
 }
 
 // ------------------------------------------------------------------ the kernel

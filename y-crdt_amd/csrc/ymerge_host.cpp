@@ -67,7 +67,12 @@ struct ymerge_ctx {
   DevBuf status, path, out_start, out_len, pack_off, counts, need, scr_off, scratch, sizes, spill_off, scan_tmp;
   DevBuf arena, packed, counter, stamps, plan_small, plan_big, rec, ovf, big_scratch, lean_scr, lean_tot, cscr;
   DevBuf gs_list, gs1, gs2; // long single-client documents (ygiant.hip)
-  DevBuf huge;              // k_decode_huge's list and bump counter
+  DevBuf huge;              // k_decode's list of long updates, overflow bump counter
+  DevBuf lp;                // the parallel parse of long updates (ylong.hip): scratch
+  bool long_parse = true;   // env YMERGE_LONG_PARSE=0: every long update takes the exact walk
+  bool long_grid = true;    // env YMERGE_LONG_GRID=0: single long update documents take the tiled kernel / planners
+  uint32_t ls_min_diff = ym::LS_MIN_DIFF; // diff / SV documents on the long-update grid path (env YMERGE_LS_MIN)
+  DevBuf ls_list, ls_scr, ls_done, ls_ovf; // their list, per-document scratch, planner skip flags, records
   DevBuf lean_ord;          // k_lean dispatch order: 8 counters, then n_docs document indices
   DevBuf plan_wlist;        // diff / SV: documents k_plan_lane leaves to k_plan_wave
   DevBuf lean_dbg;          // YMERGE_LEAN_DEBUG hand-over reasons (this context's device only)
@@ -129,6 +134,9 @@ static bool ctx_init(ymerge_ctx *c, int device) {
   if (const char *v = getenv("YMERGE_PLANNER"))
     c->planner = strcmp(v, "ring") == 0 ? 1u : strcmp(v, "wave") == 0 ? 2u : 0u;
   if (const char *v = getenv("YMERGE_LEAN_SCR_MAX")) c->lean_scr_max = strtoull(v, nullptr, 10);
+  if (const char *v = getenv("YMERGE_LONG_PARSE")) c->long_parse = atoi(v) != 0;
+  if (const char *v = getenv("YMERGE_LONG_GRID")) c->long_grid = atoi(v) != 0;
+  if (const char *v = getenv("YMERGE_LS_MIN")) c->ls_min_diff = (uint32_t)atoi(v);
   // the fast kernel's LDS layout must fit one workgroup (160 KB on gfx950)
   int lds_max = 0;
   if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess) return false;
@@ -156,7 +164,7 @@ extern "C" void ymerge_ctx_destroy(ymerge_ctx *c) {
                     &c->sync_end, &c->sync_st, &c->rec, &c->ovf, &c->status, &c->path,
                     &c->out_start, &c->out_len, &c->pack_off, &c->counts, &c->need, &c->scr_off, &c->scratch,
                     &c->sizes, &c->spill_off, &c->scan_tmp, &c->arena, &c->packed, &c->counter, &c->stamps,
-                    &c->plan_small, &c->plan_big, &c->big_scratch, &c->lean_scr, &c->lean_tot, &c->cscr, &c->gs_list, &c->gs1, &c->gs2, &c->huge, &c->lean_ord, &c->lean_dbg, &c->plan_wlist, &c->v2x, &c->v2x_sz, &c->v2x_off, &c->v2_ust,
+                    &c->plan_small, &c->plan_big, &c->big_scratch, &c->lean_scr, &c->lean_tot, &c->cscr, &c->gs_list, &c->gs1, &c->gs2, &c->huge, &c->lp, &c->ls_list, &c->ls_scr, &c->ls_done, &c->ls_ovf, &c->lean_ord, &c->lean_dbg, &c->plan_wlist, &c->v2x, &c->v2x_sz, &c->v2x_off, &c->v2_ust,
                     &c->v2_out, &c->v2_osz, &c->v2_ooff, &c->v2_svoff, &c->v2_svend, &c->v2_pre})
     b->release();
   if (c->h_pinned) hipHostFree(c->h_pinned);
@@ -288,6 +296,51 @@ static bool ensure_keep(ymerge_ctx *c, DevBuf &b, size_t bytes, size_t keep) {
 // the merge kernels' walk)
 static uint32_t huge_words(uint64_t n_bytes) { return (uint32_t)std::min<uint64_t>(n_bytes / 2 + 65536, 1u << 24); }
 
+// Scratch of the parallel long-update parse, sized from the batch's bytes (long updates total at
+// most n_bytes; past LP_PMAX positions the rest take the exact walk).  Null when disabled or the
+// allocation fails (then every long update takes the exact walk).
+constexpr uint64_t LP_PMAX = 16u << 20;
+static const ym::LpArgs *lp_args(ymerge_ctx *c, uint64_t n_bytes, uint32_t v1x) {
+  static thread_local ym::LpArgs a;
+  if (!c->long_parse) return nullptr;
+  const uint64_t pcap = std::min<uint64_t>(n_bytes + 16, LP_PMAX);
+  const uint64_t ccap = pcap / ym::LP_CH + ym::HUGE_LIST, scap = 4 * ccap + 65536, seccap = pcap / 3 + 16,
+                 ocap = pcap / 2 + ym::HUGE_LIST;
+  const uint64_t tmp = ym::scan_tmp_elems((uint32_t)ocap) + 2;
+  const uint64_t bytes = 64ull * ym::HUGE_LIST + 64 + 4 * ccap + 4 * pcap + 8 * pcap + 4 * ym::LP_SEGW * scap +
+                         16 * seccap + 8 * ocap + 8 * (ocap + 1) + 4 * ocap + 8ull * ym::HUGE_LIST + 8 * tmp + 256;
+  if (!c->lp.ensure(bytes)) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  uint8_t *q = c->lp.as<uint8_t>();
+  auto take = [&](uint64_t n) {
+    uint8_t *r = q;
+    q += (n + 15) & ~15ull;
+    return r;
+  };
+  a = ym::LpArgs{};
+  a.meta = (uint32_t *)take(4ull * ym::LP_MW * ym::HUGE_LIST);
+  a.g = (uint32_t *)take(4 * ym::LPG_WORDS);
+  a.c2e = (uint32_t *)take(4 * ccap);
+  a.ext = (uint32_t *)take(4 * pcap);
+  a.jc = (uint64_t *)take(8 * pcap);
+  a.seg = (uint32_t *)take(4 * ym::LP_SEGW * scap);
+  a.sec = (uint32_t *)take(16 * seccap);
+  a.blen = (uint64_t *)take(8 * ocap);
+  a.sblen = (uint64_t *)take(8 * (ocap + 1));
+  a.omap = (uint32_t *)take(4 * ocap);
+  a.fb = (uint64_t *)take(8ull * ym::HUGE_LIST);
+  a.scan_tmp = (uint64_t *)take(8 * tmp);
+  a.pcap = (uint32_t)pcap;
+  a.ccap = (uint32_t)ccap;
+  a.scap = (uint32_t)scap;
+  a.seccap = (uint32_t)seccap;
+  a.ocap = (uint32_t)ocap;
+  a.v1x = v1x;
+  return &a;
+}
+
 // Stage times of a merge whose documents were all written by k_lean: its one host round trip
 // (hand-over count and output bytes) is taken right after k_lean, so the events recorded after
 // it are read here -- by the stats getter, or before the next call records the events again --
@@ -354,6 +407,41 @@ static int run_giant(ymerge_ctx *c, const ym::BatchIn &b, const ym::FastOut &fo,
   return hipGetLastError() == hipSuccess ? 0 : YMERGE_ERR_DEVICE;
 }
 
+// Single long update documents (ylong.hip): list entries read back from the device (LS_EW words:
+// doc, update, L, NB, NE, NR, overflow word).  Scratch per document: 16 words, block sizes and
+// offsets, range sizes and offsets, the scan's tiles; `scr_words` sums them for a list.
+struct LsEntry {
+  uint32_t d, L, NB, NE, NR, ovf;
+  uint64_t u;
+};
+static uint64_t ls_scratch_words(const LsEntry &e) {
+  return 16 + 2 * (2ull * e.NB + 2 + 2ull * e.NR + 2 + ym::scan_tmp_elems(std::max(e.NB, e.NR)) + 2) + 16;
+}
+static std::vector<LsEntry> ls_entries(const uint32_t *w) {
+  std::vector<LsEntry> v;
+  const uint32_t n = std::min(w[0], ym::LS_LIST);
+  for (uint32_t k = 0; k < n; k++) {
+    const uint32_t *e = w + 4 + ym::LS_EW * k;
+    v.push_back(LsEntry{e[0], e[3], e[4], e[5], e[6], e[7], e[1] | ((uint64_t)e[2] << 32)});
+  }
+  return v;
+}
+static void ls_bind(ym::LsArgs &a, const LsEntry &e, uint32_t *scr) {
+  a.L = e.L;
+  a.NB = e.NB;
+  a.NE = e.NE;
+  a.NR = e.NR;
+  a.d = e.d;
+  a.u = e.u;
+  a.g = scr;
+  uint64_t *q = (uint64_t *)(scr + 16);
+  a.bsz = q;
+  a.boff = q + e.NB;
+  a.rsz = a.boff + e.NB + 2;
+  a.roff = a.rsz + e.NR;
+  a.scan_tmp = a.roff + e.NR + 2;
+}
+
 // One batch: fast path for every document, exact engine for the documents it hands over.
 static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes, const uint64_t *d_upd_off,
                         uint64_t n_updates, const uint64_t *d_doc_upd, uint64_t n_docs, ymerge_device_result *res) {
@@ -408,7 +496,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     hipEventRecord(c->ev[7], c->s);
     hipEventRecord(c->ev[0], c->s);
     ym::launch_decode(d_bytes, d_upd_off, n_updates, c->rec.as<uint32_t>(), c->ovf.as<uint32_t>(), c->huge.as<uint32_t>(),
-                      huge_words(n_bytes), c->s);
+                      huge_words(n_bytes), c->s, lp_args(c, n_bytes, b.v1x));
     hipEventRecord(c->ev[5], c->s);
     const int rc = run_giant(c, b, fo, 0, (uint32_t)n_updates, 0, n_bytes);
     if (rc) return rc;
@@ -489,7 +577,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   const bool fast = c->fast_threads && n_rej > 0;
   if (fast) {
     ym::launch_decode(d_bytes, d_upd_off, n_updates, c->rec.as<uint32_t>(), c->ovf.as<uint32_t>(), c->huge.as<uint32_t>(),
-                      huge_words(n_bytes), c->s);
+                      huge_words(n_bytes), c->s, lp_args(c, n_bytes, b.v1x));
     hipEventRecord(c->ev[5], c->s);
     ym::launch_fast_merge(b, c->caps, fo, c->fast_threads, c->s);
     if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
@@ -516,13 +604,24 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     // long single-client documents first (ygiant.hip): listed and marked GS_PATH, merged by the
     // grid-wide kernels; the ones that are not that shape return to path 2 before k_big_count
     const bool giant = c->giant_min && n_updates >= c->giant_min && !c->want_stamps;
+    // single long update documents (one REC_LONG record, ylong.hip): listed in the same round trip
+    const bool lsg = c->long_parse && c->long_grid && !c->want_stamps;
+    constexpr size_t GSL = 1 + 6 * ym::GS_LIST, LSL = 4 + ym::LS_EW * ym::LS_LIST;
+    if (giant || lsg) {
+      if (!c->gs_list.ensure(GSL * 8) || !c->ls_list.ensure(LSL * 4)) return YMERGE_ERR_DEVICE;
+      if (giant) {
+        hipMemsetAsync(c->gs_list.p, 0, 8, c->s);
+        ym::launch_gs_find(b, path, c->giant_min, c->gs_list.as<uint64_t>(), c->s);
+        hipMemcpyAsync(c->h_pinned + 128, c->gs_list.p, GSL * 8, hipMemcpyDeviceToHost, c->s);
+      }
+      if (lsg) {
+        hipMemsetAsync(c->ls_list.p, 0, 16, c->s);
+        ym::launch_ls_find(b, path, c->ls_list.as<uint32_t>(), c->s);
+        hipMemcpyAsync(c->h_pinned + 256, c->ls_list.p, LSL * 4, hipMemcpyDeviceToHost, c->s);
+      }
+      if (hipStreamSynchronize(c->s) != hipSuccess) return dev_err("long-document listing");
+    }
     if (giant) {
-      constexpr size_t GSL = 1 + 6 * ym::GS_LIST;
-      if (!c->gs_list.ensure(GSL * 8)) return YMERGE_ERR_DEVICE;
-      hipMemsetAsync(c->gs_list.p, 0, 8, c->s);
-      ym::launch_gs_find(b, path, c->giant_min, c->gs_list.as<uint64_t>(), c->s);
-      hipMemcpyAsync(c->h_pinned + 128, c->gs_list.p, GSL * 8, hipMemcpyDeviceToHost, c->s);
-      if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
       uint64_t ent[GSL];
       memcpy(ent, c->h_pinned + 128, sizeof ent);
       const uint64_t ng = std::min<uint64_t>(ent[0], ym::GS_LIST);
@@ -531,6 +630,29 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
         const int rc = run_giant(c, b, fo, (uint32_t)e[0], (uint32_t)e[1], e[3], e[5]);
         if (rc) return rc;
       }
+    }
+    if (lsg) {
+      const std::vector<LsEntry> ls = ls_entries((const uint32_t *)(c->h_pinned + 256));
+      uint64_t words = 0;
+      for (const LsEntry &e : ls) words = std::max(words, ls_scratch_words(e));
+      if (!ls.empty() && !c->ls_scr.ensure(words * 4 + 64)) return YMERGE_ERR_DEVICE;
+      for (const LsEntry &e : ls) { // one after the other on the stream: the scratch is reused
+        ym::LsArgs a{};
+        a.bytes = b.bytes;
+        a.upd_off = b.upd_off;
+        a.ov = b.ovf + e.ovf;
+        a.mode = 0;
+        a.v1x = b.v1x;
+        a.out = fo.out;
+        a.out_start = fo.out_start;
+        a.out_len = fo.out_len;
+        a.status = fo.status;
+        a.path = fo.path;
+        a.npath = fo.npath;
+        ls_bind(a, e, c->ls_scr.as<uint32_t>());
+        ym::launch_ls_doc(a, 0, c->s);
+      }
+      if (hipGetLastError() != hipSuccess) return dev_err("long-document merge launch");
     }
     ym::launch_big_count(b, fo, c->counts.as<uint32_t>(), c->need.as<uint64_t>(), c->counter.as<uint32_t>() + 2, c->s);
     ym::launch_scan_u64(c->need.as<uint64_t>(), c->scr_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
@@ -556,14 +678,14 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     hipMemcpyAsync(c->h_pinned + 8, c->scr_off.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, c->s);
     hipMemcpyAsync(c->h_pinned + 9, c->counter.p, 4, hipMemcpyDeviceToHost, c->s);
     hipMemcpyAsync(c->h_pinned + 14, c->counter.as<uint32_t>() + 7, 12, hipMemcpyDeviceToHost, c->s);
-    hipMemcpyAsync(c->h_pinned + 17, c->counter.as<uint32_t>() + 18, 4, hipMemcpyDeviceToHost, c->s); // npath[14]
+    hipMemcpyAsync(c->h_pinned + 17, c->counter.as<uint32_t>() + 18, 8, hipMemcpyDeviceToHost, c->s); // npath[14..15]
     if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
     words = c->h_pinned[8];
     n_exact = (uint32_t)(c->h_pinned[9] & 0xFFFFFFFFu);
     n_overlap = (uint32_t)(c->h_pinned[14] & 0xFFFFFFFFu);
     n_big -= (uint32_t)(c->h_pinned[14] >> 32); // tiled-kernel documents handed to the exact engine
     n_tiny = (uint32_t)(c->h_pinned[15] & 0xFFFFFFFFu);
-    n_giant = (uint32_t)(c->h_pinned[17] & 0xFFFFFFFFu);
+    n_giant = (uint32_t)(c->h_pinned[17] & 0xFFFFFFFFu) + (uint32_t)(c->h_pinned[17] >> 32); // + long-update grid path
   }
   if (n_exact) {
     if (!c->scratch.ensure((size_t)words * 4 + 64)) return YMERGE_ERR_DEVICE;
@@ -702,6 +824,72 @@ static int plan_exec(ymerge_ctx *c, bool diff, const uint8_t *d_bytes, const uin
   }
   hipMemsetAsync(c->counter.p, 0, 64, c->s);
   hipEventRecord(c->ev[0], c->s);
+  // documents of >= ls_min_diff bytes: the parallel long-update parse, then the grid path for the
+  // single-section ones (ylong.hip); the planners skip what it takes (b.ls_done)
+  std::vector<LsEntry> ls;
+  std::vector<uint64_t> ls_off;
+  if (c->long_parse && c->long_grid && c->ls_min_diff && !c->want_stamps) {
+    if (!c->huge.ensure(16 + 8 * ym::HUGE_LIST)) return YMERGE_ERR_DEVICE;
+    hipMemsetAsync(c->huge.p, 0, 16, c->s);
+    ym::launch_ls_list_diff(d_upd_off, b.pre_status, n, c->ls_min_diff, c->huge.as<uint32_t>(), c->s);
+    hipMemcpyAsync(c->h_pinned + 9, c->huge.p, 4, hipMemcpyDeviceToHost, c->s);
+    if (hipError_t e = hipStreamSynchronize(c->s); e != hipSuccess) return dev_err("long-document listing", e);
+    if ((uint32_t)c->h_pinned[9]) {
+      constexpr uint64_t OVW = 4u << 20; // overflow words for the parsed records
+      constexpr size_t LSL = 4 + ym::LS_EW * ym::LS_LIST;
+      const ym::LpArgs *lp = lp_args(c, LP_PMAX, b.v1x);
+      if (lp && c->rec.ensure(nn * ym::REC_WORDS * 4) && c->ls_ovf.ensure(OVW * 4) && c->ls_list.ensure(LSL * 4) &&
+          c->ls_done.ensure(nn)) {
+        ym::LpArgs a = *lp;
+        a.bytes = d_bytes;
+        a.upd_off = d_upd_off;
+        a.rec = c->rec.as<uint32_t>();
+        a.ovf = c->ls_ovf.as<uint32_t>();
+        a.huge = c->huge.as<uint32_t>();
+        a.huge_base = 0;
+        a.huge_cap = OVW;
+        ym::launch_long_decode(a, c->s);
+        hipMemsetAsync(c->ls_list.p, 0, 16, c->s);
+        ym::launch_ls_collect(a, c->ls_list.as<uint32_t>(), c->s);
+        hipMemcpyAsync(c->h_pinned + 256, c->ls_list.p, LSL * 4, hipMemcpyDeviceToHost, c->s);
+        if (hipError_t e = hipStreamSynchronize(c->s); e != hipSuccess) return dev_err("long-document parse", e);
+        ls = ls_entries((const uint32_t *)(c->h_pinned + 256));
+        uint64_t words = 0;
+        for (const LsEntry &e : ls) {
+          ls_off.push_back(words);
+          words += ls_scratch_words(e);
+        }
+        if (!ls.empty() && c->ls_scr.ensure(words * 4 + 64)) {
+          hipMemsetAsync(c->ls_done.p, 0, nn, c->s);
+          b.ls_done = c->ls_done.as<uint8_t>();
+        } else {
+          ls.clear();
+        }
+      }
+      (void)hipGetLastError(); // a failed optional allocation leaves these documents to the planners
+    }
+  }
+  auto ls_args = [&](size_t k) {
+    ym::LsArgs a{};
+    a.bytes = d_bytes;
+    a.upd_off = d_upd_off;
+    a.ov = c->ls_ovf.as<uint32_t>() + ls[k].ovf;
+    a.mode = diff ? 1 : 2;
+    a.v1x = b.v1x;
+    a.frame = frame;
+    a.sv = b.sv;
+    a.sv_off = b.sv_off;
+    a.sv_end = b.sv_end;
+    a.out = c->arena.as<uint8_t>();
+    a.size = ps.size;
+    a.status = ps.status;
+    a.path = ps.big;
+    a.done = c->ls_done.as<uint8_t>();
+    a.pack_off = c->pack_off.as<uint64_t>();
+    ls_bind(a, ls[k], c->ls_scr.as<uint32_t>() + ls_off[k]);
+    return a;
+  };
+  for (size_t k = 0; k < ls.size(); k++) ym::launch_ls_doc(ls_args(k), 0, c->s);
   ym::launch_plan(diff, 0, b, ps, c->s);
   if (hipGetLastError() != hipSuccess) return dev_err("plan launch");
   hipEventRecord(c->ev[1], c->s);
@@ -724,6 +912,7 @@ static int plan_exec(ymerge_ctx *c, bool diff, const uint8_t *d_bytes, const uin
   if (!c->arena.ensure(total + 64)) return YMERGE_ERR_DEVICE;
   hipEventRecord(c->ev[4], c->s);
   ym::launch_exec(b, ps, c->pack_off.as<uint64_t>(), c->arena.as<uint8_t>(), c->s);
+  for (size_t k = 0; k < ls.size(); k++) ym::launch_ls_doc(ls_args(k), 1, c->s);
   hipEventRecord(c->ev[3], c->s);
   if (hipError_t e = hipStreamSynchronize(c->s); e != hipSuccess) return dev_err("exec", e);
   if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
