@@ -68,6 +68,9 @@ void ymerge_binary_destroy(char *ptr, uint32_t len);
 void ybinary_destroy(char *ptr, uint32_t len);
 /* error code of the last failed call on this thread (0 after a success) */
 uint8_t ymerge_last_error(void);
+/* where the last YMERGE_ERR_DEVICE on this thread came from: the failing stage and the HIP
+ * error string (empty before any device failure; valid until the next one on the thread) */
+const char *ymerge_last_error_message(void);
 /* device of the single-document calls (default: env YMERGE_DEVICE, else 0);
  * returns 0 or YMERGE_ERR_DEVICE for a device that does not exist */
 int ymerge_set_default_device(int device);

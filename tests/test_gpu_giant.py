@@ -85,3 +85,29 @@ def test_mixed_batch(forced, oracle):
         [c.doc_updates(d) for d in range(25, 50)] + [a.doc_updates(2)]
     check_batch(forced, oracle, batch_of(docs))
     assert forced.stats()["docs_giant"] == 3
+
+
+def test_single_document_fallbacks(forced, oracle):
+    """One document alone in the batch (the grid lane: k_decode, then the grid kernels) that is
+    not the grid shape -- several clients, a gap, duplicates -- must come out of the general
+    route exact (the lane's rejection used to be retried on the same document)."""
+    multi = workloads.text_docs(1, 2500, seed=34, min_clients=2, max_clients=3)
+    one = workloads.text_docs(2, 2500, seed=35, min_clients=1, max_clients=1)
+    u0, u1 = list(one.doc_updates(0)), list(one.doc_updates(1))
+    for ups in ([bytes(x) for x in multi.doc_updates(0)], u0[:1000] + u0[1010:], u1[:1200] + u1[1100:1300] + u1[1200:]):
+        check_batch(forced, oracle, batch_of([ups]))
+        assert forced.stats()["docs_giant"] == 0
+
+
+def test_high_clocks(forced, oracle):
+    """A single-client log whose clocks start near 2^32 (the recent tail of a long-lived
+    document): the deleted-clock bitmap starts at the smallest deleted clock."""
+    from test_gpu_long import section, text, update
+    c, k0 = 7777, 3_000_000_000
+    ups = []
+    for k in range(2400):
+        ups.append(update([section(c, k0 + 2 * k, [text("ab")], chained=False)]))
+        if k % 10 == 9:
+            ups.append(update([], ds=[(c, [(k0 + 2 * k - 7, 3)])]))
+    check_batch(forced, oracle, batch_of([ups]))
+    assert forced.stats()["docs_giant"] == 1

@@ -28,7 +28,8 @@ namespace ym {
 
 enum : uint32_t {
   GS_BAD = 0, GS_CMIN, GS_CMAX, GS_MAXEND, GS_FIRST = 4 /* u64 at words 4-5 */, GS_NW = 6 /* bitmap words */,
-  GS_K = 7 /* squashed ranges */, GS_WORDS = 8
+  GS_K = 7 /* squashed ranges */, GS_MINST = 8 /* smallest range start: the bitmap's base (its word) */,
+  GS_WORDS = 16
 };
 enum : uint32_t {
   GSB_SLOW = 1,      // an update k_decode did not decode (exact walk needed)
@@ -77,7 +78,7 @@ __device__ __forceinline__ uint32_t gs_visit(const GsArgs &a, uint32_t i, FB blk
 __global__ void __launch_bounds__(256) k_gs_pre(GsArgs a) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   for (uint32_t j = i; j < a.nwords; j += gridDim.x * 256) a.bm[j] = 0; // (k_gs_write sets it)
-  uint32_t nb = 0, nr = 0, bad = 0, cmin = 0xFFFFFFFFu, cmax = 0, maxend = 0;
+  uint32_t nb = 0, nr = 0, bad = 0, cmin = 0xFFFFFFFFu, cmax = 0, maxend = 0, minst = 0xFFFFFFFFu;
   uint64_t bytes = 0, lens = 0, first = ~0ull;
   if (i < a.U) bad |= gs_visit(
       a, i,
@@ -94,6 +95,7 @@ __global__ void __launch_bounds__(256) k_gs_pre(GsArgs a) {
         if (e <= s) bad |= GSB_DS;
         nr++;
         maxend = e > maxend ? e : maxend;
+        minst = s < minst ? s : minst;
         cmin = c < cmin ? c : cmin;
         cmax = c > cmax ? c : cmax;
       });
@@ -106,13 +108,15 @@ __global__ void __launch_bounds__(256) k_gs_pre(GsArgs a) {
   for (int o = 32; o > 0; o >>= 1) {
     bad |= __shfl_xor(bad, o, 64);
     const uint32_t c0 = __shfl_xor(cmin, o, 64), c1 = __shfl_xor(cmax, o, 64), m = __shfl_xor(maxend, o, 64);
+    const uint32_t ms = __shfl_xor(minst, o, 64);
     cmin = c0 < cmin ? c0 : cmin;
     cmax = c1 > cmax ? c1 : cmax;
     maxend = m > maxend ? m : maxend;
+    minst = ms < minst ? ms : minst;
     const uint64_t f = __shfl_xor(first, o, 64);
     first = f < first ? f : first;
   }
-  __shared__ uint32_t part[4][6];
+  __shared__ uint32_t part[4][7];
   const uint32_t wv = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
     part[wv][0] = bad;
@@ -121,6 +125,7 @@ __global__ void __launch_bounds__(256) k_gs_pre(GsArgs a) {
     part[wv][3] = maxend;
     part[wv][4] = (uint32_t)first;
     part[wv][5] = (uint32_t)(first >> 32);
+    part[wv][6] = minst;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -129,43 +134,48 @@ __global__ void __launch_bounds__(256) k_gs_pre(GsArgs a) {
       cmin = part[q][1] < cmin ? part[q][1] : cmin;
       cmax = part[q][2] > cmax ? part[q][2] : cmax;
       maxend = part[q][3] > maxend ? part[q][3] : maxend;
+      minst = part[q][6] < minst ? part[q][6] : minst;
       const uint64_t f = ((uint64_t)part[q][5] << 32) | part[q][4];
       first = f < first ? f : first;
     }
-    uint32_t *gp = a.gp + 6 * blockIdx.x;
+    uint32_t *gp = a.gp + 7 * blockIdx.x;
     gp[0] = bad;
     gp[1] = cmin;
     gp[2] = cmax;
     gp[3] = maxend;
     gp[4] = (uint32_t)first;
     gp[5] = (uint32_t)(first >> 32);
+    gp[6] = minst;
   }
 }
 
 // one workgroup: the k_gs_pre partials -> the document's flags / client range / max range end /
 // first block key
 __global__ void __launch_bounds__(1024) k_gs_reduce(GsArgs a, uint32_t nparts) {
-  uint32_t bad = 0, cmin = 0xFFFFFFFFu, cmax = 0, maxend = 0;
+  uint32_t bad = 0, cmin = 0xFFFFFFFFu, cmax = 0, maxend = 0, minst = 0xFFFFFFFFu;
   uint64_t first = ~0ull;
   for (uint32_t q = threadIdx.x; q < nparts; q += 1024) {
-    const uint32_t *gp = a.gp + 6 * q;
+    const uint32_t *gp = a.gp + 7 * q;
     bad |= gp[0];
     cmin = gp[1] < cmin ? gp[1] : cmin;
     cmax = gp[2] > cmax ? gp[2] : cmax;
     maxend = gp[3] > maxend ? gp[3] : maxend;
+    minst = gp[6] < minst ? gp[6] : minst;
     const uint64_t f = ((uint64_t)gp[5] << 32) | gp[4];
     first = f < first ? f : first;
   }
   for (int o = 32; o > 0; o >>= 1) {
     bad |= __shfl_xor(bad, o, 64);
     const uint32_t c0 = __shfl_xor(cmin, o, 64), c1 = __shfl_xor(cmax, o, 64), m = __shfl_xor(maxend, o, 64);
+    const uint32_t ms = __shfl_xor(minst, o, 64);
     cmin = c0 < cmin ? c0 : cmin;
     cmax = c1 > cmax ? c1 : cmax;
     maxend = m > maxend ? m : maxend;
+    minst = ms < minst ? ms : minst;
     const uint64_t f = __shfl_xor(first, o, 64);
     first = f < first ? f : first;
   }
-  __shared__ uint32_t part[16][6];
+  __shared__ uint32_t part[16][7];
   const uint32_t wv = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
     part[wv][0] = bad;
@@ -174,6 +184,7 @@ __global__ void __launch_bounds__(1024) k_gs_reduce(GsArgs a, uint32_t nparts) {
     part[wv][3] = maxend;
     part[wv][4] = (uint32_t)first;
     part[wv][5] = (uint32_t)(first >> 32);
+    part[wv][6] = minst;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -182,6 +193,7 @@ __global__ void __launch_bounds__(1024) k_gs_reduce(GsArgs a, uint32_t nparts) {
       cmin = part[q][1] < cmin ? part[q][1] : cmin;
       cmax = part[q][2] > cmax ? part[q][2] : cmax;
       maxend = part[q][3] > maxend ? part[q][3] : maxend;
+      minst = part[q][6] < minst ? part[q][6] : minst;
       const uint64_t f = ((uint64_t)part[q][5] << 32) | part[q][4];
       first = f < first ? f : first;
     }
@@ -190,6 +202,7 @@ __global__ void __launch_bounds__(1024) k_gs_reduce(GsArgs a, uint32_t nparts) {
     a.g[GS_CMAX] = cmax;
     a.g[GS_MAXEND] = maxend;
     *(uint64_t *)(a.g + GS_FIRST) = first;
+    a.g[GS_MINST] = minst == 0xFFFFFFFFu ? 0u : minst >> 5; // (word of the smallest start)
   }
 }
 
@@ -212,8 +225,11 @@ __global__ void __launch_bounds__(256) k_gs_write(GsArgs a) {
   uint8_t *dst = gs_out(a) + gs_hdr(a) + (a.s_bl[i] >> 32);
   const uint8_t *src = a.bytes + a.upd_off[a.u0 + i];
   uint32_t bad = 0;
+  // the bitmap covers clocks from the word of the smallest deleted clock on (a log whose clocks
+  // start high -- the recent tail of a long-lived document -- does not need bits below it)
+  const uint32_t base = 32 * a.g[GS_MINST];
   if (i == 0) { // bitmap words in use (the last one stays clear: run ends); over the buffer: bad
-    const uint32_t nw = a.g[GS_MAXEND] / 32 + 2;
+    const uint32_t nw = a.g[GS_MAXEND] > base ? (a.g[GS_MAXEND] - base) / 32 + 2 : 2u;
     a.g[GS_NW] = nw <= a.nwords ? nw : 0;
     if (nw > a.nwords) bad |= GSB_RANGE;
   }
@@ -227,10 +243,12 @@ __global__ void __launch_bounds__(256) k_gs_write(GsArgs a) {
         dst += n;
       },
       [&](uint32_t, uint32_t s, uint32_t e) {
-        if (e > a.nbits) {
+        if (e - base > a.nbits) {
           bad |= GSB_RANGE;
           return;
         }
+        s -= base;
+        e -= base;
         // bits [s, e): the partial end words and the whole words between them
         const uint32_t w0 = s >> 5, w1 = (e - 1) >> 5;
         const uint32_t m0 = 0xFFFFFFFFu << (s & 31), m1 = 0xFFFFFFFFu >> (31 - ((e - 1) & 31));
@@ -281,12 +299,13 @@ __global__ void __launch_bounds__(256) k_gs_comp(GsArgs a) {
     uint32_t ks = (uint32_t)sc, ke = (uint32_t)(sc >> 32);
     uint32_t st = gs_starts(a, j), en = gs_ends(a, j);
     if (ks + __popc(st) > a.kcap || ke + __popc(en) > a.kcap) continue; // (then the document is bad)
+    const uint32_t base = 32 * a.g[GS_MINST];
     while (st) {
-      a.k_start[ks++] = 32 * j + __builtin_ctz(st);
+      a.k_start[ks++] = base + 32 * j + __builtin_ctz(st);
       st &= st - 1;
     }
     while (en) {
-      a.k_len[ke++] = 32 * j + __builtin_ctz(en) + 1; // end (exclusive) for now: k_gs_size subtracts
+      a.k_len[ke++] = base + 32 * j + __builtin_ctz(en) + 1; // end (exclusive) for now: k_gs_size subtracts
       en &= en - 1;
     }
   }

@@ -52,10 +52,32 @@ struct LpRd {
     }
     return g[q];
   }
+  // the 8 stream bytes from q (q - s0 + 8 <= se - s0): three dword reads and a funnel shift
+  YM_INLINE uint64_t win8(uint32_t q) const {
+    const uint32_t o = q - s0 + sh, i = o >> 2, b = (o & 3) * 8;
+    const uint64_t d = ((uint64_t)w[i + 1] << 32) | w[i];
+    return b ? (d >> b) | ((uint64_t)w[i + 2] << (64 - b)) : d;
+  }
 };
 
-// read_var_u32 (varint.rs:244-260) at q; false = not decodable (EOS / E_VARINT)
+// read_var_u32 (varint.rs:244-260) at q; false = not decodable (EOS / E_VARINT).  Inside the
+// stage: one 8-byte window, the terminator by ctz over the continuation bits (<= 8 bytes)
 YM_INLINE bool lp_var(const LpRd &r, uint32_t &q, uint32_t L, uint32_t &v) {
+  if (q - r.s0 < r.se - r.s0 && r.se - q >= 8) {
+    const uint64_t d = r.win8(q);
+    const uint64_t stop = ~d & 0x8080808080808080ull;
+    if (stop) {
+      const uint32_t n = ((uint32_t)__builtin_ctzll(stop) >> 3) + 1;
+      if (n > L - q) return false;
+      uint32_t x = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < 8; k++)
+        if (k < n) x |= ((uint32_t)(d >> (8 * k)) & 0x7Fu) << ((7 * k) & 31);
+      v = x;
+      q += n;
+      return true;
+    }
+  }
   uint32_t x = 0, sh = 0;
   for (;;) {
     if (q >= L) return false;
@@ -180,9 +202,12 @@ __device__ __forceinline__ void lp_fail(const LpArgs &a, uint32_t k) { atomicOr(
 // map; updates that do not fit the scratch (or are >= 1 GiB) go to the exact walker.
 __global__ void __launch_bounds__(1024) k_lp_plan(LpArgs a) {
   __shared__ uint64_t ws[1024 / 64 + 1];
+  __shared__ uint32_t s_nch;
   const uint32_t n = a.huge[0] < HUGE_LIST ? a.huge[0] : HUGE_LIST;
   const uint64_t *list = (const uint64_t *)(a.huge + 4);
   uint64_t cbase = 0, pbase = 0;
+  if (threadIdx.x == 0) s_nch = 0;
+  __syncthreads();
   for (uint32_t k0 = 0; k0 < n; k0 += 1024) {
     const uint32_t k = k0 + threadIdx.x;
     uint64_t L = 0, ch = 0;
@@ -206,14 +231,17 @@ __global__ void __launch_bounds__(1024) k_lp_plan(LpArgs a) {
       m[LPM_NCH] = fits ? (uint32_t)ch : 0u;
       m[LPM_PB] = (uint32_t)pb;
       m[LPM_FLAGS] = fits ? 0u : LPF_FALLBACK;
-      if (fits)
+      if (fits) { // (the updates that fit are a prefix of the list: the bases only grow)
         for (uint32_t c = 0; c < ch; c++) a.c2e[cb + c] = k;
+        atomicMax(&s_nch, (uint32_t)(cb + ch));
+      }
     }
     pbase += TL;
     cbase += TC;
   }
+  __syncthreads();
   if (threadIdx.x == 0) {
-    a.g[LPG_CHUNKS] = (uint32_t)(cbase < a.ccap ? cbase : a.ccap);
+    a.g[LPG_CHUNKS] = s_nch; // chunks of the updates that fit (every c2e entry below is written)
     a.g[LPG_SEGS] = 0;
     a.g[LPG_ORDS] = 0;
     a.g[LPG_SECS] = 0;
@@ -223,13 +251,48 @@ __global__ void __launch_bounds__(1024) k_lp_plan(LpArgs a) {
   }
 }
 
+// ------------------------------------------------------------------ k_lp_ext
+// workgroup per LP_EXT positions of a chunk (the whole GPU busy even for one update): the bytes
+// staged in LDS with a look-ahead, every position parsed speculatively
+constexpr uint32_t LPE_NT = 256, LP_EXT = 1024, LPE_LA = 512, LPE_PER = LP_EXT / LPE_NT;
+constexpr uint32_t LPE_STAGE_W = (LP_EXT + LPE_LA) / 4 + 4;
+__global__ void __launch_bounds__(LPE_NT) k_lp_ext(LpArgs a) {
+  __shared__ __align__(16) uint32_t stage[LPE_STAGE_W];
+  __shared__ uint32_t s_k;
+  const uint32_t t = threadIdx.x, ntile = a.g[LPG_CHUNKS] * (LP_CH / LP_EXT);
+  for (uint32_t tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
+    const uint32_t c = tile / (LP_CH / LP_EXT);
+    __syncthreads();
+    if (t == 0) s_k = a.c2e[c];
+    __syncthreads();
+    const uint32_t *m = lp_meta(a, s_k);
+    const uint64_t u = m[LPM_U] | ((uint64_t)m[LPM_U + 1] << 32);
+    const uint32_t L = m[LPM_L], pb = m[LPM_PB];
+    const uint32_t ts = (c - m[LPM_CB]) * LP_CH + (tile % (LP_CH / LP_EXT)) * LP_EXT;
+    if (ts >= L) continue; // (uniform) past the update's end in its last chunk
+    const uint32_t te = ts + LP_EXT < L ? ts + LP_EXT : L;
+    const uint8_t *ub = a.bytes + a.upd_off[u];
+    const uint64_t abs0 = (uint64_t)(ub + ts);
+    const uint32_t sh = (uint32_t)(abs0 & 3);
+    const uint32_t se = ts + LP_EXT + LPE_LA < L ? ts + LP_EXT + LPE_LA : L;
+    const uint32_t nw = (se - ts + sh + 3) >> 2;
+    const uint32_t *src = (const uint32_t *)(abs0 - sh);
+    for (uint32_t q = t; q < nw; q += LPE_NT) stage[q] = src[q]; // (the arena is padded: +16 B)
+    __syncthreads();
+    LpRd r{(const lp_lds_u32 *)stage, ts, se, sh, ub};
+#pragma unroll 1
+    for (uint32_t j = 0; j < LPE_PER; j++) {
+      const uint32_t p = ts + t + j * LPE_NT;
+      if (p < te) a.ext[(size_t)pb + p] = lp_spec(r, p, L);
+    }
+  }
+}
+
 // ------------------------------------------------------------------ k_lp_chunk
-// LDS: stage (chunk + look-ahead bytes) + two (jump, count) tables for the doubling
-constexpr uint32_t LP_NT = 1024, LP_LA = 1024, LP_PER = LP_CH / LP_NT;
-constexpr uint32_t LP_STAGE_W = (LP_CH + LP_LA) / 4 + 4;
+// workgroup per chunk: two (jump, count) tables in LDS for the doubling
+constexpr uint32_t LP_NT = 1024, LP_PER = LP_CH / LP_NT;
 
 __global__ void __launch_bounds__(LP_NT) k_lp_chunk(LpArgs a) {
-  __shared__ __align__(16) uint32_t stage[LP_STAGE_W];
   __shared__ uint64_t jc0[LP_CH], jc1[LP_CH];
   __shared__ uint32_t s_k;
   const uint32_t t = threadIdx.x, nch = a.g[LPG_CHUNKS];
@@ -239,26 +302,14 @@ __global__ void __launch_bounds__(LP_NT) k_lp_chunk(LpArgs a) {
     __syncthreads();
     const uint32_t k = s_k;
     const uint32_t *m = lp_meta(a, k);
-    const uint64_t u = m[LPM_U] | ((uint64_t)m[LPM_U + 1] << 32);
     const uint32_t L = m[LPM_L], pb = m[LPM_PB];
     const uint32_t cs = (c - m[LPM_CB]) * LP_CH, ce = cs + LP_CH < L ? cs + LP_CH : L;
-    const uint8_t *ub = a.bytes + a.upd_off[u];
-    // stage [cs, min(cs + CH + LA, L)) as dwords from the aligned address at or below
-    const uint64_t abs0 = (uint64_t)(ub + cs);
-    const uint32_t sh = (uint32_t)(abs0 & 3);
-    const uint32_t se = cs + LP_CH + LP_LA < L ? cs + LP_CH + LP_LA : L;
-    const uint32_t nw = (se - cs + sh + 3) >> 2;
-    const uint32_t *src = (const uint32_t *)(abs0 - sh);
-    for (uint32_t q = t; q < nw; q += LP_NT) stage[q] = src[q]; // (the arena is padded: +16 B)
-    __syncthreads();
-    LpRd r{(const lp_lds_u32 *)stage, cs, se, sh, ub};
     const uint32_t cn = ce - cs;
     for (uint32_t j = 0; j < LP_PER; j++) {
       const uint32_t i = t + j * LP_NT;
       if (i >= cn) break;
       const uint32_t p = cs + i;
-      const uint32_t e = lp_spec(r, p, L);
-      a.ext[(size_t)pb + p] = e;
+      const uint32_t e = a.ext[(size_t)pb + p];
       uint64_t x;
       if (e >= LP_COLD) x = p; // terminal: BAD / COLD block start (self loop, no blocks)
       else x = (uint64_t)(e & LP_OFF) | ((uint64_t)(1u | ((e & LP_UNST) ? 0u : 0x10000u)) << 32);
@@ -341,6 +392,7 @@ __global__ void __launch_bounds__(64) k_lp_stitch(LpArgs a) {
         while (r) {
           if (E >= L) return false;
           const uint32_t x = a.ext[(size_t)pb + E];
+          const uint64_t y = a.jc[(size_t)pb + E]; // (issued with the ext load: one round trip a hop)
           if (x == LP_BAD) return false;
           if (x == LP_COLD) { // exact parse of this one block
             Cur cc{ub, L, E};
@@ -353,7 +405,6 @@ __global__ void __launch_bounds__(64) k_lp_stitch(LpArgs a) {
             r--;
             continue;
           }
-          const uint64_t y = a.jc[(size_t)pb + E];
           const uint32_t h = (uint32_t)(y >> 32) & 0xFFFF, hs = (uint32_t)(y >> 48);
           if (h <= r) {
             if (!lp_seg(a, k, E, h, sb + s, ord, st)) return false;
@@ -400,9 +451,11 @@ __global__ void __launch_bounds__(64) k_lp_stitch(LpArgs a) {
 
 // ------------------------------------------------------------------ k_lp_expand
 constexpr uint32_t LPX_NT = 256;
+constexpr uint32_t LPX_LA = 1024, LPX_STAGE_W = (LP_CH + LPX_LA) / 4 + 4;
 __global__ void __launch_bounds__(LPX_NT) k_lp_expand(LpArgs a) {
   __shared__ uint32_t extl[LP_CH];
   __shared__ uint32_t pos[LP_CH / 2 + 1];
+  __shared__ __align__(16) uint32_t stage[LPX_STAGE_W]; // the chunk's bytes (+ look-ahead)
   __shared__ uint32_t ws[LPX_NT / 64 + 1];
   __shared__ uint32_t s_flags;
   ym_set_grammar(a.v1x);
@@ -418,12 +471,25 @@ __global__ void __launch_bounds__(LPX_NT) k_lp_expand(LpArgs a) {
     __syncthreads();
     if (s_flags & LPF_FALLBACK) continue;
     const uint64_t u = m[LPM_U] | ((uint64_t)m[LPM_U + 1] << 32);
-    const uint32_t L = m[LPM_L], pb = m[LPM_PB], ovb = m[LPM_OVF], ob = m[LPM_OB];
+    const uint32_t L = m[LPM_L], pb = m[LPM_PB], ovb = m[LPM_OVF], ob = m[LPM_OB], nbs = m[LPM_NB];
     const uint32_t client = a.sec[(size_t)sec * 4];
     const uint8_t *ub = a.bytes + a.upd_off[u];
     const uint32_t cs = E - E % LP_CH, cn = (cs + LP_CH < L ? cs + LP_CH : L) - cs;
     __syncthreads();
     for (uint32_t i = t; i < cn; i += LPX_NT) extl[i] = a.ext[(size_t)pb + cs + i];
+    // the chunk's bytes: blocks that end inside the stage are parsed from LDS (the exact parse
+    // reads byte by byte: dependent global loads otherwise)
+    const uint64_t abs0 = (uint64_t)(ub + cs);
+    const uint32_t sh = (uint32_t)(abs0 & 3);
+    const uint32_t se = cs + LP_CH + LPX_LA < L ? cs + LP_CH + LPX_LA : L;
+    {
+      const uint32_t nw = (se - cs + sh + 3) >> 2;
+      const uint32_t *src = (const uint32_t *)(abs0 - sh);
+      for (uint32_t q = t; q < nw; q += LPX_NT) stage[q] = src[q];
+    }
+    // lb[q - cs] = update byte q for q in [cs, se); positions are passed relative to cs (a
+    // pointer below the LDS array would leave the LDS aperture once cast to a flat address)
+    const uint8_t *lb = (const uint8_t *)stage + sh;
     if (t == 0) s_flags = 0;
     __syncthreads();
     if (t == 0) { // the segment's block starts: hops inside the chunk (nb <= CH / 2)
@@ -443,11 +509,13 @@ __global__ void __launch_bounds__(LPX_NT) k_lp_expand(LpArgs a) {
       uint32_t p = 0, end = 0;
       if (i < nb) {
         p = pos[i];
-        Cur cc{ub, L, p};
+        const uint32_t x0 = extl[p - cs];
+        const bool in_lds = x0 < LP_COLD && (x0 & LP_OFF) <= se;
+        Cur cc = in_lds ? Cur{lb, L - cs, p - cs} : Cur{ub, L, p};
         if (parse_block(cc, bi)) {
           flags |= LPF_FALLBACK;
         } else {
-          end = cc.i;
+          end = cc.i + (in_lds ? cs : 0u);
           stored = !(bi.kind == BK_SKIP || (bi.kind == BK_ITEM && bi.len == 0));
           const uint32_t x = extl[p - cs];
           if (x != LP_COLD && (x == LP_BAD || (x & LP_OFF) != end || !(x & LP_UNST) != stored))
@@ -464,7 +532,7 @@ __global__ void __launch_bounds__(LPX_NT) k_lp_expand(LpArgs a) {
       const uint32_t pre = bscan_sum<LPX_NT>(stored ? 1u : 0u, ws, tot);
       if (i < nb) {
         const size_t og = (size_t)ob + ord0 + i;
-        if (stored) {
+        if (stored && stc + pre < nbs) { // (bound: cannot fail when the two parses agree)
           const uint32_t at = ovb + 5 * (stc + pre);
           uint32_t *w = a.ovf + at;
           w[0] = client;
@@ -536,6 +604,7 @@ __global__ void __launch_bounds__(LPD_NT) k_lp_ds(LpArgs a) {
   __shared__ uint32_t ws[LPD_NT / 64 + 1];
   __shared__ uint32_t s_hdr[4]; // ok, nr, pos
   __shared__ uint32_t s_fail, s_cl[DS_SMALL], s_code[DS_SMALL];
+  __shared__ uint32_t tileb[LPD_NT * LPD_B / 4 + 4];
   const uint32_t t = threadIdx.x, n = a.g[LPG_N];
   for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
     uint32_t *m = lp_meta(a, k);
@@ -581,11 +650,21 @@ __global__ void __launch_bounds__(LPD_NT) k_lp_ds(LpArgs a) {
       const uint32_t nr = s_hdr[1];
       uint32_t q0 = s_hdr[2], done = 0; // varints decoded of this entry's 2 * nr
       while (done < 2 * nr) {
-        // tile [q0, q0 + LPD_NT * LPD_B): lane t looks at bytes q0 + t * B .. + B
+        // tile [q0, q0 + LPD_NT * LPD_B) staged in LDS: lane t looks at bytes q0 + t * B .. + B
+        const uint32_t te = q0 + LPD_NT * LPD_B < L ? q0 + LPD_NT * LPD_B : L;
+        const uint64_t abs0 = (uint64_t)(ub + q0);
+        const uint32_t sh = (uint32_t)(abs0 & 3), nw = (te - q0 + sh + 3) >> 2;
+        __syncthreads();
+        for (uint32_t q = t; q < nw; q += LPD_NT) tileb[q] = ((const uint32_t *)(abs0 - sh))[q];
+        __syncthreads();
+        auto tb = [&](uint32_t q) -> uint32_t { // update byte q in [q0, te)
+          const uint32_t o = q - q0 + sh;
+          return (tileb[o >> 2] >> ((o & 3) * 8)) & 0xFF;
+        };
         const uint32_t b0 = q0 + t * LPD_B;
         uint32_t tm = 0; // terminator mask of my bytes
         for (uint32_t j = 0; j < LPD_B; j++)
-          if (b0 + j < L && ub[b0 + j] < 0x80) tm |= 1u << j;
+          if (b0 + j < te && tb(b0 + j) < 0x80) tm |= 1u << j;
         uint32_t tot;
         const uint32_t pre = bscan_sum<LPD_NT>(__popc(tm), ws, tot);
         if (tot == 0) { // no terminator in the tile: EOS or an over-long varint
@@ -595,20 +674,32 @@ __global__ void __launch_bounds__(LPD_NT) k_lp_ds(LpArgs a) {
         }
         const uint32_t need = 2 * nr - done, take = tot < need ? tot : need;
         uint32_t lastend = 0;
-        // varint j (0-based within the tile) starts after terminator j - 1 (or at q0)
+        // varint j (0-based within the tile) starts after terminator j - 1 (or at q0); the
+        // ones taken end inside the tile
         for (uint32_t j = 0; j < LPD_B; j++) {
-          if (b0 + j >= L) break;
-          const bool starts = (b0 + j == q0) || (j ? (tm >> (j - 1)) & 1 : (b0 > q0 && ub[b0 - 1] < 0x80));
+          if (b0 + j >= te) break;
+          const bool starts = (b0 + j == q0) || (j ? (tm >> (j - 1)) & 1 : (b0 > q0 && tb(b0 - 1) < 0x80));
           const uint32_t ordv = pre + __popc(tm & ((1u << j) - 1)); // terminators before this byte
           if (starts && ordv < take) {
-            uint32_t v;
-            if (!lp_dvar(ub, L, b0 + j, v)) {
+            uint32_t x = 0, shv = 0, q = b0 + j;
+            bool ok = true;
+            for (;;) { // read_var_u32 (varint.rs:244-260)
+              const uint32_t byte = tb(q++);
+              x |= (byte & 0x7f) << (shv & 31);
+              shv += 7;
+              if (byte < 0x80) break;
+              if (shv > 70) {
+                ok = false;
+                break;
+              }
+            }
+            if (!ok) {
               s_fail = 1;
             } else if (!big) {
               const uint32_t gi = done + ordv, kr = rtot + gi / 2;
-              if (gi & 1) rw[3 * kr + 1] = v; // length (start + length below)
+              if (gi & 1) rw[3 * kr + 1] = x; // length (start + length below)
               else {
-                rw[3 * kr] = v;
+                rw[3 * kr] = x;
                 rw[3 * kr + 2] = e;
               }
             }
@@ -710,6 +801,7 @@ __global__ void __launch_bounds__(256) k_lp_final(LpArgs a) {
 void launch_long_decode(const LpArgs &a, hipStream_t s) {
   hipLaunchKernelGGL(k_lp_plan, dim3(1), dim3(1024), 0, s, a);
   const uint32_t gch = a.ccap < 1024 ? a.ccap : 1024;
+  hipLaunchKernelGGL(k_lp_ext, dim3(2048), dim3(LPE_NT), 0, s, a);
   hipLaunchKernelGGL(k_lp_chunk, dim3(gch ? gch : 1), dim3(LP_NT), 0, s, a);
   hipLaunchKernelGGL(k_lp_stitch, dim3(256), dim3(64), 0, s, a);
   hipLaunchKernelGGL(k_lp_expand, dim3(1024), dim3(LPX_NT), 0, s, a);
@@ -862,8 +954,31 @@ __global__ void k_ls_prep(LsArgs a) {
   g[LSG_HDR] = k0 < NB ? varlen(1) + varlen(NB - k0) + varlen(client) + varlen(g[LSG_CLOCK]) : 1u;
 }
 
+// The bytes of blocks [i0, i0 + 256) (consecutive in the update: one section) staged in LDS, at
+// most LS_STAGE of them; returns the pointer p with p[q - s0] = update byte q for q in [s0, s1)
+// (positions are passed relative to s0: a pointer below the LDS array would leave the LDS
+// aperture once cast to a flat address)
+constexpr uint32_t LS_STAGE = 16384;
+__device__ __forceinline__ const uint8_t *ls_stage(const LsArgs &a, const uint8_t *ub, uint32_t i0, uint32_t *stage,
+                                                   uint32_t &s0, uint32_t &s1) {
+  s0 = s1 = 0;
+  if (i0 >= a.NB) return ub;
+  const uint32_t last = i0 + 255 < a.NB ? i0 + 255 : a.NB - 1;
+  s0 = a.ov[5 * i0 + 3];
+  s1 = a.ov[5 * last + 3] + (a.ov[5 * last + 4] >> 8);
+  if (s1 - s0 > LS_STAGE) s1 = s0 + LS_STAGE;
+  const uint64_t abs0 = (uint64_t)(ub + s0);
+  const uint32_t sh = (uint32_t)(abs0 & 3), nw = (s1 - s0 + sh + 3) >> 2;
+  const uint32_t *src = (const uint32_t *)(abs0 - sh);
+  __syncthreads();
+  for (uint32_t q = threadIdx.x; q < nw; q += 256) stage[q] = src[q];
+  __syncthreads();
+  return (const uint8_t *)stage + sh; // p[q - s0] = update byte q
+}
+
 // lane per block and per range: sizes and checks
 __global__ void __launch_bounds__(256) k_ls_size(LsArgs a) {
+  __shared__ __align__(16) uint32_t stage[LS_STAGE / 4 + 4];
   ym_set_grammar(a.v1x);
   uint32_t *g = a.g;
   const uint32_t n = a.NB > a.NR ? a.NB : a.NR;
@@ -871,18 +986,24 @@ __global__ void __launch_bounds__(256) k_ls_size(LsArgs a) {
   const uint32_t *rv = ls_rv(a);
   const uint8_t *ub = ls_ub(a);
   uint32_t bad = 0, runs = 0;
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+  for (uint32_t i0 = blockIdx.x * 256; i0 < n; i0 += gridDim.x * 256) {
+    const uint32_t i = i0 + threadIdx.x;
+    uint32_t s0, s1;
+    const uint8_t *lb = a.mode == 2 ? ub : ls_stage(a, ub, i0, stage, s0, s1);
     if (i < a.NB) {
       const uint32_t *r = a.ov + 5 * i;
+      const bool in_lds = r[3] >= s0 && r[3] + (r[4] >> 8) <= s1;
+      const uint8_t *bp = in_lds ? lb : ub;
+      const uint32_t bn = in_lds ? a.L - s0 : a.L, bq = in_lds ? r[3] - s0 : r[3];
       uint64_t sz = 0;
       if (a.mode == 1 && i < k0) {
         sz = 0;
       } else if (a.mode == 1 && i == k0 && off) {
         Counter cn;
-        if (emit_block(ub, a.L, r[3], r[0], r[1], r[2], off, cn)) bad = 1;
+        if (emit_block(bp, bn, bq, r[0], r[1], r[2], off, cn)) bad = 1;
         sz = cn.n;
       } else {
-        sz = canon_size(ub, a.L, r[3], r[0], r[1], r[2], r[4]);
+        sz = canon_size(bp, bn, bq, r[0], r[1], r[2], r[4]);
       }
       a.bsz[i] = sz;
     }
@@ -951,6 +1072,7 @@ __global__ void k_ls_total(LsArgs a) {
 }
 
 __global__ void __launch_bounds__(256) k_ls_write(LsArgs a) {
+  __shared__ __align__(16) uint32_t stage[LS_STAGE / 4 + 4];
   ym_set_grammar(a.v1x);
   const uint32_t *g = a.g;
   if (g[LSG_BAD]) return;
@@ -998,15 +1120,21 @@ __global__ void __launch_bounds__(256) k_ls_write(LsArgs a) {
   uint8_t *blocks = base + g[LSG_HDR];
   uint8_t *ds = blocks + a.boff[a.NB] +
                 (a.NE == 0 ? 1 : varlen(1) + varlen(a.ov[5 * a.NB]) + varlen(a.mode == 0 ? g[LSG_K] : a.NR));
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+  for (uint32_t i0 = blockIdx.x * 256; i0 < n; i0 += gridDim.x * 256) {
+    const uint32_t i = i0 + threadIdx.x;
+    uint32_t s0, s1;
+    const uint8_t *lb = ls_stage(a, ub, i0, stage, s0, s1);
     if (i < a.NB && i >= k0) {
       const uint32_t *r = a.ov + 5 * i;
+      const bool in_lds = r[3] >= s0 && r[3] + (r[4] >> 8) <= s1;
+      const uint8_t *bp = in_lds ? lb : ub;
+      const uint32_t bn = in_lds ? a.L - s0 : a.L, bq = in_lds ? r[3] - s0 : r[3];
       Writer w{blocks + a.boff[i], 0};
       const uint32_t o = i == k0 ? off : 0u;
       if (o || ((r[4] & 4) && !(r[4] & 8))) {
-        emit_block(ub, a.L, r[3], r[0], r[1], r[2], o, w);
+        emit_block(bp, bn, bq, r[0], r[1], r[2], o, w);
       } else {
-        const uint8_t *src = ub + r[3];
+        const uint8_t *src = bp + bq;
         const uint32_t nb = r[4] >> 8;
         for (uint32_t q = 0; q < nb; q++) w.p[q] = src[q];
       }

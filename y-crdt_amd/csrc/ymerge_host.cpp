@@ -47,15 +47,21 @@ struct DevBuf {
 };
 
 thread_local uint8_t g_last_error = 0;
-// YMERGE_ERR_DEVICE with the HIP error named on stderr when env YMERGE_VERBOSE is set
+// Provenance of the last YMERGE_ERR_DEVICE on this thread: the failing stage (file:line or a
+// name) and the HIP error, kept until the next device failure (ymerge_last_error_message);
+// also printed to stderr when env YMERGE_VERBOSE is set.
+thread_local char g_last_msg[256] = "";
 int dev_err(const char *where, hipError_t e = hipSuccess) {
   static const bool verbose = getenv("YMERGE_VERBOSE") != nullptr;
-  if (verbose) {
-    if (e == hipSuccess) e = hipPeekAtLastError();
-    fprintf(stderr, "ymerge: device error at %s: %s\n", where, hipGetErrorString(e));
-  }
+  if (e == hipSuccess) e = hipPeekAtLastError();
+  snprintf(g_last_msg, sizeof g_last_msg, "device error at %s: %s (%d)", where,
+           e == hipSuccess ? "allocation or bound" : hipGetErrorString(e), (int)e);
+  if (verbose) fprintf(stderr, "ymerge: %s\n", g_last_msg);
   return YMERGE_ERR_DEVICE;
 }
+#define YM_STR2(x) #x
+#define YM_STR(x) YM_STR2(x)
+#define DEV_FAIL() dev_err("ymerge_host.cpp:" YM_STR(__LINE__))
 ymerge_batch_result *alloc_result(uint64_t n_docs, uint64_t out_bytes);
 
 } // namespace
@@ -380,17 +386,17 @@ static int run_giant(ymerge_ctx *c, const ym::BatchIn &b, const ym::FastOut &fo,
   a.kcap = (uint32_t)std::min<uint64_t>(nwc * 16, doc_bytes / 2 + 2);
   const size_t nw = a.nwords, kc = (size_t)a.kcap + 2;
   const size_t nparts = ((size_t)U + 255) / 256;
-  if (!c->gs1.ensure((4 * nu + 4) * 8 + nparts * 24 + 64) ||
+  if (!c->gs1.ensure((4 * nu + 8) * 8 + nparts * 28 + 64) ||
       !c->scan_tmp.ensure(ym::scan_tmp_elems((uint32_t)std::max<size_t>(std::max<size_t>(nu, nw), kc)) * 8 + 64) ||
       !c->gs2.ensure(nw * 4 + (2 * nw + 1) * 8 + 2 * kc * 4 + 2 * kc * 8 + 64))
-    return YMERGE_ERR_DEVICE;
+    return DEV_FAIL();
   uint64_t *w = c->gs1.as<uint64_t>();
   a.cnt = w;
   a.bl = w + nu;
   a.s_cnt = w + 2 * nu;
   a.s_bl = w + 3 * nu;
   a.g = (uint32_t *)(w + 4 * nu);
-  a.gp = a.g + 8;
+  a.gp = a.g + 16; // (GS_WORDS)
   uint8_t *q = c->gs2.as<uint8_t>();
   a.w_cnt = (uint64_t *)q;
   a.w_scan = a.w_cnt + nw;
@@ -404,7 +410,7 @@ static int run_giant(ymerge_ctx *c, const ym::BatchIn &b, const ym::FastOut &fo,
   ym::launch_scan_u64(a.cnt, a.s_cnt, U, c->scan_tmp.as<uint64_t>(), c->s);
   ym::launch_scan_u64(a.bl, a.s_bl, U, c->scan_tmp.as<uint64_t>(), c->s);
   ym::launch_gs_rest(a, fo, c->scan_tmp.as<uint64_t>(), c->s);
-  return hipGetLastError() == hipSuccess ? 0 : YMERGE_ERR_DEVICE;
+  return hipGetLastError() == hipSuccess ? 0 : DEV_FAIL();
 }
 
 // Single long update documents (ylong.hip): list entries read back from the device (LS_EW words:
@@ -446,7 +452,7 @@ static void ls_bind(ym::LsArgs &a, const LsEntry &e, uint32_t *scr) {
 static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes, const uint64_t *d_upd_off,
                         uint64_t n_updates, const uint64_t *d_doc_upd, uint64_t n_docs, ymerge_device_result *res) {
   resolve_times(c);
-  if (hipSetDevice(c->device) != hipSuccess) return YMERGE_ERR_DEVICE;
+  if (hipSetDevice(c->device) != hipSuccess) return DEV_FAIL();
   if (n_docs > 0xFFFFFFFFull) return YMERGE_ERR_OTHER;
   const uint32_t n = (uint32_t)n_docs;
   ym::BatchIn b{d_bytes, d_upd_off, d_doc_upd, n, nullptr, nullptr};
@@ -462,7 +468,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
                            !c->ovf.ensure(((n_updates + ym::DEC_NT - 1) / ym::DEC_NT + 1) * ym::DEC_OVF * 4 +
                                           (uint64_t)huge_words(n_bytes) * 4) ||
                            !c->huge.ensure(16 + 8 * ym::HUGE_LIST))))
-    return YMERGE_ERR_DEVICE;
+    return DEV_FAIL();
   b.rec = c->rec.as<uint32_t>();
   b.ovf = c->ovf.as<uint32_t>();
   uint8_t *arena = c->arena.as<uint8_t>();
@@ -472,7 +478,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   hipMemsetAsync(c->counter.p, 0, 128 + 64 * 64, c->s);
   uint64_t *stamps = nullptr;
   if (c->want_stamps) {
-    if (!c->stamps.ensure(nn * 16 * 8)) return YMERGE_ERR_DEVICE;
+    if (!c->stamps.ensure(nn * 16 * 8)) return DEV_FAIL();
     hipMemsetAsync(c->stamps.p, 0, nn * 16 * 8, c->s);
     stamps = c->stamps.as<uint64_t>();
     c->stamps_docs = n_docs;
@@ -490,7 +496,9 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   // One long document alone in the batch (C1: an editing trace as per-op updates): k_decode,
   // then the grid-wide kernels, with one host round trip at the end instead of the hand-over
   // reads of k_lean, k_fast_merge and the listing.  Not that shape: the batch takes the
-  // general route below (which recomputes everything).
+  // general route below, which keeps the records and does not list the document for the grid
+  // path again (that second attempt failed the same way).
+  bool decoded = false, giant_rejected = false;
   if (n == 1 && c->giant_min && n_updates >= c->giant_min && n_updates < (1ull << 31) && c->fast_threads &&
       !c->want_stamps && c->giant_lane) {
     hipEventRecord(c->ev[7], c->s);
@@ -498,12 +506,13 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     ym::launch_decode(d_bytes, d_upd_off, n_updates, c->rec.as<uint32_t>(), c->ovf.as<uint32_t>(), c->huge.as<uint32_t>(),
                       huge_words(n_bytes), c->s, lp_args(c, n_bytes, b.v1x));
     hipEventRecord(c->ev[5], c->s);
+    decoded = true;
     const int rc = run_giant(c, b, fo, 0, (uint32_t)n_updates, 0, n_bytes);
     if (rc) return rc;
     hipEventRecord(c->ev[1], c->s);
     hipMemcpyAsync(c->h_pinned + 20, path, 1, hipMemcpyDeviceToHost, c->s);
     hipMemcpyAsync(c->h_pinned + 21, olen, 8, hipMemcpyDeviceToHost, c->s);
-    if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
+    if (hipStreamSynchronize(c->s) != hipSuccess) return DEV_FAIL();
     if ((c->h_pinned[20] & 0xFF) == 0) {
       float t05 = 0, t51 = 0, t71 = 0;
       hipEventElapsedTime(&t05, c->ev[0], c->ev[5]);
@@ -527,6 +536,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
       res->out_bytes = c->h_pinned[21];
       return 0;
     }
+    giant_rejected = true; // k_gs_final left it on path 2: the general route takes it
   }
   hipEventRecord(c->ev[7], c->s);
   if (lean) {
@@ -544,18 +554,18 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     // (batches of many small documents: Zipf-like tenants, where one long document would
     // otherwise end the kernel; also the ~48 MB groups of the pipelined host entry)
     if (c->lean_order == 1 || (c->lean_order < 0 && n >= 8192 && n_updates < 256ull * n)) {
-      if (!c->lean_ord.ensure((size_t)n * 4 + 64)) return YMERGE_ERR_DEVICE;
+      if (!c->lean_ord.ensure((size_t)n * 4 + 64)) return DEV_FAIL();
       hipMemsetAsync(c->lean_ord.p, 0, 64, c->s); // class counts and cursors (<= 16 words)
       ym::launch_lean_order(d_doc_upd, n, c->lean_ord.as<uint32_t>(), c->lean_ord.as<uint32_t>() + 16, c->s);
       bl.order = c->lean_ord.as<uint32_t>() + 16;
     }
     ym::launch_lean(bl, fo, lscr, c->s);
-    if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
+    if (hipGetLastError() != hipSuccess) return DEV_FAIL();
     // hand-over count and k_lean's output bytes (npath[6] at counter byte 40, the 64 partial
     // sums from byte 128) in one copy and one sync: byte 128 lands on h_pinned[512]
     hipMemcpyAsync((uint8_t *)(c->h_pinned + 512) - 88, c->counter.as<uint8_t>() + 40, 88 + 64 * 64,
                    hipMemcpyDeviceToHost, c->s);
-    if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
+    if (hipStreamSynchronize(c->s) != hipSuccess) return DEV_FAIL();
     n_rej = (uint32_t)(c->h_pinned[501] & 0xFFFFFFFFu);
     b.only_path3 = 1;
     if (n_rej && getenv("YMERGE_LEAN_DEBUG")) {
@@ -576,11 +586,12 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   hipEventRecord(c->ev[0], c->s);
   const bool fast = c->fast_threads && n_rej > 0;
   if (fast) {
-    ym::launch_decode(d_bytes, d_upd_off, n_updates, c->rec.as<uint32_t>(), c->ovf.as<uint32_t>(), c->huge.as<uint32_t>(),
-                      huge_words(n_bytes), c->s, lp_args(c, n_bytes, b.v1x));
+    if (!decoded) // (the grid lane's records are still valid)
+      ym::launch_decode(d_bytes, d_upd_off, n_updates, c->rec.as<uint32_t>(), c->ovf.as<uint32_t>(),
+                        c->huge.as<uint32_t>(), huge_words(n_bytes), c->s, lp_args(c, n_bytes, b.v1x));
     hipEventRecord(c->ev[5], c->s);
     ym::launch_fast_merge(b, c->caps, fo, c->fast_threads, c->s);
-    if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
+    if (hipGetLastError() != hipSuccess) return DEV_FAIL();
     hipEventRecord(c->ev[6], c->s);
   }
   else {
@@ -593,7 +604,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   uint32_t n_p1 = c->fast_threads ? 0 : n, n_p2 = 0;
   if (fast) {
     hipMemcpyAsync(c->h_pinned + 12, c->counter.as<uint32_t>() + 4, 16, hipMemcpyDeviceToHost, c->s);
-    if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
+    if (hipStreamSynchronize(c->s) != hipSuccess) return DEV_FAIL();
     const uint32_t *np = (const uint32_t *)(c->h_pinned + 12);
     n_p1 = np[1];
     n_p2 = np[2];
@@ -603,12 +614,12 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   if (fast && n_p2) {
     // long single-client documents first (ygiant.hip): listed and marked GS_PATH, merged by the
     // grid-wide kernels; the ones that are not that shape return to path 2 before k_big_count
-    const bool giant = c->giant_min && n_updates >= c->giant_min && !c->want_stamps;
+    const bool giant = c->giant_min && n_updates >= c->giant_min && !c->want_stamps && !giant_rejected;
     // single long update documents (one REC_LONG record, ylong.hip): listed in the same round trip
     const bool lsg = c->long_parse && c->long_grid && !c->want_stamps;
     constexpr size_t GSL = 1 + 6 * ym::GS_LIST, LSL = 4 + ym::LS_EW * ym::LS_LIST;
     if (giant || lsg) {
-      if (!c->gs_list.ensure(GSL * 8) || !c->ls_list.ensure(LSL * 4)) return YMERGE_ERR_DEVICE;
+      if (!c->gs_list.ensure(GSL * 8) || !c->ls_list.ensure(LSL * 4)) return DEV_FAIL();
       if (giant) {
         hipMemsetAsync(c->gs_list.p, 0, 8, c->s);
         ym::launch_gs_find(b, path, c->giant_min, c->gs_list.as<uint64_t>(), c->s);
@@ -635,7 +646,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
       const std::vector<LsEntry> ls = ls_entries((const uint32_t *)(c->h_pinned + 256));
       uint64_t words = 0;
       for (const LsEntry &e : ls) words = std::max(words, ls_scratch_words(e));
-      if (!ls.empty() && !c->ls_scr.ensure(words * 4 + 64)) return YMERGE_ERR_DEVICE;
+      if (!ls.empty() && !c->ls_scr.ensure(words * 4 + 64)) return DEV_FAIL();
       for (const LsEntry &e : ls) { // one after the other on the stream: the scratch is reused
         ym::LsArgs a{};
         a.bytes = b.bytes;
@@ -658,13 +669,13 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     ym::launch_scan_u64(c->need.as<uint64_t>(), c->scr_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
     hipMemcpyAsync(c->h_pinned + 10, c->scr_off.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, c->s);
     hipMemcpyAsync(c->h_pinned + 11, c->counter.as<uint32_t>() + 2, 4, hipMemcpyDeviceToHost, c->s);
-    if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
+    if (hipStreamSynchronize(c->s) != hipSuccess) return DEV_FAIL();
     n_big = (uint32_t)(c->h_pinned[11] & 0xFFFFFFFFu);
     if (n_big) {
-      if (!c->big_scratch.ensure((size_t)c->h_pinned[10] * 4 + 64)) return YMERGE_ERR_DEVICE;
+      if (!c->big_scratch.ensure((size_t)c->h_pinned[10] * 4 + 64)) return DEV_FAIL();
       ym::launch_big_merge(b, c->counts.as<uint32_t>(), c->scr_off.as<uint64_t>(), c->big_scratch.as<uint32_t>(), fo,
                            c->s);
-      if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
+      if (hipGetLastError() != hipSuccess) return DEV_FAIL();
     }
   }
   hipEventRecord(c->ev[1], c->s);
@@ -679,7 +690,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     hipMemcpyAsync(c->h_pinned + 9, c->counter.p, 4, hipMemcpyDeviceToHost, c->s);
     hipMemcpyAsync(c->h_pinned + 14, c->counter.as<uint32_t>() + 7, 12, hipMemcpyDeviceToHost, c->s);
     hipMemcpyAsync(c->h_pinned + 17, c->counter.as<uint32_t>() + 18, 8, hipMemcpyDeviceToHost, c->s); // npath[14..15]
-    if (hipStreamSynchronize(c->s) != hipSuccess) return YMERGE_ERR_DEVICE;
+    if (hipStreamSynchronize(c->s) != hipSuccess) return DEV_FAIL();
     words = c->h_pinned[8];
     n_exact = (uint32_t)(c->h_pinned[9] & 0xFFFFFFFFu);
     n_overlap = (uint32_t)(c->h_pinned[14] & 0xFFFFFFFFu);
@@ -688,19 +699,19 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     n_giant = (uint32_t)(c->h_pinned[17] & 0xFFFFFFFFu) + (uint32_t)(c->h_pinned[17] >> 32); // + long-update grid path
   }
   if (n_exact) {
-    if (!c->scratch.ensure((size_t)words * 4 + 64)) return YMERGE_ERR_DEVICE;
+    if (!c->scratch.ensure((size_t)words * 4 + 64)) return DEV_FAIL();
     ym::launch_seq_merge(false, b, path, status, c->counts.as<uint32_t>(), c->scr_off.as<uint64_t>(),
                          c->scratch.as<uint32_t>(), c->sizes.as<uint64_t>(), nullptr, nullptr, 0, nullptr, nullptr,
                          status, c->s);
     ym::launch_scan_u64(c->sizes.as<uint64_t>(), c->spill_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
     uint64_t spill = 0;
-    if (!read_words(c, c->spill_off.as<uint64_t>() + n, 8, &spill)) return YMERGE_ERR_DEVICE;
-    if (!ensure_keep(c, c->arena, slots + spill + 4096, slots)) return YMERGE_ERR_DEVICE;
+    if (!read_words(c, c->spill_off.as<uint64_t>() + n, 8, &spill)) return DEV_FAIL();
+    if (!ensure_keep(c, c->arena, slots + spill + 4096, slots)) return DEV_FAIL();
     arena = c->arena.as<uint8_t>();
     ym::launch_seq_merge(true, b, path, status, c->counts.as<uint32_t>(), c->scr_off.as<uint64_t>(),
                          c->scratch.as<uint32_t>(), nullptr, c->spill_off.as<uint64_t>(), arena, slots, ostart, olen,
                          nullptr, c->s);
-    if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
+    if (hipGetLastError() != hipSuccess) return DEV_FAIL();
   }
   hipEventRecord(c->ev[2], c->s);
   // total output bytes (and packed offsets for host copies); when k_lean wrote every
@@ -710,7 +721,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   if (c->pack_stale) {
     for (int q = 0; q < 64; q++) total += c->h_pinned[512 + 8 * q];
     hipEventRecord(c->ev[3], c->s);
-    if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
+    if (hipGetLastError() != hipSuccess) return DEV_FAIL();
     c->stats = ymerge_stats{};
     c->stats.n_docs = n_docs;
     c->stats.bytes_in = n_bytes;
@@ -727,9 +738,9 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   } else {
     ym::launch_scan_u64(olen, c->pack_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
     hipEventRecord(c->ev[3], c->s);
-    if (!read_words(c, c->pack_off.as<uint64_t>() + n, 8, &total)) return YMERGE_ERR_DEVICE;
+    if (!read_words(c, c->pack_off.as<uint64_t>() + n, 8, &total)) return DEV_FAIL();
   }
-  if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
+  if (hipGetLastError() != hipSuccess) return DEV_FAIL();
   float t01 = 0, t12 = 0, t23 = 0, t03 = 0, t05 = 0, t61 = 0, t70 = 0;
   hipEventElapsedTime(&t70, c->ev[7], c->ev[0]);
   hipEventElapsedTime(&t05, c->ev[0], c->ev[5]);
@@ -783,7 +794,7 @@ static int plan_exec(ymerge_ctx *c, bool diff, const uint8_t *d_bytes, const uin
                      const uint8_t *d_sv, const uint64_t *d_sv_off, uint64_t n_docs, ymerge_device_result *res,
                      uint32_t frame = 0, const uint64_t *sv_end = nullptr, const uint8_t *pre_status = nullptr) {
   resolve_times(c);
-  if (hipSetDevice(c->device) != hipSuccess) return YMERGE_ERR_DEVICE;
+  if (hipSetDevice(c->device) != hipSuccess) return DEV_FAIL();
   if (n_docs > 0xFFFFFFFFull) return YMERGE_ERR_OTHER;
   const uint32_t n = (uint32_t)n_docs;
   ym::DiffBatch b{d_bytes, d_upd_off, d_sv, d_sv_off, n};
@@ -792,7 +803,7 @@ static int plan_exec(ymerge_ctx *c, bool diff, const uint8_t *d_bytes, const uin
   b.frame = frame;
   if (frame == 1) {
     if (!c->sync_off.ensure((n + 1) * 8) || !c->sync_end.ensure((n + 1) * 8) || !c->sync_st.ensure(n + 1))
-      return YMERGE_ERR_DEVICE;
+      return DEV_FAIL();
     ym::launch_sync_parse(d_sv, d_sv_off, n, c->sync_off.as<uint64_t>(), c->sync_end.as<uint64_t>(),
                           c->sync_st.as<uint8_t>(), c->s);
     b.sv_off = c->sync_off.as<uint64_t>();
@@ -808,7 +819,7 @@ static int plan_exec(ymerge_ctx *c, bool diff, const uint8_t *d_bytes, const uin
   if (!c->status.ensure(nn) || !c->path.ensure(nn) || !c->out_len.ensure(nn * 8) || !c->pack_off.ensure(nn * 8) ||
       !c->need.ensure(nn * 8) || !c->spill_off.ensure(nn * 8) || !c->scan_tmp.ensure(ym::scan_tmp_elems(n) * 8 + 64) ||
       !c->counter.ensure(64) || !c->plan_small.ensure(nn * sw * 4) || !c->plan_wlist.ensure(nn * 4))
-    return YMERGE_ERR_DEVICE;
+    return DEV_FAIL();
   ym::PlanScratch ps{c->plan_small.as<uint32_t>(), sw,       nullptr,
                      c->spill_off.as<uint64_t>(), c->path.as<uint8_t>(), c->status.as<uint8_t>(),
                      c->out_len.as<uint64_t>(),    c->counter.as<uint32_t>()};
@@ -817,7 +828,7 @@ static int plan_exec(ymerge_ctx *c, bool diff, const uint8_t *d_bytes, const uin
   ps.wave_list = c->plan_wlist.as<uint32_t>();
   ps.wave_n = c->counter.as<uint32_t>() + 8; // zeroed with the counters below
   if (c->want_stamps) { // diagnostic: k_plan_ring phase cycles
-    if (!c->stamps.ensure(nn * 16 * 8)) return YMERGE_ERR_DEVICE;
+    if (!c->stamps.ensure(nn * 16 * 8)) return DEV_FAIL();
     hipMemsetAsync(c->stamps.p, 0, nn * 16 * 8, c->s);
     ps.stamps = c->stamps.as<uint64_t>();
     c->stamps_docs = n_docs;
@@ -829,7 +840,7 @@ static int plan_exec(ymerge_ctx *c, bool diff, const uint8_t *d_bytes, const uin
   std::vector<LsEntry> ls;
   std::vector<uint64_t> ls_off;
   if (c->long_parse && c->long_grid && c->ls_min_diff && !c->want_stamps) {
-    if (!c->huge.ensure(16 + 8 * ym::HUGE_LIST)) return YMERGE_ERR_DEVICE;
+    if (!c->huge.ensure(16 + 8 * ym::HUGE_LIST)) return DEV_FAIL();
     hipMemsetAsync(c->huge.p, 0, 16, c->s);
     ym::launch_ls_list_diff(d_upd_off, b.pre_status, n, c->ls_min_diff, c->huge.as<uint32_t>(), c->s);
     hipMemcpyAsync(c->h_pinned + 9, c->huge.p, 4, hipMemcpyDeviceToHost, c->s);
@@ -900,22 +911,22 @@ static int plan_exec(ymerge_ctx *c, bool diff, const uint8_t *d_bytes, const uin
     ym::launch_big_need(d_upd_off, ps.big, n, c->need.as<uint64_t>(), c->s);
     ym::launch_scan_u64(c->need.as<uint64_t>(), c->spill_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
     uint64_t words = 0;
-    if (!read_words(c, c->spill_off.as<uint64_t>() + n, 8, &words)) return YMERGE_ERR_DEVICE;
-    if (!c->plan_big.ensure(words * 4 + 64)) return YMERGE_ERR_DEVICE;
+    if (!read_words(c, c->spill_off.as<uint64_t>() + n, 8, &words)) return DEV_FAIL();
+    if (!c->plan_big.ensure(words * 4 + 64)) return DEV_FAIL();
     ps.bigscr = c->plan_big.as<uint32_t>();
     ym::launch_plan(diff, 1, b, ps, c->s);
   }
   hipEventRecord(c->ev[2], c->s);
   ym::launch_scan_u64(ps.size, c->pack_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
   uint64_t total = 0;
-  if (!read_words(c, c->pack_off.as<uint64_t>() + n, 8, &total)) return YMERGE_ERR_DEVICE;
-  if (!c->arena.ensure(total + 64)) return YMERGE_ERR_DEVICE;
+  if (!read_words(c, c->pack_off.as<uint64_t>() + n, 8, &total)) return DEV_FAIL();
+  if (!c->arena.ensure(total + 64)) return DEV_FAIL();
   hipEventRecord(c->ev[4], c->s);
   ym::launch_exec(b, ps, c->pack_off.as<uint64_t>(), c->arena.as<uint8_t>(), c->s);
   for (size_t k = 0; k < ls.size(); k++) ym::launch_ls_doc(ls_args(k), 1, c->s);
   hipEventRecord(c->ev[3], c->s);
   if (hipError_t e = hipStreamSynchronize(c->s); e != hipSuccess) return dev_err("exec", e);
-  if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
+  if (hipGetLastError() != hipSuccess) return DEV_FAIL();
   float t01 = 0, t12 = 0, t43 = 0, t03 = 0;
   hipEventElapsedTime(&t01, c->ev[0], c->ev[1]);
   hipEventElapsedTime(&t12, c->ev[1], c->ev[2]);
@@ -975,7 +986,7 @@ extern "C" int ydiff_updates_v1_batch_device(ymerge_ctx *c, const uint8_t *d_byt
 static int compact_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes, const uint64_t *d_upd_off,
                           uint64_t n_updates, const uint64_t *d_doc_upd, uint64_t n_docs, ymerge_device_result *res) {
   resolve_times(c);
-  if (hipSetDevice(c->device) != hipSuccess) return YMERGE_ERR_DEVICE;
+  if (hipSetDevice(c->device) != hipSuccess) return DEV_FAIL();
   if (n_docs > 0xFFFFFFFFull) return YMERGE_ERR_OTHER;
   const uint32_t n = (uint32_t)n_docs;
   const size_t nn = (size_t)n + 1;
@@ -984,12 +995,12 @@ static int compact_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_byte
       !c->pack_off.ensure(nn * 8) || !c->scan_tmp.ensure(ym::scan_tmp_elems(n) * 8 + 64) ||
       !ensure_keep(c, c->arena, slots + 4096, 0) || !c->need.ensure(nn * 8) || !c->scr_off.ensure(nn * 8) ||
       !c->counts.ensure(nn * ym::COMPACT_HDR_WORDS * 4))
-    return YMERGE_ERR_DEVICE;
+    return DEV_FAIL();
   ym::BatchIn b{d_bytes, d_upd_off, d_doc_upd, n, nullptr, nullptr};
   ym::FastOut fo{c->arena.as<uint8_t>(), c->out_start.as<uint64_t>(), c->out_len.as<uint64_t>(),
                  c->status.as<uint8_t>(), c->path.as<uint8_t>(), nullptr, nullptr, nullptr};
   if (c->want_stamps) { // diagnostic: per-document phase cycles (ycompact.hip)
-    if (!c->stamps.ensure(nn * 16 * 8)) return YMERGE_ERR_DEVICE;
+    if (!c->stamps.ensure(nn * 16 * 8)) return DEV_FAIL();
     hipMemsetAsync(c->stamps.p, 0, nn * 16 * 8, c->s);
     fo.stamps = c->stamps.as<uint64_t>();
     c->stamps_docs = n_docs;
@@ -999,17 +1010,17 @@ static int compact_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_byte
   ym::launch_compact_count(b, c->counts.as<uint32_t>(), c->need.as<uint64_t>(), c->s);
   ym::launch_scan_u64(c->need.as<uint64_t>(), c->scr_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
   uint64_t words = 0;
-  if (!read_words(c, c->scr_off.as<uint64_t>() + n, 8, &words)) return YMERGE_ERR_DEVICE;
-  if (!c->cscr.ensure(words * 4 + 64)) return YMERGE_ERR_DEVICE;
+  if (!read_words(c, c->scr_off.as<uint64_t>() + n, 8, &words)) return DEV_FAIL();
+  if (!c->cscr.ensure(words * 4 + 64)) return DEV_FAIL();
   hipEventRecord(c->ev[2], c->s);
   ym::launch_compact(b, fo, c->counts.as<uint32_t>(), c->scr_off.as<uint64_t>(), c->cscr.as<uint32_t>(),
                      c->compact_lpw, c->s);
-  if (hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
+  if (hipGetLastError() != hipSuccess) return DEV_FAIL();
   hipEventRecord(c->ev[1], c->s);
   ym::launch_scan_u64(c->out_len.as<uint64_t>(), c->pack_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
   c->pack_stale = false;
   uint64_t total = 0;
-  if (!read_words(c, c->pack_off.as<uint64_t>() + n, 8, &total)) return YMERGE_ERR_DEVICE;
+  if (!read_words(c, c->pack_off.as<uint64_t>() + n, 8, &total)) return DEV_FAIL();
   float t01 = 0, t21 = 0;
   hipEventElapsedTime(&t01, c->ev[0], c->ev[1]);
   hipEventElapsedTime(&t21, c->ev[2], c->ev[1]);
@@ -1044,36 +1055,36 @@ static int v2_transcode(ymerge_ctx *c, const uint8_t *d_bytes, const uint64_t *d
   const size_t nn = (size_t)n_upd + 1;
   if (!c->v2x_sz.ensure(nn * 8) || !c->v2x_off.ensure(nn * 8) || !c->v2_ust.ensure(nn) ||
       !c->scan_tmp.ensure(ym::scan_tmp_elems((uint32_t)n_upd) * 8 + 64))
-    return YMERGE_ERR_DEVICE;
+    return DEV_FAIL();
   ym::launch_v2_decode(false, d_bytes, d_upd_off, n_upd, c->v2x_sz.as<uint64_t>(), nullptr, c->v2_ust.as<uint8_t>(),
                        c->s);
   ym::launch_scan_u64(c->v2x_sz.as<uint64_t>(), c->v2x_off.as<uint64_t>(), (uint32_t)n_upd,
                       c->scan_tmp.as<uint64_t>(), c->s);
-  if (!read_words(c, c->v2x_off.as<uint64_t>() + n_upd, 8, total)) return YMERGE_ERR_DEVICE;
-  if (!c->v2x.ensure(*total + 64)) return YMERGE_ERR_DEVICE;
+  if (!read_words(c, c->v2x_off.as<uint64_t>() + n_upd, 8, total)) return DEV_FAIL();
+  if (!c->v2x.ensure(*total + 64)) return DEV_FAIL();
   ym::launch_v2_decode(true, d_bytes, d_upd_off, n_upd, c->v2x_off.as<uint64_t>(), c->v2x.as<uint8_t>(),
                        c->v2_ust.as<uint8_t>(), c->s);
-  return hipGetLastError() == hipSuccess ? 0 : YMERGE_ERR_DEVICE;
+  return hipGetLastError() == hipSuccess ? 0 : DEV_FAIL();
 }
 // v1x result -> v2 (mode 0 update, 1 state vector) in c->v2_out; `res` then describes it
 static int v2_encode(ymerge_ctx *c, ymerge_device_result *res, uint32_t n, int mode) {
   const size_t nn = (size_t)n + 1;
   if (!c->v2_osz.ensure(nn * 8) || !c->v2_ooff.ensure(nn * 8) || !c->pack_off.ensure(nn * 8) ||
       !c->scan_tmp.ensure(ym::scan_tmp_elems(n) * 8 + 64))
-    return YMERGE_ERR_DEVICE;
+    return DEV_FAIL();
   ym::launch_v2_encode(false, res->d_out, res->d_out_start, res->d_out_len, res->d_status, n,
                        c->v2_osz.as<uint64_t>(), nullptr, mode, c->s);
   ym::launch_scan_u64(c->v2_osz.as<uint64_t>(), c->v2_ooff.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
   uint64_t total = 0;
-  if (!read_words(c, c->v2_ooff.as<uint64_t>() + n, 8, &total)) return YMERGE_ERR_DEVICE;
-  if (!c->v2_out.ensure(total + 64)) return YMERGE_ERR_DEVICE;
+  if (!read_words(c, c->v2_ooff.as<uint64_t>() + n, 8, &total)) return DEV_FAIL();
+  if (!c->v2_out.ensure(total + 64)) return DEV_FAIL();
   ym::launch_v2_encode(true, res->d_out, res->d_out_start, res->d_out_len, res->d_status, n,
                        c->v2_ooff.as<uint64_t>(), c->v2_out.as<uint8_t>(), mode, c->s);
   // packed offsets of the result (pack_to_host copies the arena in their order)
   c->pack_stale = false;
   if (hipMemcpyAsync(c->pack_off.p, c->v2_ooff.p, nn * 8, hipMemcpyDeviceToDevice, c->s) != hipSuccess)
-    return YMERGE_ERR_DEVICE;
-  if (hipStreamSynchronize(c->s) != hipSuccess || hipGetLastError() != hipSuccess) return YMERGE_ERR_DEVICE;
+    return DEV_FAIL();
+  if (hipStreamSynchronize(c->s) != hipSuccess || hipGetLastError() != hipSuccess) return DEV_FAIL();
   res->d_out = c->v2_out.as<uint8_t>();
   res->d_out_start = c->v2_ooff.as<uint64_t>();
   res->d_out_len = c->v2_osz.as<uint64_t>();
@@ -1083,7 +1094,7 @@ static int v2_encode(ymerge_ctx *c, ymerge_device_result *res, uint32_t n, int m
 }
 static int merge_v2_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes, const uint64_t *d_upd_off,
                            uint64_t n_updates, const uint64_t *d_doc_upd, uint64_t n_docs, ymerge_device_result *res) {
-  if (hipSetDevice(c->device) != hipSuccess) return YMERGE_ERR_DEVICE;
+  if (hipSetDevice(c->device) != hipSuccess) return DEV_FAIL();
   if (n_docs > 0xFFFFFFFFull) return YMERGE_ERR_OTHER;
   uint64_t xbytes = 0;
   hipEventRecord(c->v2ev[0], c->s);
@@ -1108,14 +1119,14 @@ static int merge_v2_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_byt
 // diff_updates_v2 (diff = true) / encode_state_vector_from_update_v2: one update per document
 static int plan_v2_device(ymerge_ctx *c, bool diff, const uint8_t *d_bytes, const uint64_t *d_upd_off,
                           const uint8_t *d_sv, const uint64_t *d_sv_off, uint64_t n_docs, ymerge_device_result *res) {
-  if (hipSetDevice(c->device) != hipSuccess) return YMERGE_ERR_DEVICE;
+  if (hipSetDevice(c->device) != hipSuccess) return DEV_FAIL();
   if (n_docs > 0xFFFFFFFFull) return YMERGE_ERR_OTHER;
   const uint32_t n = (uint32_t)n_docs;
   uint64_t xbytes = 0;
   int st = v2_transcode(c, d_bytes, d_upd_off, n_docs, &xbytes);
   if (st) return st;
   if (!c->v2_svoff.ensure((n + 1) * 8) || !c->v2_svend.ensure((n + 1) * 8) || !c->v2_pre.ensure(n + 1))
-    return YMERGE_ERR_DEVICE;
+    return DEV_FAIL();
   ym::launch_v2_sv_parse(diff ? d_sv : nullptr, d_sv_off, c->v2_ust.as<uint8_t>(), n, c->v2_svoff.as<uint64_t>(),
                          c->v2_svend.as<uint64_t>(), c->v2_pre.as<uint8_t>(), c->s);
   st = plan_exec(c, diff, c->v2x.as<uint8_t>(), c->v2x_off.as<uint64_t>(), d_sv,
@@ -1133,13 +1144,13 @@ extern "C" int yconvert_updates_v1_to_v2_batch_device(ymerge_ctx *c, const uint8
                                                      ymerge_device_result *res) {
   if (!c || !res) return YMERGE_ERR_OTHER;
   std::lock_guard<std::mutex> g(c->mu);
-  if (hipSetDevice(c->device) != hipSuccess) return YMERGE_ERR_DEVICE;
+  if (hipSetDevice(c->device) != hipSuccess) return DEV_FAIL();
   if (n_updates > 0xFFFFFFFFull) return YMERGE_ERR_OTHER;
   std::vector<uint64_t> iota(n_updates + 1);
   for (uint64_t i = 0; i <= n_updates; i++) iota[i] = i;
   if (!c->in_doc_upd.ensure((n_updates + 1) * 8) ||
       hipMemcpyAsync(c->in_doc_upd.p, iota.data(), (n_updates + 1) * 8, hipMemcpyHostToDevice, c->s) != hipSuccess)
-    return YMERGE_ERR_DEVICE;
+    return DEV_FAIL();
   int st = merge_device(c, d_bytes, n_bytes, d_upd_off, n_updates, c->in_doc_upd.as<uint64_t>(), n_updates, res);
   if (st) return st;
   return v2_encode(c, res, (uint32_t)n_updates, 0);
@@ -1170,19 +1181,19 @@ extern "C" int yencode_state_vector_from_update_v2_batch_device(ymerge_ctx *c, c
 static int pack_to_host(ymerge_ctx *c, const ymerge_device_result *res, uint64_t n_docs, uint8_t *out,
                         uint64_t *out_off, uint8_t *status) {
   const uint32_t n = (uint32_t)n_docs;
-  if (!c->packed.ensure(res->out_bytes + 64)) return YMERGE_ERR_DEVICE;
+  if (!c->packed.ensure(res->out_bytes + 64)) return DEV_FAIL();
   if (c->pack_stale) { // packed offsets of a merge whose documents were all written by k_lean
     ym::launch_scan_u64(res->d_out_len, c->pack_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
     c->pack_stale = false;
   }
   ym::launch_pack(res->d_out, res->d_out_start, res->d_out_len, c->pack_off.as<uint64_t>(),
                   c->packed.as<uint8_t>(), n, c->s);
-  if (out && res->out_bytes && !copy_d2h(c, out, c->packed.p, res->out_bytes)) return YMERGE_ERR_DEVICE;
+  if (out && res->out_bytes && !copy_d2h(c, out, c->packed.p, res->out_bytes)) return DEV_FAIL();
   if (out_off && hipMemcpyAsync(out_off, c->pack_off.p, (n_docs + 1) * 8, hipMemcpyDeviceToHost, c->s) != hipSuccess)
-    return YMERGE_ERR_DEVICE;
+    return DEV_FAIL();
   if (status && n_docs && hipMemcpyAsync(status, res->d_status, n_docs, hipMemcpyDeviceToHost, c->s) != hipSuccess)
-    return YMERGE_ERR_DEVICE;
-  return hipStreamSynchronize(c->s) == hipSuccess ? 0 : YMERGE_ERR_DEVICE;
+    return DEV_FAIL();
+  return hipStreamSynchronize(c->s) == hipSuccess ? 0 : DEV_FAIL();
 }
 
 extern "C" int ymerge_result_to_host(ymerge_ctx *c, const ymerge_device_result *res, uint64_t n_docs, uint8_t *out,
@@ -1201,7 +1212,7 @@ extern "C" int ymerge_debug_stamps(ymerge_ctx *c, uint64_t n_docs, uint64_t *dst
   if (n_docs > c->stamps_docs) n_docs = c->stamps_docs; // never past the last batch's stamps
   if (!n_docs) return 0;
   hipSetDevice(c->device);
-  if (hipMemcpy(dst, c->stamps.p, n_docs * 16 * 8, hipMemcpyDeviceToHost) != hipSuccess) return YMERGE_ERR_DEVICE;
+  if (hipMemcpy(dst, c->stamps.p, n_docs * 16 * 8, hipMemcpyDeviceToHost) != hipSuccess) return DEV_FAIL();
   return 0;
 }
 
@@ -1245,18 +1256,18 @@ static int host_merge_pipelined(ymerge_ctx *c, const uint8_t *bytes, const uint6
     if (upd_off[doc_upd[d + 1]] - upd_off[doc_upd[gd.back()]] >= GROUP_BYTES && gd.size() < 64) gd.push_back(d + 1);
   if (gd.back() != n_docs) gd.push_back(n_docs);
   const size_t G = gd.size() - 1;
-  if (!c->s_in && hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking) != hipSuccess) return YMERGE_ERR_DEVICE;
-  if (!c->s_out && hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking) != hipSuccess) return YMERGE_ERR_DEVICE;
+  if (!c->s_in && hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking) != hipSuccess) return DEV_FAIL();
+  if (!c->s_out && hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking) != hipSuccess) return DEV_FAIL();
   for (size_t k = 0; k < G; k++)
     if (!c->ev_in[k] && hipEventCreateWithFlags(&c->ev_in[k], hipEventDisableTiming) != hipSuccess)
-      return YMERGE_ERR_DEVICE;
+      return DEV_FAIL();
   for (int k = 0; k < 2; k++)
     if ((!c->ev_out[k] && hipEventCreateWithFlags(&c->ev_out[k], hipEventDisableTiming) != hipSuccess) ||
         (!c->ev_packed[k] && hipEventCreateWithFlags(&c->ev_packed[k], hipEventDisableTiming) != hipSuccess))
-      return YMERGE_ERR_DEVICE;
+      return DEV_FAIL();
   if (!stage_init(c) || !c->in_bytes.ensure(nbytes + 16) || !c->in_upd_off.ensure((n_updates + G + 1) * 8) ||
       !c->grp_doc_upd.ensure((n_docs + G + 1) * 8))
-    return YMERGE_ERR_DEVICE;
+    return DEV_FAIL();
   // rebased tables of every group: its documents index its slice of the update offsets, and
   // those count from the group's first byte rounded down to 16 (the kernels' aligned loads), so
   // each merge_device call sizes its slots and scratch by the group, not the whole batch
@@ -1273,7 +1284,7 @@ static int host_merge_pipelined(ymerge_ctx *c, const uint8_t *bytes, const uint6
   if (hipMemcpyAsync(c->in_upd_off.p, guo.data(), guo_off[G] * 8, hipMemcpyHostToDevice, c->s_in) != hipSuccess ||
       hipMemcpyAsync(c->grp_doc_upd.p, gdu.data(), gdu_off[G] * 8, hipMemcpyHostToDevice, c->s_in) != hipSuccess ||
       hipStreamSynchronize(c->s_in) != hipSuccess)
-    return YMERGE_ERR_DEVICE;
+    return DEV_FAIL();
   // producer: stage every group's bytes through the pinned ring on s_in, one event per group
   std::atomic<int> prod_rc{0};
   std::atomic<size_t> recorded{0}; // groups whose ev_in the producer has recorded
@@ -1286,18 +1297,18 @@ static int host_merge_pipelined(ymerge_ctx *c, const uint8_t *bytes, const uint6
         const int b = (int)(i & 1);
         const size_t len = std::min<uint64_t>(STAGE_CHUNK, z - off);
         if (i >= 2 && hipEventSynchronize(c->stage_ev[b]) != hipSuccess) {
-          prod_rc = YMERGE_ERR_DEVICE;
+          prod_rc = DEV_FAIL();
           break;
         }
         par_memcpy(c->stage[b], bytes + off, len);
         if (hipMemcpyAsync(c->in_bytes.as<uint8_t>() + off, c->stage[b], len, hipMemcpyHostToDevice, c->s_in) !=
                 hipSuccess ||
             hipEventRecord(c->stage_ev[b], c->s_in) != hipSuccess) {
-          prod_rc = YMERGE_ERR_DEVICE;
+          prod_rc = DEV_FAIL();
           break;
         }
       }
-      if (!prod_rc && hipEventRecord(c->ev_in[k], c->s_in) != hipSuccess) prod_rc = YMERGE_ERR_DEVICE;
+      if (!prod_rc && hipEventRecord(c->ev_in[k], c->s_in) != hipSuccess) prod_rc = DEV_FAIL();
       recorded.store(k + 1);
     }
   });
@@ -1318,7 +1329,7 @@ static int host_merge_pipelined(ymerge_ctx *c, const uint8_t *bytes, const uint6
       std::this_thread::yield();
     }
     if (rc || hipStreamWaitEvent(c->s, c->ev_in[k], 0) != hipSuccess) {
-      rc = rc ? rc : YMERGE_ERR_DEVICE;
+      rc = rc ? rc : DEV_FAIL();
       break;
     }
     ymerge_device_result dr{};
@@ -1382,11 +1393,11 @@ static int host_merge(ymerge_ctx *c, int version, const uint8_t *bytes, const ui
     return host_merge_pipelined(c, bytes, upd_off, n_updates, doc_upd, n_docs, out);
   if (!c->in_bytes.ensure(nbytes + 16) || !c->in_upd_off.ensure((n_updates + 1) * 8) ||
       !c->in_doc_upd.ensure((n_docs + 1) * 8))
-    return YMERGE_ERR_DEVICE;
-  if (!copy_h2d(c, c->in_bytes.p, bytes, nbytes)) return YMERGE_ERR_DEVICE;
+    return DEV_FAIL();
+  if (!copy_h2d(c, c->in_bytes.p, bytes, nbytes)) return DEV_FAIL();
   if (hipMemcpyAsync(c->in_upd_off.p, upd_off, (n_updates + 1) * 8, hipMemcpyHostToDevice, c->s) != hipSuccess ||
       hipMemcpyAsync(c->in_doc_upd.p, doc_upd, (n_docs + 1) * 8, hipMemcpyHostToDevice, c->s) != hipSuccess)
-    return YMERGE_ERR_DEVICE;
+    return DEV_FAIL();
   ymerge_device_result dr{};
   int st = (version == 3 ? compact_device : version == 2 ? merge_v2_device : merge_device)(c, c->in_bytes.as<uint8_t>(), nbytes,
                                                            c->in_upd_off.as<uint64_t>(), n_updates,
@@ -1597,7 +1608,7 @@ static std::vector<ymerge_ctx *> g_default;
 static int g_default_device = -1;
 extern "C" int ymerge_set_default_device(int device) {
   int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return YMERGE_ERR_DEVICE;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return DEV_FAIL();
   std::lock_guard<std::mutex> g(g_default_mu);
   g_default_device = device;
   return 0;
@@ -1616,6 +1627,7 @@ static ymerge_ctx *default_ctx() {
 }
 
 extern "C" uint8_t ymerge_last_error(void) { return g_last_error; }
+extern "C" const char *ymerge_last_error_message(void) { return g_last_msg; }
 
 extern "C" char *ymerge_updates_v1(const char *const *updates, const uint32_t *updates_len, uint32_t updates_count,
                                    uint32_t *out_len) {
@@ -1669,14 +1681,14 @@ static int host_plan_exec(ymerge_ctx *c, bool diff, const uint8_t *bytes, const 
   const uint64_t nbytes = upd_off[n_docs], nsv = diff ? sv_off[n_docs] : 0;
   if (!c->in_bytes.ensure(nbytes + 16) || !c->in_upd_off.ensure((n_docs + 1) * 8) ||
       (diff && (!c->in_sv.ensure(nsv + 16) || !c->in_sv_off.ensure((n_docs + 1) * 8))))
-    return YMERGE_ERR_DEVICE;
-  if (!copy_h2d(c, c->in_bytes.p, bytes, nbytes)) return YMERGE_ERR_DEVICE;
+    return DEV_FAIL();
+  if (!copy_h2d(c, c->in_bytes.p, bytes, nbytes)) return DEV_FAIL();
   if (hipMemcpyAsync(c->in_upd_off.p, upd_off, (n_docs + 1) * 8, hipMemcpyHostToDevice, c->s) != hipSuccess)
-    return YMERGE_ERR_DEVICE;
+    return DEV_FAIL();
   if (diff) {
-    if (!copy_h2d(c, c->in_sv.p, sv, nsv)) return YMERGE_ERR_DEVICE;
+    if (!copy_h2d(c, c->in_sv.p, sv, nsv)) return DEV_FAIL();
     if (hipMemcpyAsync(c->in_sv_off.p, sv_off, (n_docs + 1) * 8, hipMemcpyHostToDevice, c->s) != hipSuccess)
-      return YMERGE_ERR_DEVICE;
+      return DEV_FAIL();
   }
   ymerge_device_result dr{};
   int st = version == 2

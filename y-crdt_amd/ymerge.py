@@ -30,7 +30,17 @@ class YrsError(Exception):
 
 
 class DeviceError(RuntimeError):
-    pass
+    """A HIP failure inside the engine.  The message carries the library's provenance of it
+    (ymerge_last_error_message: the failing stage and the HIP error string)."""
+
+    def __init__(self, msg):
+        where = ""
+        try:
+            if _lib is not None:
+                where = (_lib.ymerge_last_error_message() or b"").decode(errors="replace")
+        except Exception:  # noqa: BLE001 -- the provenance is best effort
+            where = ""
+        super().__init__(f"{msg}: {where}" if where else msg)
 
 
 class _Stats(ctypes.Structure):
@@ -111,6 +121,7 @@ def lib():
     L.ymerge_binary_destroy.argtypes = [vp, u32]
     L.ymerge_set_default_device.argtypes = [c.c_int]
     L.ymerge_last_error.restype = c.c_uint8
+    L.ymerge_last_error_message.restype = c.c_char_p
     L.ydiff_updates_v1_batch.argtypes = [vp, vp, vp, vp, vp, u64, c.POINTER(c.c_void_p)]
     L.yencode_state_vector_from_update_v1_batch.argtypes = [vp, vp, vp, u64, c.POINTER(c.c_void_p)]
     L.ymerge_batch_result_destroy.argtypes = [vp]
