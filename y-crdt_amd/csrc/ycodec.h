@@ -124,11 +124,32 @@ struct Writer {
   uint8_t *p;
   uint64_t n;
   __device__ __forceinline__ void u8(uint8_t b) { p[n++] = b; }
+  // in groups of 16 whose loads are all issued before the group's stores (a plain byte loop
+  // waits one load latency per byte: the stores may alias the next loads)
   __device__ __forceinline__ void bytes(const uint8_t *s, uint32_t k) {
-    for (uint32_t i = 0; i < k; i++) p[n + i] = s[i];
+    uint32_t i = 0;
+    for (; i + 16 <= k; i += 16) {
+      uint8_t t[16];
+#pragma unroll
+      for (uint32_t j = 0; j < 16; j++) t[j] = s[i + j];
+#pragma unroll
+      for (uint32_t j = 0; j < 16; j++) p[n + i + j] = t[j];
+    }
+    for (; i < k; i++) p[n + i] = s[i];
     n += k;
   }
 };
+// no byte >= 0x80 in s[0, n) (independent loads, 16 in flight)
+__device__ __forceinline__ bool bytes_ascii(const uint8_t *s, uint32_t n) {
+  uint32_t hi = 0, i = 0;
+  for (; i + 16 <= n; i += 16) {
+#pragma unroll
+    for (uint32_t j = 0; j < 16; j++) hi |= s[i + j];
+    if (hi & 0x80) return false;
+  }
+  for (; i < n; i++) hi |= s[i];
+  return !(hi & 0x80);
+}
 template <class W> __device__ __forceinline__ void w_var(W &w, uint64_t v) {
   while (v >= 0x80) {
     w.u8((uint8_t)(v | 0x80));
@@ -980,6 +1001,13 @@ __device__ __noinline__ int emit_block(const uint8_t *p, uint32_t n, uint32_t po
     rd_var_u32(c, v, cn);
     const uint8_t *s = p + c.i;
     uint32_t sn = v, bo;
+    if ((off != 0 || end != 0) && sn > 1 && bytes_ascii(s, sn)) { // UTF-16 offsets are byte offsets
+      if (off > sn || end - off + 1 > sn - off) return E_PANIC; // (not reached for decoded lengths)
+      s += off;
+      sn = end - off + 1;
+      w_str(w, s, sn);
+      return 0;
+    }
     if (off != 0) {
       YM_TRY(str_split16(s, sn, off, bo));
       s += bo;

@@ -585,7 +585,7 @@ __global__ void __launch_bounds__(256) k_lp_clock(LpArgs a) {
 // headers are read by one lane; an entry's 2 * nr range varints are decoded in tiles of
 // LPD_NT * 16 bytes: a byte ends a varint iff < 0x80, the varint ordinal of a byte is the count
 // of terminators before it.
-constexpr uint32_t LPD_NT = 256, LPD_B = 16;
+constexpr uint32_t LPD_NT = 1024, LPD_B = 16;
 __device__ __forceinline__ bool lp_dvar(const uint8_t *p, uint32_t L, uint32_t q, uint32_t &v) {
   uint32_t x = 0, sh = 0;
   for (;;) {
