@@ -127,6 +127,39 @@ def main_zipf(n):
                   + ", ".join(f"{nm} {d[sel, i].mean():.0f}" for i, nm in enumerate(NAMES) if nm != "-"))
 
 
+def main_corpus():
+    """The reference corpus (small-test-dataset.bin, 5,320 documents): fast-path phase cycles,
+    records still walked over HBM (REC_SLOW) and re-walked (fill), and the slowest documents."""
+    b = workloads.dataset_docs()
+    e = ymerge.Engine(0)
+    e.merge_host(b.data, b.upd_off, b.doc_upd)
+    L = ymerge.lib()
+    L.ymerge_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+    n = b.n_docs
+    st = np.zeros((n, 16), np.uint64)
+    assert L.ymerge_debug_stamps(e._ctx, n, st.ctypes.data) == 0
+    print("stats", {k: (round(v, 3) if isinstance(v, float) else v) for k, v in e.stats().items()})
+    fast = (st[:, 11] > 0) & (st[:, 7] != 0xB16)
+    big = st[:, 7] == 0xB16
+    U = np.diff(b.doc_upd.astype(np.int64))
+    nbytes = np.diff(b.upd_off[b.doc_upd.astype(np.int64)].astype(np.int64))
+    d = np.diff(st[fast][:, :12].astype(np.int64), axis=1)
+    tot = d.sum(axis=1)
+    print(f"fast docs {fast.sum()}, big docs {big.sum()}; fast cycles/doc mean {tot.mean():.0f}, max {tot.max()}")
+    print("  phases: " + ", ".join(f"{nm} {d[:, i].mean():.0f}" for i, nm in enumerate(NAMES) if nm != "-"))
+    print(f"  records: slow {st[fast, 12].sum()}, complex {st[fast, 13].sum()}, fill walks {st[fast, 14].sum()}, "
+          f"overflow words {st[fast, 15].sum()}")
+    idx = np.nonzero(fast)[0][np.argsort(-tot)[:8]]
+    for q in idx:
+        dd = np.diff(st[q, :12].astype(np.int64))
+        print(f"  doc {q}: U {U[q]} bytes {nbytes[q]} slow {st[q, 12]} cx {st[q, 13]}: "
+              + ", ".join(f"{nm} {dd[i]}" for i, nm in enumerate(NAMES) if nm != "-"))
+    if big.any():
+        db = np.diff(st[big][:, :6].astype(np.int64), axis=1)
+        print(f"big docs: U {U[big].tolist()[:10]} bytes {nbytes[big].tolist()[:10]}")
+        print("  cycles/doc " + ", ".join(f"{nm} {db[:, i].mean():.0f}" for i, nm in enumerate(BIG_NAMES)))
+
+
 LEAN_NAMES = ["init", "decode", "layout", "copy", "ds_union", "ds_write"]
 LEAN_SUB = ["stage+prefetch", "walk", "blocks", "deleteset"]
 
@@ -169,6 +202,8 @@ def main():
         return main_big(int(sys.argv[2]) if len(sys.argv) > 2 else 2000, "c4")
     if len(sys.argv) > 1 and sys.argv[1] == "c1":
         return main_c1()
+    if len(sys.argv) > 1 and sys.argv[1] == "corpus":
+        return main_corpus()
     if len(sys.argv) > 1 and sys.argv[1] == "c5":
         return main_c5(int(sys.argv[2]) if len(sys.argv) > 2 else 20000)
     if len(sys.argv) > 1 and sys.argv[1] == "compact":

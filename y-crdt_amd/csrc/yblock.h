@@ -269,33 +269,39 @@ struct OvfFill {
   uint32_t *ov;
   uint32_t NBt, NEt; // totals of this update (RegSink pass)
   uint32_t nb, ne, nr;
+  bool on = true; // writes (a wave walking one update in lockstep: lane 0 only)
   YM_INLINE void on_section(uint32_t) {}
   YM_INLINE int on_block(uint32_t client, uint32_t clock, const BlockInfo &bi, uint32_t bpos, uint32_t blen) {
     if (bi.kind == BK_SKIP) return 0;
-    uint32_t *w = ov + 5 * nb;
-    w[0] = client;
-    w[1] = clock;
-    w[2] = bi.len;
-    w[3] = bpos;
-    w[4] = (uint32_t)bi.kind | (bi.reenc ? 4u : 0u) | (bi.enc_panic ? 8u : 0u) | (blen << 8);
+    if (on) {
+      uint32_t *w = ov + 5 * nb;
+      w[0] = client;
+      w[1] = clock;
+      w[2] = bi.len;
+      w[3] = bpos;
+      w[4] = (uint32_t)bi.kind | (bi.reenc ? 4u : 0u) | (bi.enc_panic ? 8u : 0u) | (blen << 8);
+    }
     nb++;
     return 0;
   }
   YM_INLINE int on_ds_begin(uint32_t) { return 0; }
   YM_INLINE int on_ds_entry(uint32_t client, uint32_t) {
-    ov[5 * NBt + ne] = client;
+    if (on) ov[5 * NBt + ne] = client;
     ne++;
     return 0;
   }
   YM_INLINE void on_ds_range(uint32_t s0, uint32_t e0) {
-    uint32_t *w = ov + 5 * NBt + 2 * NEt + 3 * nr;
-    w[0] = s0;
-    w[1] = e0;
-    w[2] = ne - 1;
+    if (on) {
+      uint32_t *w = ov + 5 * NBt + 2 * NEt + 3 * nr;
+      w[0] = s0;
+      w[1] = e0;
+      w[2] = ne - 1;
+    }
     nr++;
   }
   YM_INLINE int on_ds_done() {
     uint32_t *cl = ov + 5 * NBt;
+    if (!on) return 0;
     if (ne == 1) cl[1] = 0x80000000u;
     else if (ne >= 2) ds_order_packed(cl, ne, cl + ne, 0);
     return 0;

@@ -35,9 +35,17 @@ constexpr uint32_t DEC_NT = 256, DEC_STAGE = 16384, DEC_OVF = 1024; // overflow 
 constexpr uint32_t REC_WORDS = 6;
 constexpr uint32_t REC_UNSUP = 1u << 8, REC_BIGDS = 1u << 9, REC_SLOW = 1u << 14, REC_OVF = 1u << 15;
 constexpr uint32_t REC_EMPTY = 0, REC_BLOCK = 1, REC_DS = 2, REC_COMPLEX = 3;
-// huge: [count, bump, -, -, u64 list of HUGE_LIST update indices]; huge_cap: overflow words
-// after the k_decode workgroups' DEC_OVF words for the updates k_decode_huge decodes
-constexpr uint32_t HUGE_MIN = 2048, HUGE_LIST = 4096;
+// huge: [count, exact-walker count, u64 overflow bump, u64 list of HUGE_LIST update indices];
+// huge_cap: overflow words after the k_decode workgroups' DEC_OVF words for the long updates
+constexpr uint32_t HUGE_LIST = 65536;
+// an update k_decode could not stage: >= LP_MIN_LEN bytes -> the parallel parse (ylong.hip),
+// shorter ones -> k_decode_exact's later staging rounds
+constexpr uint32_t LP_MIN_LEN = 8192;
+// k_decode workgroups with staged updates for the exact walk (k_decode_exact): count at word
+// EXQ_COUNT of `huge`, then (workgroup, overflow words used) pairs, one per decode workgroup
+constexpr uint32_t EXQ_COUNT = 4 + 2 * HUGE_LIST, EXQ_LIST = EXQ_COUNT + 4;
+inline uint64_t huge_bytes(uint64_t n_updates) { return 4ull * EXQ_LIST + 8 * ((n_updates + DEC_NT - 1) / DEC_NT + 1); }
+constexpr uint32_t REC_STAGED = 1u << 17; // with REC_SLOW: walked exactly by k_decode_exact (LDS stage)
 // REC_COMPLEX record written by the parallel long-update parse (ylong.hip) for an update of one
 // client section without Skips, zero-length GC blocks, panicking splits or unsupported content,
 // and <= 1 DeleteSet entry; w5 = its LP entry + 1 (grid paths for single-update documents)
@@ -91,7 +99,9 @@ struct LsArgs {
   const uint64_t *sv_off, *sv_end;
   uint32_t *g;             // LSG_WORDS per document
   uint64_t *bsz, *boff;    // [NB], [NB + 1]
-  uint64_t *rsz, *roff;    // [NR], [NR + 1]
+  uint64_t *rsz, *roff;    // [NR], [NR + 1] (merge: run starts, run indices)
+  uint64_t *rsz2, *roff2;  // merge: [NR], [NR + 1] run sizes, offsets
+  uint32_t *rstart, *rend; // merge: [NR] run starts / ends
   uint64_t *scan_tmp;
   // merge: the document's slot in the output arena; diff / SV: the packed output (after the scan)
   uint8_t *out;
@@ -109,7 +119,8 @@ void launch_ls_collect(const LpArgs &a, uint32_t *list, hipStream_t s);
 // phase 0: checks, sizes, scans, totals (merge: also the write); phase 1 (diff / SV): the write
 void launch_ls_doc(const LsArgs &a, int phase, hipStream_t s);
 void launch_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_updates, uint32_t *rec, uint32_t *ovf,
-                   uint32_t *huge, uint32_t huge_cap, hipStream_t s, const LpArgs *lp = nullptr);
+                   uint32_t *huge, uint32_t huge_cap, hipStream_t s, const LpArgs *lp = nullptr, uint32_t v1x = 0,
+                   uint64_t *dbg = nullptr);
 
 // LDS capacities of the one-workgroup-per-document fast path (per document)
 struct FastCaps {
@@ -128,6 +139,7 @@ struct FastOut {
                     // tiny documents (FastCaps.in_cap / u_cap), [6] k_lean -> fast path,
                     // [7..13] k_lean hand-over reasons
   unsigned long long *lean_total = nullptr; // k_lean output bytes: 64 partial sums, 8 words apart
+  uint32_t *big_list = nullptr; // [n_docs]: the documents handed to path 2, in npath[2] order
 };
 size_t fast_lds_bytes(const FastCaps &c);
 // one wavefront per document for the common editor shape (ymerge_lean.hip): writes the
@@ -179,10 +191,11 @@ void launch_compact(const BatchIn &b, const FastOut &o, uint32_t *hdr, const uin
                     uint32_t lpw, hipStream_t s);
 
 // documents over the fast path's LDS capacities (path == 2): tiled, HBM scratch
+// over o.big_list[0, n_list) (need[] of the other documents must be zero)
 void launch_big_count(const BatchIn &b, const FastOut &o, uint32_t *counts, uint64_t *need, uint32_t *n_big,
-                      hipStream_t s);
+                      uint32_t n_list, hipStream_t s);
 void launch_big_merge(const BatchIn &b, const uint32_t *counts, const uint64_t *scr_off, uint32_t *scratch,
-                      const FastOut &o, hipStream_t s);
+                      const FastOut &o, uint32_t n_list, hipStream_t s);
 
 // exact per-document engine; `path` (optional) restricts it to documents with path == 1
 void launch_seq_count(const BatchIn &b, const uint8_t *path, uint8_t *status, uint32_t *counts, uint64_t *need,

@@ -165,4 +165,63 @@ template <class S> YM_INLINE int fast_walk(const uint32_t *w, uint32_t start, ui
   return s.on_ds_done();
 }
 
+// Exact-walk cursor over a staged update (smwalk_update, ysm.h: same interface as WCur / LWin):
+// the cold shapes fast_walk bails on (Any / Type / Binary / Embed / Format / Doc / Move content,
+// non-ASCII text, multi-byte varints, malformed input) are walked where they are staged instead
+// of over HBM by the merge kernels.  Varints read from one 8-byte window of the stage.
+struct SCur {
+  const uint8_t *p;  // the update's first byte (in the stage)
+  uint32_t n, i;
+  const uint32_t *w; // the stage's dwords
+  uint32_t base;     // the update's byte offset in the stage
+};
+YM_INLINE uint32_t wc_byte(SCur &c, uint32_t pos) {
+  const uint32_t o = c.base + pos;
+  return (c.w[o >> 2] >> ((o & 3) * 8)) & 0xFF;
+}
+YM_INLINE void wc_ensure(SCur &, uint32_t) {}
+YM_INLINE int wc_skip(SCur &c, uint64_t len) {
+  if (len > (uint64_t)(c.n - c.i)) return E_EOS;
+  c.i += (uint32_t)len;
+  return 0;
+}
+YM_INLINE int wc_read(SCur &c, bool raw, uint32_t &v, bool &canon) {
+  if (raw) {
+    if (c.i >= c.n) return E_EOS;
+    v = wc_byte(c, c.i++);
+    return 0;
+  }
+  if (c.i + 8 <= c.n) {
+    const uint32_t o = c.base + c.i, q = o >> 2, b = (o & 3) * 8;
+    const uint64_t d0 = ((uint64_t)c.w[q + 1] << 32) | c.w[q];
+    const uint64_t d = b ? (d0 >> b) | ((uint64_t)c.w[q + 2] << (64 - b)) : d0;
+    const uint64_t stop = ~d & 0x8080808080808080ull;
+    if (stop) {
+      const uint32_t nb = ((uint32_t)__builtin_ctzll(stop) >> 3) + 1;
+      uint32_t x = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < 8; k++)
+        if (k < nb) x |= ((uint32_t)(d >> (8 * k)) & 0x7Fu) << ((7 * k) & 31);
+      const uint32_t last = (uint32_t)(d >> (8 * (nb - 1))) & 0xFF;
+      v = x;
+      canon = nb == varlen(x) && (nb != 5 || last < 16);
+      c.i += nb;
+      return 0;
+    }
+  }
+  uint32_t sh = 0, nbytes = 0, b = 0;
+  v = 0;
+  for (;;) {
+    if (c.i >= c.n) return E_EOS;
+    b = wc_byte(c, c.i++);
+    v |= (b & 0x7f) << (sh & 31);
+    sh += 7;
+    nbytes++;
+    if (b < 0x80) break;
+    if (sh > 70) return E_VARINT;
+  }
+  canon = nbytes == varlen(v) && (nbytes != 5 || b < 16);
+  return 0;
+}
+
 } // namespace ym

@@ -246,8 +246,8 @@ __global__ void __launch_bounds__(1024) k_lp_plan(LpArgs a) {
     a.g[LPG_ORDS] = 0;
     a.g[LPG_SECS] = 0;
     a.g[LPG_N] = n;
-    a.huge[1] = 0; // the exact walker's list count (k_lp_final)
-    *(unsigned long long *)(a.huge + 2) = 0; // overflow bump (64-bit: never wraps)
+    // (huge[1], the exact walker's list count, and the 64-bit overflow bump at huge[2..3] were
+    // zeroed before k_decode, whose workgroups may already have used the bump)
   }
 }
 
@@ -985,7 +985,7 @@ __global__ void __launch_bounds__(256) k_ls_size(LsArgs a) {
   const uint32_t k0 = g[LSG_K0], off = g[LSG_OFF];
   const uint32_t *rv = ls_rv(a);
   const uint8_t *ub = ls_ub(a);
-  uint32_t bad = 0, runs = 0;
+  uint32_t bad = 0;
   for (uint32_t i0 = blockIdx.x * 256; i0 < n; i0 += gridDim.x * 256) {
     const uint32_t i = i0 + threadIdx.x;
     uint32_t s0, s1;
@@ -1011,14 +1011,10 @@ __global__ void __launch_bounds__(256) k_ls_size(LsArgs a) {
       const uint32_t st = rv[3 * i], en = rv[3 * i + 1];
       const uint32_t pe = i ? rv[3 * (i - 1) + 1] : 0u;
       uint64_t sz = 0;
-      if (a.mode == 0) { // IdRange::squash (id_set.rs:129-164) of sorted, non-overlapping ranges
+      if (a.mode == 0) { // IdRange::squash (id_set.rs:129-164) of sorted, non-overlapping ranges:
+        // adjacent ranges join into runs; here 1 per run start, scanned into run indices
         if (en <= st || (i && pe > st)) bad = 1;
-        if (i == 0 || st > pe) {
-          uint32_t q = i;
-          while (q + 1 < a.NR && rv[3 * (q + 1)] == rv[3 * q + 1]) q++; // adjacent ranges join
-          sz = varlen(st) + varlen(rv[3 * q + 1] - st);
-          runs++;
-        }
+        sz = i == 0 || st > pe;
       } else { // encoded as decoded when squashed (id_set.rs:166-187, 256-266)
         if (i && st < pe) bad = 1;
         sz = varlen(st) + varlen(en - st);
@@ -1028,18 +1024,17 @@ __global__ void __launch_bounds__(256) k_ls_size(LsArgs a) {
   }
   for (int o = 32; o > 0; o >>= 1) {
     bad |= __shfl_xor(bad, o, 64);
-    runs += __shfl_xor(runs, o, 64);
   }
   if ((threadIdx.x & 63) == 0) {
     if (bad) atomicOr(&g[LSG_BAD], 1u);
-    if (runs) atomicAdd(&g[LSG_K], runs);
   }
 }
 
 __device__ __forceinline__ uint64_t ls_payload(const LsArgs &a, const uint32_t *g) {
   const uint64_t body = a.mode == 2 ? 0 : a.boff[a.NB];
-  const uint32_t k = a.mode == 0 ? g[LSG_K] : a.NR;
-  const uint64_t ds = a.mode == 2 ? 0 : a.NE == 0 ? 1 : varlen(1) + varlen(a.ov[5 * a.NB]) + varlen(k) + a.roff[a.NR];
+  const uint32_t k = a.mode == 0 ? (uint32_t)a.roff[a.NR] : a.NR; // merge: runs
+  const uint64_t rb = a.mode == 0 ? a.roff2[a.NR] : a.roff[a.NR];  // range bytes
+  const uint64_t ds = a.mode == 2 ? 0 : a.NE == 0 ? 1 : varlen(1) + varlen(a.ov[5 * a.NB]) + varlen(k) + rb;
   return g[LSG_HDR] + body + ds;
 }
 __device__ __forceinline__ uint64_t ls_framed(const LsArgs &a, uint64_t p) {
@@ -1109,7 +1104,7 @@ __global__ void __launch_bounds__(256) k_ls_write(LsArgs a) {
     } else {
       w_var(v, 1);
       w_var(v, a.ov[5 * a.NB]);
-      w_var(v, a.mode == 0 ? g[LSG_K] : a.NR);
+      w_var(v, a.mode == 0 ? (uint32_t)a.roff[a.NR] : a.NR);
     }
   }
   if (a.mode == 2) return;
@@ -1119,7 +1114,7 @@ __global__ void __launch_bounds__(256) k_ls_write(LsArgs a) {
   const uint8_t *ub = ls_ub(a);
   uint8_t *blocks = base + g[LSG_HDR];
   uint8_t *ds = blocks + a.boff[a.NB] +
-                (a.NE == 0 ? 1 : varlen(1) + varlen(a.ov[5 * a.NB]) + varlen(a.mode == 0 ? g[LSG_K] : a.NR));
+                (a.NE == 0 ? 1 : varlen(1) + varlen(a.ov[5 * a.NB]) + varlen(a.mode == 0 ? (uint32_t)a.roff[a.NR] : a.NR));
   for (uint32_t i0 = blockIdx.x * 256; i0 < n; i0 += gridDim.x * 256) {
     const uint32_t i = i0 + threadIdx.x;
     uint32_t s0, s1;
@@ -1139,19 +1134,37 @@ __global__ void __launch_bounds__(256) k_ls_write(LsArgs a) {
         for (uint32_t q = 0; q < nb; q++) w.p[q] = src[q];
       }
     }
-    if (i < a.NR && a.rsz[i]) {
-      const uint32_t st = rv[3 * i];
-      uint32_t en = rv[3 * i + 1];
-      if (a.mode == 0) {
-        uint32_t q = i;
-        while (q + 1 < a.NR && rv[3 * (q + 1)] == rv[3 * q + 1]) q++;
-        en = rv[3 * q + 1];
+    if (a.mode == 0) { // run i (< the run count)
+      if (i < a.NR && i < a.roff[a.NR]) {
+        Writer w{ds + a.roff2[i], 0};
+        w_var(w, a.rstart[i]);
+        w_var(w, a.rend[i] - a.rstart[i]);
       }
+    } else if (i < a.NR) {
+      const uint32_t st = rv[3 * i];
       Writer w{ds + a.roff[i], 0};
       w_var(w, st);
-      w_var(w, en - st);
+      w_var(w, rv[3 * i + 1] - st);
     }
   }
+}
+
+// merge: lane per range -> the runs' starts and ends at their run indices (run starts scanned),
+// then lane per run -> its encoded size
+__global__ void __launch_bounds__(256) k_ls_runs(LsArgs a) {
+  if (a.g[LSG_BAD]) return;
+  const uint32_t *rv = ls_rv(a);
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < a.NR; i += gridDim.x * 256) {
+    const uint32_t st = rv[3 * i], en = rv[3 * i + 1];
+    const bool f = i == 0 || st > rv[3 * (i - 1) + 1], last = i + 1 == a.NR || rv[3 * (i + 1)] > en;
+    if (f) a.rstart[a.roff[i]] = st;
+    if (last) a.rend[a.roff[i] + (f ? 1 : 0) - 1] = en;
+  }
+}
+__global__ void __launch_bounds__(256) k_ls_runsize(LsArgs a) {
+  const uint32_t K = a.g[LSG_BAD] ? 0u : (uint32_t)a.roff[a.NR];
+  for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < a.NR; k += gridDim.x * 256)
+    a.rsz2[k] = k < K ? varlen(a.rstart[k]) + varlen(a.rend[k] - a.rstart[k]) : 0u;
 }
 
 void launch_ls_doc(const LsArgs &a, int phase, hipStream_t s) {
@@ -1163,6 +1176,14 @@ void launch_ls_doc(const LsArgs &a, int phase, hipStream_t s) {
       hipLaunchKernelGGL(k_ls_size, dim3(gr), dim3(256), 0, s, a);
       launch_scan_u64(a.bsz, a.boff, a.NB, a.scan_tmp, s);
       launch_scan_u64(a.rsz, a.roff, a.NR, a.scan_tmp, s);
+      if (a.mode == 0 && a.NR) {
+        const uint32_t gn = (a.NR + 255) / 256 < 1024 ? (a.NR + 255) / 256 : 1024;
+        hipLaunchKernelGGL(k_ls_runs, dim3(gn), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_ls_runsize, dim3(gn), dim3(256), 0, s, a);
+        launch_scan_u64(a.rsz2, a.roff2, a.NR, a.scan_tmp, s);
+      } else if (a.mode == 0) {
+        launch_scan_u64(a.rsz2, a.roff2, 0, a.scan_tmp, s); // (roff2[0] = 0)
+      }
     }
     hipLaunchKernelGGL(k_ls_total, dim3(1), dim3(64), 0, s, a);
     if (a.mode == 0) hipLaunchKernelGGL(k_ls_write, dim3(gr), dim3(256), 0, s, a);

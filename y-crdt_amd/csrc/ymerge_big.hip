@@ -122,9 +122,9 @@ __device__ inline void big_uniform(BigMem &m) {
 template <int NT>
 __global__ void __launch_bounds__(NT) k_big_count(BatchIn b, uint8_t *path, uint8_t *status, uint64_t *out_start,
                                                   uint64_t *out_len, uint32_t *counts, uint64_t *need,
-                                                  uint32_t *n_big, uint32_t *npath) {
+                                                  uint32_t *n_big, uint32_t *npath, const uint32_t *list) {
   ym_set_grammar(b.v1x);
-  const uint32_t d = blockIdx.x;
+  const uint32_t d = list[blockIdx.x];
   if (d >= b.n_docs) return;
   const uint32_t t = threadIdx.x;
   if (path[d] != 2) {
@@ -718,7 +718,7 @@ template <int NT, int OCC>
 __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t *counts, const uint64_t *scr_off,
                                                        uint32_t *scratch, FastOut o) {
   ym_set_grammar(b.v1x);
-  const uint32_t d = blockIdx.x;
+  const uint32_t d = o.big_list[blockIdx.x];
   if (d >= b.n_docs || o.path[d] != 2) return;
   __shared__ BigShared<NT> S;
   const uint32_t t = threadIdx.x;
@@ -1667,22 +1667,22 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
 
 // ------------------------------------------------------------------ launchers
 void launch_big_count(const BatchIn &b, const FastOut &o, uint32_t *counts, uint64_t *need, uint32_t *n_big,
-                      hipStream_t s) {
-  if (!b.n_docs) return;
-  hipLaunchKernelGGL((k_big_count<256>), dim3(b.n_docs), dim3(256), 0, s, b, o.path, o.status, o.out_start,
-                     o.out_len, counts, need, n_big, o.npath);
+                      uint32_t n_list, hipStream_t s) {
+  if (!b.n_docs || !n_list) return;
+  hipLaunchKernelGGL((k_big_count<256>), dim3(n_list), dim3(256), 0, s, b, o.path, o.status, o.out_start,
+                     o.out_len, counts, need, n_big, o.npath, (const uint32_t *)o.big_list);
 }
 void launch_big_merge(const BatchIn &b, const uint32_t *counts, const uint64_t *scr_off, uint32_t *scratch,
-                      const FastOut &o, hipStream_t s) {
-  if (!b.n_docs) return;
+                      const FastOut &o, uint32_t n_list, hipStream_t s) {
+  if (!b.n_docs || !n_list) return;
   // two 512-lane workgroups per CU (4 waves per SIMD at 128 VGPRs, 2 x 68 KB of LDS): twice the
   // documents in flight of one 1024-lane workgroup per CU (C4: tiled 9.05 -> 6.81 ms);
   // env YMERGE_BIG_NT=1024 selects the single-workgroup build (A/B)
   static const int nt = getenv("YMERGE_BIG_NT") ? atoi(getenv("YMERGE_BIG_NT")) : 512;
   if (nt == 1024)
-    hipLaunchKernelGGL((k_big_merge<1024, 4>), dim3(b.n_docs), dim3(1024), 0, s, b, counts, scr_off, scratch, o);
+    hipLaunchKernelGGL((k_big_merge<1024, 4>), dim3(n_list), dim3(1024), 0, s, b, counts, scr_off, scratch, o);
   else
-    hipLaunchKernelGGL((k_big_merge<512, 4>), dim3(b.n_docs), dim3(512), 0, s, b, counts, scr_off, scratch, o);
+    hipLaunchKernelGGL((k_big_merge<512, 4>), dim3(n_list), dim3(512), 0, s, b, counts, scr_off, scratch, o);
 }
 
 } // namespace ym

@@ -104,10 +104,10 @@ __host__ __device__ inline FastLayout fast_layout(const FastCaps &c) {
 // 8 workgroups per CU (8 waves per SIMD): <= 64 VGPRs and < 20 KB of LDS (the second-walk
 // list keeps 16-bit lane / count fields)
 __global__ void __launch_bounds__(DEC_NT, 8) k_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_upd,
-                                                      uint32_t *rec, uint32_t *ovf, uint32_t *huge) {
+                                                      uint32_t *rec, uint32_t *ovf, uint32_t *huge, uint32_t v1x) {
   __shared__ __align__(16) uint32_t stage[DEC_STAGE / 4 + 4];
-  __shared__ uint32_t ovf_top, n_cx;
-  ym_set_grammar(0); // fast_walk bails on every content it does not restate; v1 by construction
+  __shared__ uint32_t ovf_top, n_cx, n_sl;
+  ym_set_grammar(v1x); // (fast_walk bails on every content it does not restate)
   __shared__ uint32_t cx_at[DEC_NT];
   __shared__ uint16_t cx_lane[DEC_NT], cx_nb[DEC_NT], cx_ne[DEC_NT];
   const uint64_t g0 = (uint64_t)blockIdx.x * DEC_NT;
@@ -134,6 +134,7 @@ __global__ void __launch_bounds__(DEC_NT, 8) k_decode(const uint8_t *bytes, cons
   if (t == 0) {
     ovf_top = 0;
     n_cx = 0;
+    n_sl = 0;
   }
   __syncthreads();
   if (i < n_upd) {
@@ -145,11 +146,13 @@ __global__ void __launch_bounds__(DEC_NT, 8) k_decode(const uint8_t *bytes, cons
     s.ubase = 0;
     const bool staged = a1 - sbase <= 4 * nd;
     const int e = staged ? fast_walk(stage, (uint32_t)(a0 - sbase), ulen, s) : -1;
-    if (!staged && ulen >= HUGE_MIN) { // a long update: k_decode_huge walks it (a wavefront, LDS window)
+    if (!staged && ulen >= LP_MIN_LEN) { // a long update: the parallel parse (ylong.hip) takes it
       const uint32_t k = atomicAdd(&huge[0], 1u);
       if (k < HUGE_LIST) ((uint64_t *)(huge + 4))[k] = i;
+    } else if (e < 0) { // a shape the fast walk does not restate, or past the stage:
+      atomicAdd(&n_sl, 1u); // k_decode_exact (record REC_SLOW | REC_STAGED)
     }
-    uint32_t w0 = REC_SLOW, w1 = 0, w2 = 0, w3 = 0, w4 = 0, w5 = 0;
+    uint32_t w0 = staged || ulen < LP_MIN_LEN ? REC_SLOW | REC_STAGED : REC_SLOW, w1 = 0, w2 = 0, w3 = 0, w4 = 0, w5 = 0;
     if (e >= 0) rec_pack(s, e, w0, w1, w2, w3, w4, w5);
     if (e == 0 && ((w0 >> 10) & 3) == REC_COMPLEX && !s.big_ds) {
       // multi-record update: its records go to this workgroup's overflow words (LDS bump
@@ -157,7 +160,10 @@ __global__ void __launch_bounds__(DEC_NT, 8) k_decode(const uint8_t *bytes, cons
       // walks the update again
       const uint32_t need = 5 * s.nb + 2 * s.ne + 3 * s.nr;
       const uint32_t off = need <= DEC_OVF ? atomicAdd(&ovf_top, need) : DEC_OVF;
-      if (off + need <= DEC_OVF) {
+      if (off + need > DEC_OVF) { // no room here: k_decode_exact walks it (global overflow words)
+        w0 = REC_SLOW | REC_STAGED;
+        atomicAdd(&n_sl, 1u);
+      } else {
         const uint32_t at = blockIdx.x * DEC_OVF + off;
         w0 |= REC_OVF;
         w4 = at;
@@ -174,6 +180,14 @@ __global__ void __launch_bounds__(DEC_NT, 8) k_decode(const uint8_t *bytes, cons
     o[2] = make_uint2(w4, w5);
   }
   __syncthreads();
+  // the staged updates the fast walk left: k_decode_exact walks them exactly over the same stage
+  // (a kernel of its own: the exact walk's registers would halve this kernel's occupancy)
+  if (t == 0 && n_sl) {
+    const uint32_t k = atomicAdd(&huge[EXQ_COUNT], 1u);
+    uint32_t *e = huge + EXQ_LIST + 2 * k;
+    e[0] = blockIdx.x;
+    e[1] = ovf_top; // (the exact walks continue the workgroup's overflow allocation)
+  }
   // second walk of the multi-record updates, packed onto the first lanes: a wave runs it
   // only when it holds one of them (a few percent of an editor's updates), instead of every
   // wave whose lanes happen to include one
@@ -182,6 +196,133 @@ __global__ void __launch_bounds__(DEC_NT, 8) k_decode(const uint8_t *bytes, cons
     const uint64_t a0 = upd_off[j], a1 = upd_off[j + 1];
     OvfFill f{ovf + cx_at[q], cx_nb[q], cx_ne[q], 0, 0, 0};
     fast_walk(stage, (uint32_t)(a0 - sbase), (uint32_t)(a1 - a0), f);
+  }
+}
+
+// The workgroups of k_decode that left updates to the exact walk (listed with their overflow
+// bump): k_decode's 16 KB stage again, and further stages from the first update still pending
+// (the updates past the first stage).  The pending updates of a stage are walked exactly (ysm.h
+// over the stage) one per wavefront, all 64 lanes in lockstep: the state-machine walk of 64
+// different updates on 64 lanes diverges at every step (a tile of rich-content updates took
+// ~17 ms that way), one walk in lockstep does not.  Records and overflow words are written as
+// k_decode writes them (lane 0).
+// overflow words past a workgroup's DEC_OVF: from the long-update region's 64-bit bump
+// (huge[2..3]); UINT32_MAX when that is full too
+__device__ __forceinline__ uint32_t ovf_global(uint32_t *huge, uint32_t need, uint32_t huge_base, uint64_t huge_cap) {
+  const uint64_t at = atomicAdd((unsigned long long *)(huge + 2), (unsigned long long)need);
+  return at + need <= huge_cap ? huge_base + (uint32_t)at : 0xFFFFFFFFu;
+}
+
+constexpr uint32_t EX_NT = 1024, EX_NW = EX_NT / 64;
+__global__ void __launch_bounds__(EX_NT) k_decode_exact(const uint8_t *bytes, const uint64_t *upd_off,
+                                                       uint64_t n_upd, uint32_t *rec, uint32_t *ovf,
+                                                       uint32_t *huge, uint32_t v1x, uint32_t huge_base,
+                                                       uint64_t huge_cap, uint64_t *dbg) {
+  __shared__ __align__(16) uint32_t stage[DEC_STAGE / 4 + 4];
+  __shared__ uint32_t ovf_top, n_sl, n_go;
+  __shared__ unsigned long long s_next, s_max;
+  __shared__ uint16_t sl_lane[DEC_NT], go_lane[DEC_NT];
+  ym_set_grammar(v1x);
+  const uint32_t t = threadIdx.x, wv = t >> 6, lane = t & 63, ntiles = huge[EXQ_COUNT];
+  for (uint32_t k = blockIdx.x; k < ntiles; k += gridDim.x) {
+    const uint32_t b = huge[EXQ_LIST + 2 * k];
+    const uint64_t g0 = (uint64_t)b * DEC_NT;
+    const uint64_t rl = n_upd - g0 < DEC_NT ? n_upd - g0 : DEC_NT;
+    const uint64_t A = upd_off[g0], E = upd_off[g0 + rl];
+    const uint64_t tk0 = dbg ? __builtin_amdgcn_s_memtime() : 0;
+    uint32_t nround = 0;
+    __syncthreads();
+    if (t == 0) {
+      ovf_top = huge[EXQ_LIST + 2 * k + 1];
+      n_sl = 0;
+      s_max = 0;
+    }
+    __syncthreads();
+    const uint64_t i = g0 + t;
+    if (t < rl && (rec[i * REC_WORDS] & (REC_SLOW | REC_STAGED)) == (REC_SLOW | REC_STAGED))
+      sl_lane[atomicAdd(&n_sl, 1u)] = (uint16_t)t;
+    __syncthreads();
+    uint64_t sbase = A & ~15ull;
+    for (uint32_t round = 0; round < DEC_NT; round++) { // (each round takes >= 1 pending update)
+      uint64_t n16 = (E - sbase + 15) >> 4;
+      if (n16 > DEC_STAGE / 16) n16 = DEC_STAGE / 16;
+      const uint64_t wend = sbase + 16 * n16;
+      __syncthreads();
+      for (uint32_t q = t; q < n16; q += EX_NT) ((uint4 *)stage)[q] = ((const uint4 *)(bytes + sbase))[q];
+      if (t == 0) {
+        n_go = 0;
+        s_next = ~0ull;
+      }
+      __syncthreads();
+      // the pending updates inside this stage go; the first one past it starts the next stage
+      for (uint32_t q = t; q < n_sl; q += EX_NT) {
+        const uint32_t ul = sl_lane[q];
+        if (ul == 0xFFFF) continue;
+        const uint64_t a0 = upd_off[g0 + ul], a1 = upd_off[g0 + ul + 1];
+        if (a0 >= sbase && a1 <= wend) {
+          go_lane[atomicAdd(&n_go, 1u)] = (uint16_t)ul;
+          sl_lane[q] = 0xFFFF;
+        } else {
+          atomicMin(&s_next, (unsigned long long)a0);
+        }
+      }
+      __syncthreads();
+      nround++;
+      for (uint32_t q = wv; q < n_go; q += EX_NW) { // one update per wavefront (uniform in it)
+        const uint64_t tw0 = dbg ? __builtin_amdgcn_s_memtime() : 0;
+        const uint64_t j = g0 + go_lane[q];
+        const uint64_t a0 = upd_off[j], a1 = upd_off[j + 1];
+        RegSink s;
+        s.nb = s.ne = s.nr = 0;
+        s.unsupported = s.big_ds = false;
+        s.ubase = 0;
+        const uint32_t base = (uint32_t)(a0 - sbase), len = (uint32_t)(a1 - a0);
+        SCur c{(const uint8_t *)stage + base, len, 0, stage, base};
+        const int e = smwalk_update(c, s);
+        uint32_t w0, w1, w2, w3, w4, w5;
+        rec_pack(s, e, w0, w1, w2, w3, w4, w5);
+        if (e == 0 && ((w0 >> 10) & 3) == REC_COMPLEX && !s.big_ds) {
+          const uint32_t need = 5 * s.nb + 2 * s.ne + 3 * s.nr;
+          uint32_t at = 0;
+          if (lane == 0) {
+            const uint32_t off = need <= DEC_OVF ? atomicAdd(&ovf_top, need) : DEC_OVF;
+            at = off + need <= DEC_OVF ? b * DEC_OVF + off : ovf_global(huge, need, huge_base, huge_cap);
+          }
+          at = (uint32_t)__builtin_amdgcn_readfirstlane((int)at);
+          if (at != 0xFFFFFFFFu) { // second walk: the overflow words (lane 0 writes)
+            OvfFill f{ovf + at, s.nb, s.ne, 0, 0, 0};
+            f.on = lane == 0;
+            SCur c2{(const uint8_t *)stage + base, len, 0, stage, base};
+            smwalk_update(c2, f);
+            w0 |= REC_OVF;
+            w4 = at;
+          } else {
+            w0 = REC_SLOW; // no overflow room: the merge kernels walk it
+            w1 = w2 = w3 = w4 = w5 = 0;
+          }
+        }
+        if (lane == 0) {
+          uint2 *o = (uint2 *)(rec + j * REC_WORDS);
+          o[0] = make_uint2(w0, w1);
+          o[1] = make_uint2(w2, w3);
+          o[2] = make_uint2(w4, w5);
+          if (dbg) atomicMax(&s_max, ((__builtin_amdgcn_s_memtime() - tw0) << 24) | (j & 0xFFFFFF));
+        }
+      }
+      __syncthreads();
+      if (s_next == ~0ull) break; // (uniform)
+      sbase = s_next & ~15ull;
+    }
+    if (dbg && t == 0) { // diagnostic (env YMERGE_DECODE_DBG): tile, pending, rounds, cycles, slowest walk
+      uint64_t *o = dbg + 8 * (size_t)k;
+      o[0] = b;
+      o[1] = n_sl;
+      o[2] = nround;
+      o[3] = __builtin_amdgcn_s_memtime() - tk0;
+      o[4] = s_max >> 24;
+      o[5] = s_max & 0xFFFFFF;
+      o[6] = E - A;
+    }
   }
 }
 
@@ -246,12 +387,16 @@ __global__ void __launch_bounds__(64) k_decode_huge(const uint8_t *bytes, const 
 // given, the exact lockstep walk for the ones it leaves (errors, bounds); without it every listed
 // update takes the exact walk
 void launch_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_updates, uint32_t *rec, uint32_t *ovf,
-                   uint32_t *huge, uint32_t huge_cap, hipStream_t s, const LpArgs *lp) {
+                   uint32_t *huge, uint32_t huge_cap, hipStream_t s, const LpArgs *lp, uint32_t v1x, uint64_t *dbg) {
   if (!n_updates) return;
   const uint64_t nwg = (n_updates + DEC_NT - 1) / DEC_NT;
   hipMemsetAsync(huge, 0, 16, s);
-  hipLaunchKernelGGL(k_decode, dim3((unsigned)nwg), dim3(DEC_NT), 0, s, bytes, upd_off, n_updates, rec, ovf, huge);
+  hipMemsetAsync(huge + EXQ_COUNT, 0, 4, s);
+  hipLaunchKernelGGL(k_decode, dim3((unsigned)nwg), dim3(DEC_NT), 0, s, bytes, upd_off, n_updates, rec, ovf, huge,
+                     v1x);
   const uint32_t base = (uint32_t)(nwg * DEC_OVF);
+  hipLaunchKernelGGL(k_decode_exact, dim3((unsigned)(nwg < 2048 ? nwg : 2048)), dim3(EX_NT), 0, s, bytes, upd_off,
+                     n_updates, rec, ovf, huge, v1x, (uint32_t)(nwg * DEC_OVF), (uint64_t)huge_cap, dbg);
   if (lp) {
     LpArgs a = *lp;
     a.bytes = bytes;
@@ -266,7 +411,7 @@ void launch_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_upd
                        (const uint32_t *)(huge + 1), (const uint64_t *)a.fb, base, (uint64_t)huge_cap, a.v1x);
   } else {
     hipLaunchKernelGGL(k_decode_huge, dim3(64), dim3(64), 0, s, bytes, upd_off, rec, ovf, huge, (const uint32_t *)huge,
-                       (const uint64_t *)(huge + 4), base, (uint64_t)huge_cap, 0u);
+                       (const uint64_t *)(huge + 4), base, (uint64_t)huge_cap, v1x);
   }
 }
 
@@ -307,7 +452,8 @@ __global__ void __launch_bounds__(NT, 3) k_fast_merge(BatchIn b, FastCaps caps, 
   // LDS capacities only -> the tiled HBM-scratch kernel (ymerge_big.hip)
   auto handover = [&](uint8_t p = 1) {
     if (t == 0) {
-      atomicAdd(&o.npath[p], 1u);
+      const uint32_t k = atomicAdd(&o.npath[p], 1u);
+      if (p == 2 && o.big_list) o.big_list[k] = d; // (the tiled kernel's launch list)
       o.path[d] = p;
       o.status[d] = 0;
       o.out_len[d] = 0;

@@ -73,6 +73,7 @@ struct ymerge_ctx {
   DevBuf status, path, out_start, out_len, pack_off, counts, need, scr_off, scratch, sizes, spill_off, scan_tmp;
   DevBuf arena, packed, counter, stamps, plan_small, plan_big, rec, ovf, big_scratch, lean_scr, lean_tot, cscr;
   DevBuf gs_list, gs1, gs2; // long single-client documents (ygiant.hip)
+  DevBuf big_list;          // documents handed to the tiled kernel (k_fast_merge), its launch list
   DevBuf huge;              // k_decode's list of long updates, overflow bump counter
   DevBuf lp;                // the parallel parse of long updates (ylong.hip): scratch
   bool long_parse = true;   // env YMERGE_LONG_PARSE=0: every long update takes the exact walk
@@ -170,7 +171,7 @@ extern "C" void ymerge_ctx_destroy(ymerge_ctx *c) {
                     &c->sync_end, &c->sync_st, &c->rec, &c->ovf, &c->status, &c->path,
                     &c->out_start, &c->out_len, &c->pack_off, &c->counts, &c->need, &c->scr_off, &c->scratch,
                     &c->sizes, &c->spill_off, &c->scan_tmp, &c->arena, &c->packed, &c->counter, &c->stamps,
-                    &c->plan_small, &c->plan_big, &c->big_scratch, &c->lean_scr, &c->lean_tot, &c->cscr, &c->gs_list, &c->gs1, &c->gs2, &c->huge, &c->lp, &c->ls_list, &c->ls_scr, &c->ls_done, &c->ls_ovf, &c->lean_ord, &c->lean_dbg, &c->plan_wlist, &c->v2x, &c->v2x_sz, &c->v2x_off, &c->v2_ust,
+                    &c->plan_small, &c->plan_big, &c->big_scratch, &c->lean_scr, &c->lean_tot, &c->cscr, &c->gs_list, &c->gs1, &c->gs2, &c->big_list, &c->huge, &c->lp, &c->ls_list, &c->ls_scr, &c->ls_done, &c->ls_ovf, &c->lean_ord, &c->lean_dbg, &c->plan_wlist, &c->v2x, &c->v2x_sz, &c->v2x_off, &c->v2_ust,
                     &c->v2_out, &c->v2_osz, &c->v2_ooff, &c->v2_svoff, &c->v2_svend, &c->v2_pre})
     b->release();
   if (c->h_pinned) hipHostFree(c->h_pinned);
@@ -421,7 +422,7 @@ struct LsEntry {
   uint64_t u;
 };
 static uint64_t ls_scratch_words(const LsEntry &e) {
-  return 16 + 2 * (2ull * e.NB + 2 + 2ull * e.NR + 2 + ym::scan_tmp_elems(std::max(e.NB, e.NR)) + 2) + 16;
+  return 16 + 2 * (2ull * e.NB + 2 + 4ull * e.NR + 4 + ym::scan_tmp_elems(std::max(e.NB, e.NR)) + 2 + e.NR + 1) + 16;
 }
 static std::vector<LsEntry> ls_entries(const uint32_t *w) {
   std::vector<LsEntry> v;
@@ -445,7 +446,11 @@ static void ls_bind(ym::LsArgs &a, const LsEntry &e, uint32_t *scr) {
   a.boff = q + e.NB;
   a.rsz = a.boff + e.NB + 2;
   a.roff = a.rsz + e.NR;
-  a.scan_tmp = a.roff + e.NR + 2;
+  a.rsz2 = a.roff + e.NR + 2;
+  a.roff2 = a.rsz2 + e.NR;
+  a.scan_tmp = a.roff2 + e.NR + 2;
+  a.rstart = (uint32_t *)(a.scan_tmp + ym::scan_tmp_elems(std::max(e.NB, e.NR)) + 2);
+  a.rend = a.rstart + e.NR;
 }
 
 // One batch: fast path for every document, exact engine for the documents it hands over.
@@ -467,7 +472,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
       (c->fast_threads && (!c->rec.ensure((n_updates + 1) * ym::REC_WORDS * 4) ||
                            !c->ovf.ensure(((n_updates + ym::DEC_NT - 1) / ym::DEC_NT + 1) * ym::DEC_OVF * 4 +
                                           (uint64_t)huge_words(n_bytes) * 4) ||
-                           !c->huge.ensure(16 + 8 * ym::HUGE_LIST))))
+                           !c->huge.ensure(ym::huge_bytes(n_updates)))))
     return DEV_FAIL();
   b.rec = c->rec.as<uint32_t>();
   b.ovf = c->ovf.as<uint32_t>();
@@ -483,7 +488,9 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     stamps = c->stamps.as<uint64_t>();
     c->stamps_docs = n_docs;
   }
+  if (!c->big_list.ensure(nn * 4)) return DEV_FAIL();
   ym::FastOut fo{arena, ostart, olen, status, path, stamps, nullptr, c->counter.as<uint32_t>() + 4};
+  fo.big_list = c->big_list.as<uint32_t>();
   if (getenv("YMERGE_LEAN_DEBUG") && c->lean_dbg.ensure(nn * 32)) {
     hipMemsetAsync(c->lean_dbg.p, 0xFF, nn * 32, c->s);
     fo.dbg = c->lean_dbg.as<uint32_t>();
@@ -504,7 +511,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     hipEventRecord(c->ev[7], c->s);
     hipEventRecord(c->ev[0], c->s);
     ym::launch_decode(d_bytes, d_upd_off, n_updates, c->rec.as<uint32_t>(), c->ovf.as<uint32_t>(), c->huge.as<uint32_t>(),
-                      huge_words(n_bytes), c->s, lp_args(c, n_bytes, b.v1x));
+                      huge_words(n_bytes), c->s, lp_args(c, n_bytes, b.v1x), b.v1x);
     hipEventRecord(c->ev[5], c->s);
     decoded = true;
     const int rc = run_giant(c, b, fo, 0, (uint32_t)n_updates, 0, n_bytes);
@@ -586,9 +593,31 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   hipEventRecord(c->ev[0], c->s);
   const bool fast = c->fast_threads && n_rej > 0;
   if (fast) {
+    // diagnostic (env YMERGE_DECODE_DBG): k_decode_exact's slowest workgroups to stderr
+    static const bool ddbg = getenv("YMERGE_DECODE_DBG") != nullptr;
+    const uint64_t nwg = (n_updates + ym::DEC_NT - 1) / ym::DEC_NT;
+    uint64_t *dbg = nullptr;
+    if (ddbg && c->stamps.ensure(nwg * 64 + 64)) {
+      hipMemsetAsync(c->stamps.p, 0, nwg * 64, c->s);
+      dbg = c->stamps.as<uint64_t>();
+    }
     if (!decoded) // (the grid lane's records are still valid)
       ym::launch_decode(d_bytes, d_upd_off, n_updates, c->rec.as<uint32_t>(), c->ovf.as<uint32_t>(),
-                        c->huge.as<uint32_t>(), huge_words(n_bytes), c->s, lp_args(c, n_bytes, b.v1x));
+                        c->huge.as<uint32_t>(), huge_words(n_bytes), c->s, lp_args(c, n_bytes, b.v1x), b.v1x, dbg);
+    if (dbg) {
+      std::vector<uint64_t> h(nwg * 8);
+      hipStreamSynchronize(c->s);
+      hipMemcpy(h.data(), dbg, nwg * 64, hipMemcpyDeviceToHost);
+      std::vector<size_t> idx(nwg);
+      for (size_t q = 0; q < nwg; q++) idx[q] = q;
+      std::sort(idx.begin(), idx.end(), [&](size_t x, size_t y) { return h[8 * x + 3] > h[8 * y + 3]; });
+      for (size_t q = 0; q < std::min<size_t>(8, nwg); q++) {
+        const uint64_t *o = h.data() + 8 * idx[q];
+        fprintf(stderr, "k_decode_exact tile %lu: pending %lu rounds %lu cycles %lu slowest walk %lu (update %lu) bytes %lu\n",
+                (unsigned long)o[0], (unsigned long)o[1], (unsigned long)o[2], (unsigned long)o[3], (unsigned long)o[4],
+                (unsigned long)o[5], (unsigned long)o[6]);
+      }
+    }
     hipEventRecord(c->ev[5], c->s);
     ym::launch_fast_merge(b, c->caps, fo, c->fast_threads, c->s);
     if (hipGetLastError() != hipSuccess) return DEV_FAIL();
@@ -665,7 +694,9 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
       }
       if (hipGetLastError() != hipSuccess) return dev_err("long-document merge launch");
     }
-    ym::launch_big_count(b, fo, c->counts.as<uint32_t>(), c->need.as<uint64_t>(), c->counter.as<uint32_t>() + 2, c->s);
+    hipMemsetAsync(c->need.p, 0, (size_t)n * 8, c->s); // (k_big_count writes the listed documents' words)
+    ym::launch_big_count(b, fo, c->counts.as<uint32_t>(), c->need.as<uint64_t>(), c->counter.as<uint32_t>() + 2, n_p2,
+                         c->s);
     ym::launch_scan_u64(c->need.as<uint64_t>(), c->scr_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
     hipMemcpyAsync(c->h_pinned + 10, c->scr_off.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, c->s);
     hipMemcpyAsync(c->h_pinned + 11, c->counter.as<uint32_t>() + 2, 4, hipMemcpyDeviceToHost, c->s);
@@ -674,7 +705,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     if (n_big) {
       if (!c->big_scratch.ensure((size_t)c->h_pinned[10] * 4 + 64)) return DEV_FAIL();
       ym::launch_big_merge(b, c->counts.as<uint32_t>(), c->scr_off.as<uint64_t>(), c->big_scratch.as<uint32_t>(), fo,
-                           c->s);
+                           n_p2, c->s);
       if (hipGetLastError() != hipSuccess) return DEV_FAIL();
     }
   }

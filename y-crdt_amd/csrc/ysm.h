@@ -72,6 +72,141 @@ template <class C> YM_INLINE uint32_t wc_or(C &c, uint32_t s0, uint32_t n) {
   return hi;
 }
 
+// Content refs 3 (Binary), 7 (Type, not weak) and 8 (Any of scalars and strings), restated
+// inline on the cursor (ItemContent::decode, yrs/src/block.rs:1786-1835; Any::decode,
+// yrs/src/any.rs:37-83; TypeRef::decode, yrs/src/types/mod.rs:160-200): the out-of-line
+// parse_content_slow costs a call (register saves to scratch) per block, which dominated walks
+// of rich documents.  Returns 1 (parsed: bi.len / bi.reenc set, cursor past the content), 0
+// (not this shape: cursor restored, parse_content_slow takes it) or an error in read order.
+template <class C> YM_INLINE int sm_content_inline(C &c, uint32_t ref, BlockInfo &bi) {
+  const uint32_t c0 = c.i;
+  uint32_t v = 0;
+  bool canon = true;
+  if (ref == 3) {
+    YM_TRY(wc_read(c, false, v, canon));
+    bi.reenc |= !canon;
+    YM_TRY(wc_skip(c, v));
+    bi.len = 1;
+    return 1;
+  }
+  if (ref == 7) {
+    YM_TRY(wc_read(c, true, v, canon));
+    if (v == 7) { // weak link: parse_content_slow
+      c.i = c0;
+      return 0;
+    }
+    bi.len = 1;
+    if (v == 3) {
+      YM_TRY(wc_read(c, false, v, canon));
+      bi.reenc |= !canon;
+      return wc_skip(c, v) ? E_EOS : 1;
+    }
+    if (v <= 6 || v == 9 || v == 15) return 1;
+    return E_UNEXPECTED;
+  }
+  if (ref != 8) return 0;
+  uint32_t n;
+  YM_TRY(wc_read(c, false, n, canon));
+  if ((uint64_t)n * 24 > ALLOC_LIMIT) {
+    c.i = c0;
+    return 0;
+  }
+  bool reenc = !canon;
+  for (uint32_t k = 0; k < n; k++) {
+    uint32_t tag;
+    YM_TRY(wc_read(c, true, tag, canon));
+    switch (tag) {
+    case 127: case 126: case 121: case 120: break;
+    case 125: { // signed varint (varint.rs:262-281), canonical iff num_encode gives the same bytes
+      const uint32_t s0 = c.i;
+      uint32_t b = 0;
+      if (c.i >= c.n) return E_EOS;
+      b = wc_byte(c, c.i++);
+      uint64_t num = b & 0x3f;
+      uint32_t len = 6;
+      const bool neg = (b & 0x40) != 0;
+      if (b & 0x80) {
+        for (;;) {
+          if (c.i >= c.n) return E_EOS;
+          b = wc_byte(c, c.i++);
+          num |= (uint64_t)(b & 0x7f) << (len & 63);
+          len += 7;
+          if (b < 0x80) break;
+          if (len > 70) return E_VARINT;
+        }
+      }
+      const int64_t iv = neg ? (int64_t)(0 - num) : (int64_t)num;
+      struct Cmp {
+        C &cur;
+        uint32_t at, end;
+        bool eq;
+        __device__ void u8(uint8_t x) {
+          if (at >= end || wc_byte(cur, at) != x) eq = false;
+          at++;
+        }
+        __device__ void bytes(const uint8_t *, uint32_t) {}
+      } cmp{c, s0 - 1, c.i, true};
+      num_encode(cmp, i64_to_f64_bits(iv));
+      if (!cmp.eq || cmp.at != cmp.end) reenc = true;
+      break;
+    }
+    case 124: { // f32: canonical unless NaN or integral-safe
+      if (c.n - c.i < 4) return E_EOS;
+      uint32_t fb = 0;
+      for (uint32_t q = 0; q < 4; q++) fb = fb << 8 | wc_byte(c, c.i + q);
+      c.i += 4;
+      const uint32_t ex = (fb >> 23) & 0xFF;
+      struct Peek {
+        uint8_t first = 0;
+        bool any = false;
+        __device__ void u8(uint8_t x) {
+          if (!any) first = x;
+          any = true;
+        }
+        __device__ void bytes(const uint8_t *, uint32_t) {}
+      } pk;
+      num_encode(pk, f32_to_f64_bits(fb));
+      if ((ex == 0xFF && (fb & 0x7FFFFF)) || pk.first == 125) reenc = true;
+      break;
+    }
+    case 123: { // f64: canonical iff it stays tag 123
+      if (c.n - c.i < 8) return E_EOS;
+      uint64_t bits = 0;
+      for (uint32_t q = 0; q < 8; q++) bits = bits << 8 | wc_byte(c, c.i + q);
+      c.i += 8;
+      struct Peek {
+        uint8_t first = 0;
+        bool any = false;
+        __device__ void u8(uint8_t x) {
+          if (!any) first = x;
+          any = true;
+        }
+        __device__ void bytes(const uint8_t *, uint32_t) {}
+      } pk;
+      num_encode(pk, bits);
+      if (pk.first != 123) reenc = true;
+      break;
+    }
+    case 122:
+      if (c.n - c.i < 8) return E_EOS;
+      c.i += 8;
+      break;
+    case 119: case 116:
+      YM_TRY(wc_read(c, false, v, canon));
+      if (!canon) reenc = true;
+      YM_TRY(wc_skip(c, v));
+      break;
+    case 118: case 117: // maps / arrays: parse_content_slow from the content's start
+      c.i = c0;
+      return 0;
+    default: return E_UNEXPECTED;
+    }
+  }
+  bi.len = n;
+  bi.reenc |= reenc;
+  return 1;
+}
+
 template <class S, class C> YM_INLINE int smwalk_update(C &c, S &s) {
   uint32_t st = W_NCL;
   uint32_t ncl = 0, isec = 0, nb = 0, client = 0, clock = 0, j = 0, stored = 0, slot = 4;
@@ -246,13 +381,17 @@ template <class S, class C> YM_INLINE int smwalk_update(C &c, S &s) {
         st = W_CDEL;
       } else if (ref == 4) {
         st = W_CSTR;
-      } else { // cold content kinds: out of line, on the plain pointer
-        SlowRes r = parse_content_slow(c.p, c.n, c.i, (uint8_t)ref, bi.reenc);
-        if (r.err) return r.err;
-        c.i = r.pos;
-        bi.len = r.len;
-        bi.reenc = r.reenc;
-        bi.unsupported = r.unsupported;
+      } else {
+        const int hr = sm_content_inline(c, ref, bi);
+        if (hr > 1) return hr; // (an error code)
+        if (hr == 0) { // cold content kinds: out of line, on the plain pointer
+          SlowRes r = parse_content_slow(c.p, c.n, c.i, (uint8_t)ref, bi.reenc);
+          if (r.err) return r.err;
+          c.i = r.pos;
+          bi.len = r.len;
+          bi.reenc = r.reenc;
+          bi.unsupported = r.unsupported;
+        }
         block_end = true;
       }
     }
