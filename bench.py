@@ -332,7 +332,9 @@ def run_merge(a, rank, world, dev):
                      "k_decode_ms": ms_decode, "k_fast_merge_ms": ms_fast, "big_path_ms": ms_big,
                      "exact_path_ms": ms_exact, "docs_big_path": docs_big, "docs_exact_path": docs_exact,
                      "docs_tiny_path": docs_tiny,
-                     "alg_bytes_per_launch": alg_bytes},
+                     "alg_bytes_per_launch": alg_bytes,
+                     "stage_note": f"kernel_ms and the stage times are HIP-event means over {a.steps} "
+                                   "separate untimed steps run after the timed loop (same batch)"},
         "paths": path_stats(kstats[-1]),
         "end_to_end": None if e2e is None else {
             "value": float(allst[:, 1].sum()) / float(allst[:, 6].max()) / 1e9, "unit": "GB/s",
@@ -518,7 +520,9 @@ def run_diff(a, rank, world, dev):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic("c5"), "kernel": "k_plan+k_exec",
                      "kernel_ms": ms_pipe, "k_plan_ms": mean("ms_fast"), "replan_ms": mean("ms_exact"),
-                     "k_exec_ms": mean("ms_tail"), "alg_bytes_per_launch": alg},
+                     "k_exec_ms": mean("ms_tail"), "alg_bytes_per_launch": alg,
+                     "stage_note": f"kernel_ms and the stage times are HIP-event means over {a.steps} "
+                                   "separate untimed steps run after the timed loop (same batch)"},
         "cpu_baseline": cpu,
     }
 

@@ -41,6 +41,10 @@ constexpr uint32_t HUGE_LIST = 65536;
 // an update k_decode could not stage: >= LP_MIN_LEN bytes -> the parallel parse (ylong.hip),
 // shorter ones -> k_decode_exact's later staging rounds
 constexpr uint32_t LP_MIN_LEN = 8192;
+// a staged update of >= LP_MID_LEN bytes the fast walk cannot take goes to the parallel parse too:
+// the exact walk is one wavefront stepping serially (~1,800 cycles a varint), a 5 KB rich update
+// ~6 ms of one workgroup's time (env YMERGE_LP_MID)
+constexpr uint32_t LP_MID_LEN = 128;
 // k_decode workgroups with staged updates for the exact walk (k_decode_exact): count at word
 // EXQ_COUNT of `huge`, then (workgroup, overflow words used) pairs, one per decode workgroup
 constexpr uint32_t EXQ_COUNT = 4 + 2 * HUGE_LIST, EXQ_LIST = EXQ_COUNT + 4;
@@ -80,6 +84,7 @@ struct LpArgs {
   uint64_t *scan_tmp;
   uint32_t pcap, ccap, scap, seccap, ocap;
   uint32_t v1x;
+  uint32_t mid; // k_decode lists updates of >= mid bytes its fast walk cannot take (LP_MID_LEN)
 };
 void launch_long_decode(const LpArgs &a, hipStream_t s);
 

@@ -224,4 +224,26 @@ YM_INLINE int wc_read(SCur &c, bool raw, uint32_t &v, bool &canon) {
   return 0;
 }
 
+// The lockstep form (one update per wavefront, k_decode_exact): the same cursor, with every
+// position and value it returns made wave-uniform (readfirstlane).  The compiler then proves the
+// walk's state uniform and compiles ysm.h's state switch to scalar branches; on the plain
+// cursor the state is a VGPR, and every step ran the switch's whole exec-masked cascade
+// (~1,800 cycles a step, measured with tools/walkbench.hip).
+struct SCurU : SCur {};
+YM_INLINE uint32_t ym_uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+YM_INLINE uint32_t wc_byte(SCurU &c, uint32_t pos) { return ym_uni(wc_byte((SCur &)c, ym_uni(pos))); }
+YM_INLINE void wc_ensure(SCurU &, uint32_t) {}
+YM_INLINE int wc_skip(SCurU &c, uint64_t len) {
+  const int r = wc_skip((SCur &)c, len);
+  c.i = ym_uni(c.i);
+  return (int)ym_uni((uint32_t)r);
+}
+YM_INLINE int wc_read(SCurU &c, bool raw, uint32_t &v, bool &canon) {
+  const int r = wc_read((SCur &)c, raw, v, canon);
+  v = ym_uni(v);
+  canon = ym_uni(canon ? 1u : 0u) != 0;
+  c.i = ym_uni(c.i);
+  return (int)ym_uni((uint32_t)r);
+}
+
 } // namespace ym

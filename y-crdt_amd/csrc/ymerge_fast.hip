@@ -93,6 +93,13 @@ __host__ __device__ inline FastLayout fast_layout(const FastCaps &c) {
 }
 
 // ------------------------------------------------------------------ k_decode
+// overflow words past a workgroup's DEC_OVF: from the long-update region's 64-bit bump
+// (huge[2..3]); UINT32_MAX when that is full too
+__device__ __forceinline__ uint32_t ovf_global(uint32_t *huge, uint32_t need, uint32_t huge_base, uint64_t huge_cap) {
+  const uint64_t at = atomicAdd((unsigned long long *)(huge + 2), (unsigned long long)need);
+  return at + need <= huge_cap ? huge_base + (uint32_t)at : 0xFFFFFFFFu;
+}
+
 // One lane per update over the whole batch (updates of all documents are one
 // contiguous byte range): the workgroup stages its NT updates' bytes into LDS with
 // coalesced dword loads, every lane decodes its own update (fast_walk, branch-free
@@ -104,7 +111,8 @@ __host__ __device__ inline FastLayout fast_layout(const FastCaps &c) {
 // 8 workgroups per CU (8 waves per SIMD): <= 64 VGPRs and < 20 KB of LDS (the second-walk
 // list keeps 16-bit lane / count fields)
 __global__ void __launch_bounds__(DEC_NT, 8) k_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_upd,
-                                                      uint32_t *rec, uint32_t *ovf, uint32_t *huge, uint32_t v1x) {
+                                                      uint32_t *rec, uint32_t *ovf, uint32_t *huge, uint32_t v1x,
+                                                      uint32_t lp_min, uint32_t huge_base, uint64_t huge_cap) {
   __shared__ __align__(16) uint32_t stage[DEC_STAGE / 4 + 4];
   __shared__ uint32_t ovf_top, n_cx, n_sl;
   ym_set_grammar(v1x); // (fast_walk bails on every content it does not restate)
@@ -146,13 +154,15 @@ __global__ void __launch_bounds__(DEC_NT, 8) k_decode(const uint8_t *bytes, cons
     s.ubase = 0;
     const bool staged = a1 - sbase <= 4 * nd;
     const int e = staged ? fast_walk(stage, (uint32_t)(a0 - sbase), ulen, s) : -1;
-    if (!staged && ulen >= LP_MIN_LEN) { // a long update: the parallel parse (ylong.hip) takes it
+    // a long update (or a medium one the fast walk cannot take): the parallel parse (ylong.hip)
+    const bool lp_take = e < 0 && ulen >= lp_min;
+    if (lp_take) {
       const uint32_t k = atomicAdd(&huge[0], 1u);
       if (k < HUGE_LIST) ((uint64_t *)(huge + 4))[k] = i;
     } else if (e < 0) { // a shape the fast walk does not restate, or past the stage:
       atomicAdd(&n_sl, 1u); // k_decode_exact (record REC_SLOW | REC_STAGED)
     }
-    uint32_t w0 = staged || ulen < LP_MIN_LEN ? REC_SLOW | REC_STAGED : REC_SLOW, w1 = 0, w2 = 0, w3 = 0, w4 = 0, w5 = 0;
+    uint32_t w0 = lp_take ? REC_SLOW : REC_SLOW | REC_STAGED, w1 = 0, w2 = 0, w3 = 0, w4 = 0, w5 = 0;
     if (e >= 0) rec_pack(s, e, w0, w1, w2, w3, w4, w5);
     if (e == 0 && ((w0 >> 10) & 3) == REC_COMPLEX && !s.big_ds) {
       // multi-record update: its records go to this workgroup's overflow words (LDS bump
@@ -160,11 +170,13 @@ __global__ void __launch_bounds__(DEC_NT, 8) k_decode(const uint8_t *bytes, cons
       // walks the update again
       const uint32_t need = 5 * s.nb + 2 * s.ne + 3 * s.nr;
       const uint32_t off = need <= DEC_OVF ? atomicAdd(&ovf_top, need) : DEC_OVF;
-      if (off + need > DEC_OVF) { // no room here: k_decode_exact walks it (global overflow words)
+      // no room in the workgroup's words: the long-update region's bump (huge[2..3])
+      const uint32_t at = off + need <= DEC_OVF ? blockIdx.x * DEC_OVF + off
+                                                : ovf_global(huge, need, huge_base, huge_cap);
+      if (at == 0xFFFFFFFFu) { // none there either: k_decode_exact walks it
         w0 = REC_SLOW | REC_STAGED;
         atomicAdd(&n_sl, 1u);
       } else {
-        const uint32_t at = blockIdx.x * DEC_OVF + off;
         w0 |= REC_OVF;
         w4 = at;
         const uint32_t q = atomicAdd(&n_cx, 1u);
@@ -206,26 +218,26 @@ __global__ void __launch_bounds__(DEC_NT, 8) k_decode(const uint8_t *bytes, cons
 // different updates on 64 lanes diverges at every step (a tile of rich-content updates took
 // ~17 ms that way), one walk in lockstep does not.  Records and overflow words are written as
 // k_decode writes them (lane 0).
-// overflow words past a workgroup's DEC_OVF: from the long-update region's 64-bit bump
-// (huge[2..3]); UINT32_MAX when that is full too
-__device__ __forceinline__ uint32_t ovf_global(uint32_t *huge, uint32_t need, uint32_t huge_base, uint64_t huge_cap) {
-  const uint64_t at = atomicAdd((unsigned long long *)(huge + 2), (unsigned long long)need);
-  return at + need <= huge_cap ? huge_base + (uint32_t)at : 0xFFFFFFFFu;
-}
-
-constexpr uint32_t EX_NT = 1024, EX_NW = EX_NT / 64;
+// EX_NT 256 (one wavefront per SIMD): the lockstep walk keeps its state in registers (at 1024
+// threads its 128-VGPR budget spilled the walk's state to scratch on every step); EX_SPLIT
+// workgroups share a tile, each walking the pending updates u of it with u % EX_SPLIT == its part
+// (each stages on its own), and take overflow words from the tile's bump in the exact list (a
+// global atomic)
+constexpr uint32_t EX_NT = 256, EX_NW = EX_NT / 64, EX_SPLIT = 8;
 __global__ void __launch_bounds__(EX_NT) k_decode_exact(const uint8_t *bytes, const uint64_t *upd_off,
                                                        uint64_t n_upd, uint32_t *rec, uint32_t *ovf,
                                                        uint32_t *huge, uint32_t v1x, uint32_t huge_base,
                                                        uint64_t huge_cap, uint64_t *dbg) {
   __shared__ __align__(16) uint32_t stage[DEC_STAGE / 4 + 4];
-  __shared__ uint32_t ovf_top, n_sl, n_go;
+  __shared__ uint32_t n_sl, n_go;
   __shared__ unsigned long long s_next, s_max;
   __shared__ uint16_t sl_lane[DEC_NT], go_lane[DEC_NT];
   ym_set_grammar(v1x);
   const uint32_t t = threadIdx.x, wv = t >> 6, lane = t & 63, ntiles = huge[EXQ_COUNT];
-  for (uint32_t k = blockIdx.x; k < ntiles; k += gridDim.x) {
+  const uint32_t part = blockIdx.x % EX_SPLIT, nslot = gridDim.x / EX_SPLIT; // (grid: a multiple of EX_SPLIT)
+  for (uint32_t k = blockIdx.x / EX_SPLIT; k < ntiles; k += nslot) {
     const uint32_t b = huge[EXQ_LIST + 2 * k];
+    uint32_t *ovf_top = huge + EXQ_LIST + 2 * k + 1;
     const uint64_t g0 = (uint64_t)b * DEC_NT;
     const uint64_t rl = n_upd - g0 < DEC_NT ? n_upd - g0 : DEC_NT;
     const uint64_t A = upd_off[g0], E = upd_off[g0 + rl];
@@ -233,14 +245,13 @@ __global__ void __launch_bounds__(EX_NT) k_decode_exact(const uint8_t *bytes, co
     uint32_t nround = 0;
     __syncthreads();
     if (t == 0) {
-      ovf_top = huge[EXQ_LIST + 2 * k + 1];
       n_sl = 0;
       s_max = 0;
     }
     __syncthreads();
-    const uint64_t i = g0 + t;
-    if (t < rl && (rec[i * REC_WORDS] & (REC_SLOW | REC_STAGED)) == (REC_SLOW | REC_STAGED))
-      sl_lane[atomicAdd(&n_sl, 1u)] = (uint16_t)t;
+    for (uint32_t u = part + EX_SPLIT * t; u < rl; u += EX_SPLIT * EX_NT) // this workgroup's share of the tile
+      if ((rec[(g0 + u) * REC_WORDS] & (REC_SLOW | REC_STAGED)) == (REC_SLOW | REC_STAGED))
+        sl_lane[atomicAdd(&n_sl, 1u)] = (uint16_t)u;
     __syncthreads();
     uint64_t sbase = A & ~15ull;
     for (uint32_t round = 0; round < DEC_NT; round++) { // (each round takes >= 1 pending update)
@@ -276,8 +287,13 @@ __global__ void __launch_bounds__(EX_NT) k_decode_exact(const uint8_t *bytes, co
         s.nb = s.ne = s.nr = 0;
         s.unsupported = s.big_ds = false;
         s.ubase = 0;
-        const uint32_t base = (uint32_t)(a0 - sbase), len = (uint32_t)(a1 - a0);
-        SCur c{(const uint8_t *)stage + base, len, 0, stage, base};
+        const uint32_t base = ym_uni((uint32_t)(a0 - sbase)), len = ym_uni((uint32_t)(a1 - a0));
+        SCurU c;
+        c.p = (const uint8_t *)stage + base;
+        c.n = len;
+        c.i = 0;
+        c.w = stage;
+        c.base = base;
         const int e = smwalk_update(c, s);
         uint32_t w0, w1, w2, w3, w4, w5;
         rec_pack(s, e, w0, w1, w2, w3, w4, w5);
@@ -285,14 +301,19 @@ __global__ void __launch_bounds__(EX_NT) k_decode_exact(const uint8_t *bytes, co
           const uint32_t need = 5 * s.nb + 2 * s.ne + 3 * s.nr;
           uint32_t at = 0;
           if (lane == 0) {
-            const uint32_t off = need <= DEC_OVF ? atomicAdd(&ovf_top, need) : DEC_OVF;
+            const uint32_t off = need <= DEC_OVF ? atomicAdd(ovf_top, need) : DEC_OVF;
             at = off + need <= DEC_OVF ? b * DEC_OVF + off : ovf_global(huge, need, huge_base, huge_cap);
           }
           at = (uint32_t)__builtin_amdgcn_readfirstlane((int)at);
           if (at != 0xFFFFFFFFu) { // second walk: the overflow words (lane 0 writes)
             OvfFill f{ovf + at, s.nb, s.ne, 0, 0, 0};
             f.on = lane == 0;
-            SCur c2{(const uint8_t *)stage + base, len, 0, stage, base};
+            SCurU c2;
+            c2.p = (const uint8_t *)stage + base;
+            c2.n = len;
+            c2.i = 0;
+            c2.w = stage;
+            c2.base = base;
             smwalk_update(c2, f);
             w0 |= REC_OVF;
             w4 = at;
@@ -315,13 +336,14 @@ __global__ void __launch_bounds__(EX_NT) k_decode_exact(const uint8_t *bytes, co
     }
     if (dbg && t == 0) { // diagnostic (env YMERGE_DECODE_DBG): tile, pending, rounds, cycles, slowest walk
       uint64_t *o = dbg + 8 * (size_t)k;
-      o[0] = b;
-      o[1] = n_sl;
-      o[2] = nround;
-      o[3] = __builtin_amdgcn_s_memtime() - tk0;
-      o[4] = s_max >> 24;
-      o[5] = s_max & 0xFFFFFF;
-      o[6] = E - A;
+      if (part == 0) {
+        o[0] = b;
+        o[1] = n_sl;
+        o[2] = nround;
+        o[6] = E - A;
+      }
+      atomicMax((unsigned long long *)o + 3, (unsigned long long)(__builtin_amdgcn_s_memtime() - tk0));
+      atomicMax((unsigned long long *)o + 7, s_max);
     }
   }
 }
@@ -392,10 +414,11 @@ void launch_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_upd
   const uint64_t nwg = (n_updates + DEC_NT - 1) / DEC_NT;
   hipMemsetAsync(huge, 0, 16, s);
   hipMemsetAsync(huge + EXQ_COUNT, 0, 4, s);
+  const uint32_t lp_min = lp ? (lp->mid < LP_MIN_LEN ? lp->mid : LP_MIN_LEN) : LP_MIN_LEN;
   hipLaunchKernelGGL(k_decode, dim3((unsigned)nwg), dim3(DEC_NT), 0, s, bytes, upd_off, n_updates, rec, ovf, huge,
-                     v1x);
+                     v1x, lp_min, (uint32_t)(nwg * DEC_OVF), (uint64_t)huge_cap);
   const uint32_t base = (uint32_t)(nwg * DEC_OVF);
-  hipLaunchKernelGGL(k_decode_exact, dim3((unsigned)(nwg < 2048 ? nwg : 2048)), dim3(EX_NT), 0, s, bytes, upd_off,
+  hipLaunchKernelGGL(k_decode_exact, dim3((unsigned)(nwg < 512 ? nwg : 512) * EX_SPLIT), dim3(EX_NT), 0, s, bytes, upd_off,
                      n_updates, rec, ovf, huge, v1x, (uint32_t)(nwg * DEC_OVF), (uint64_t)huge_cap, dbg);
   if (lp) {
     LpArgs a = *lp;

@@ -77,6 +77,7 @@ struct ymerge_ctx {
   DevBuf huge;              // k_decode's list of long updates, overflow bump counter
   DevBuf lp;                // the parallel parse of long updates (ylong.hip): scratch
   bool long_parse = true;   // env YMERGE_LONG_PARSE=0: every long update takes the exact walk
+  uint32_t lp_mid = ym::LP_MID_LEN; // env YMERGE_LP_MID: staged rich updates of >= this many bytes -> parallel parse
   bool long_grid = true;    // env YMERGE_LONG_GRID=0: single long update documents take the tiled kernel / planners
   uint32_t ls_min_diff = ym::LS_MIN_DIFF; // diff / SV documents on the long-update grid path (env YMERGE_LS_MIN)
   DevBuf ls_list, ls_scr, ls_done, ls_ovf; // their list, per-document scratch, planner skip flags, records
@@ -142,6 +143,7 @@ static bool ctx_init(ymerge_ctx *c, int device) {
     c->planner = strcmp(v, "ring") == 0 ? 1u : strcmp(v, "wave") == 0 ? 2u : 0u;
   if (const char *v = getenv("YMERGE_LEAN_SCR_MAX")) c->lean_scr_max = strtoull(v, nullptr, 10);
   if (const char *v = getenv("YMERGE_LONG_PARSE")) c->long_parse = atoi(v) != 0;
+  if (const char *v = getenv("YMERGE_LP_MID")) c->lp_mid = (uint32_t)std::max(1, atoi(v));
   if (const char *v = getenv("YMERGE_LONG_GRID")) c->long_grid = atoi(v) != 0;
   if (const char *v = getenv("YMERGE_LS_MIN")) c->ls_min_diff = (uint32_t)atoi(v);
   // the fast kernel's LDS layout must fit one workgroup (160 KB on gfx950)
@@ -299,9 +301,9 @@ static bool ensure_keep(ymerge_ctx *c, DevBuf &b, size_t bytes, size_t keep) {
 }
 
 // overflow words for the long updates k_decode_huge decodes (5 per block, 2 per DeleteSet entry,
-// 3 per range: at most ~2.5 words per input byte; a batch that needs more leaves the rest on
+// 3 per range: at most ~2.5 words per input byte, <= 2 on every realistic input; a batch that needs more leaves the rest on
 // the merge kernels' walk)
-static uint32_t huge_words(uint64_t n_bytes) { return (uint32_t)std::min<uint64_t>(n_bytes / 2 + 65536, 1u << 24); }
+static uint32_t huge_words(uint64_t n_bytes) { return (uint32_t)std::min<uint64_t>(2 * n_bytes + 65536, 1u << 26); }
 
 // Scratch of the parallel long-update parse, sized from the batch's bytes (long updates total at
 // most n_bytes; past LP_PMAX positions the rest take the exact walk).  Null when disabled or the
@@ -345,6 +347,7 @@ static const ym::LpArgs *lp_args(ymerge_ctx *c, uint64_t n_bytes, uint32_t v1x) 
   a.seccap = (uint32_t)seccap;
   a.ocap = (uint32_t)ocap;
   a.v1x = v1x;
+  a.mid = c->lp_mid;
   return &a;
 }
 
@@ -614,8 +617,8 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
       for (size_t q = 0; q < std::min<size_t>(8, nwg); q++) {
         const uint64_t *o = h.data() + 8 * idx[q];
         fprintf(stderr, "k_decode_exact tile %lu: pending %lu rounds %lu cycles %lu slowest walk %lu (update %lu) bytes %lu\n",
-                (unsigned long)o[0], (unsigned long)o[1], (unsigned long)o[2], (unsigned long)o[3], (unsigned long)o[4],
-                (unsigned long)o[5], (unsigned long)o[6]);
+                (unsigned long)o[0], (unsigned long)o[1], (unsigned long)o[2], (unsigned long)o[3], (unsigned long)(o[7] >> 24),
+                (unsigned long)(o[7] & 0xFFFFFF), (unsigned long)o[6]);
       }
     }
     hipEventRecord(c->ev[5], c->s);

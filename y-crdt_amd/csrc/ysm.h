@@ -207,6 +207,9 @@ template <class C> YM_INLINE int sm_content_inline(C &c, uint32_t ref, BlockInfo
   return 1;
 }
 
+#ifndef YM_SM_PROBE
+#define YM_SM_PROBE(st) // (tools/walkbench.hip: per-state cycle histogram)
+#endif
 template <class S, class C> YM_INLINE int smwalk_update(C &c, S &s) {
   uint32_t st = W_NCL;
   uint32_t ncl = 0, isec = 0, nb = 0, client = 0, clock = 0, j = 0, stored = 0, slot = 4;
@@ -221,6 +224,7 @@ template <class S, class C> YM_INLINE int smwalk_update(C &c, S &s) {
   bi.canon = 0;
   SmTrack tc{0, 0, 0, 0, 0, 0, 0, 0, 0};
   for (;;) {
+    YM_SM_PROBE(st);
     // ---- the one read of this step
     uint32_t v = 0;
     bool canon = true;

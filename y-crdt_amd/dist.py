@@ -34,15 +34,41 @@ def init_from_env(backend=None):
     return rank, world, local
 
 
+def visible_gpus():
+    """GPUs this process may use, without initialising HIP: the GPU nodes of the KFD topology
+    (/sys/class/kfd/kfd/topology/nodes/*/properties with simd_count > 0), limited by
+    HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES when set."""
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    n = 0
+    try:
+        for node in os.listdir(root):
+            try:
+                with open(os.path.join(root, node, "properties")) as f:
+                    for line in f:
+                        k, _, v = line.partition(" ")
+                        if k == "simd_count" and int(v) > 0:
+                            n += 1
+                            break
+            except (OSError, ValueError):
+                pass
+    except OSError:
+        return 0
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
+
+
 def relaunch(n, script, argv, need_gpus=True):
     """Make `python script --gpus n` mean n ranks on this node.
 
     Inside a torch.distributed.run rank (WORLD_SIZE set) the requested count must equal the
     world size; otherwise, for n > 1, the n rank processes are started as ONE child
     (`python -m torch.distributed.run --nproc-per-node n ...`, rendezvous on 127.0.0.1) and
-    its exit code is returned: the caller exits with it.  Called before anything touches the
-    GPU (torch.cuda.device_count() does not initialise it on this image).  Returns None when
-    this process should run the work itself."""
+    its exit code is returned: the caller exits with it.  The GPUs are counted from the KFD
+    topology (visible_gpus), so this parent never initialises the HIP runtime.  Returns None
+    when this process should run the work itself."""
     if "WORLD_SIZE" in os.environ:
         world = int(os.environ["WORLD_SIZE"])
         if n is not None and n != world:
@@ -51,7 +77,7 @@ def relaunch(n, script, argv, need_gpus=True):
     if n is None or n <= 1:
         return None
     if need_gpus:
-        have = torch.cuda.device_count()
+        have = visible_gpus()
         if have < n:
             raise SystemExit(f"--gpus {n} but only {have} GPU(s) visible")
     s = socket.socket()
