@@ -16,9 +16,10 @@ def engine():
     # k_lean off: every document here reaches the tiled kernel (or the exact engine) as it
     # would for shapes k_lean hands over (tests/test_gpu_lean.py covers k_lean's BIG mode)
     # (and the grid-wide long-document path off, so that C1 keeps exercising the tiled kernel;
-    # tests/test_gpu_giant.py covers that path)
+    # tests/test_gpu_giant.py covers that path); the tiny-document route forced on (by default
+    # it serves only batches of >= 65,536 documents handed to the fast path)
     from test_gpu_parity import engine_with
-    e = engine_with(YMERGE_LEAN=0, YMERGE_GIANT_MIN=0)
+    e = engine_with(YMERGE_LEAN=0, YMERGE_GIANT_MIN=0, YMERGE_TINY=4)
     yield e
     e.close()
 

@@ -92,3 +92,43 @@ def test_convert_v1_to_v2_device_merge_semantics(oracle):
         if code == 0:
             want = oracle.merge_updates_v2([u], inputs_v1=True)
             assert out[int(off[i]):int(off[i + 1])].tobytes() == want, i
+
+
+@pytest.mark.gpu
+def test_edge_updates_merge_sv_diff(oracle):
+    """The same edge updates through merge_updates_v1 (each alone and all in one document),
+    the state vector and diff_updates_v1 against an empty state vector: a client repeated in a
+    later section (update 1: its blocks queue in section order, REC_ORDER) must follow yrs'
+    queue order on every path, not the clock order the sort-based paths use."""
+    import numpy as np
+    import ymerge
+    ups = edge_updates()
+    e = ymerge.Engine(0)
+    try:
+        for docs in ([[u] for u in ups], [ups], [[ups[1], ups[0], ups[2]]]):
+            data = np.frombuffer(b"".join(b"".join(d) for d in docs), np.uint8).copy()
+            lens = [len(u) for d in docs for u in d]
+            upd_off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+            doc_upd = np.concatenate([[0], np.cumsum([len(d) for d in docs])]).astype(np.uint64)
+            out, off, st = e.merge_host(data, upd_off, doc_upd)
+            for k, d in enumerate(docs):
+                code, want = oracle.status_of(oracle.merge_updates_v1, d)
+                assert int(st[k]) == code, (k, int(st[k]), code)
+                if code == 0:
+                    assert out[int(off[k]):int(off[k + 1])].tobytes() == want, k
+        data = np.frombuffer(b"".join(ups), np.uint8).copy()
+        u_off = np.concatenate([[0], np.cumsum([len(u) for u in ups])]).astype(np.uint64)
+        sv, sv_off, sv_st = e.state_vector_host(data, u_off)
+        empty = np.zeros(len(ups), np.uint8)
+        df, df_off, df_st = e.diff_host(data, u_off, empty, np.arange(len(ups) + 1, dtype=np.uint64))
+    finally:
+        e.close()
+    for i, u in enumerate(ups):
+        code, want = oracle.status_of(oracle.encode_state_vector_from_update_v1, u)
+        assert int(sv_st[i]) == code, ("sv", i, int(sv_st[i]), code)
+        if code == 0:
+            assert sv[int(sv_off[i]):int(sv_off[i + 1])].tobytes() == want, ("sv", i)
+        code, want = oracle.status_of(oracle.diff_updates_v1, u, b"\x00")
+        assert int(df_st[i]) == code, ("diff", i, int(df_st[i]), code)
+        if code == 0:
+            assert df[int(df_off[i]):int(df_off[i + 1])].tobytes() == want, ("diff", i)

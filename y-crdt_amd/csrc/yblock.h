@@ -179,12 +179,17 @@ template <int NT> YM_INLINE void bitonic(uint64_t *k, uint32_t *v, uint32_t n) {
 struct RegSink {
   uint32_t nb, ne, nr;
   bool unsupported, big_ds;
+  bool misorder = false;                            // REC_ORDER
+  uint32_t nsec = 0, last_cl = 0;
   uint32_t b_client, b_clock, b_len, b_pos, b_meta; // first block
   uint32_t e_client;                                // first DeleteSet entry
   uint32_t r0s, r0e, r1s, r1e;                      // its first two ranges
   const uint8_t *doc;
   uint32_t doc_len, ubase;
-  YM_INLINE void on_section(uint32_t) {}
+  YM_INLINE void on_section(uint32_t client) {
+    if (nsec++ && client >= last_cl) misorder = true;
+    last_cl = client;
+  }
   YM_INLINE int on_block(uint32_t client, uint32_t clock, const BlockInfo &bi, uint32_t bpos, uint32_t blen) {
     if (bi.unsupported) unsupported = true;
     if (bi.kind == BK_SKIP) return 0;
@@ -315,6 +320,7 @@ YM_INLINE void rec_pack(const RegSink &s, int e, uint32_t &w0, uint32_t &w1, uin
   w1 = w2 = w3 = w4 = w5 = 0;
   if (s.unsupported) w0 |= REC_UNSUP;
   if (s.big_ds) w0 |= REC_BIGDS;
+  if (s.misorder) w0 |= REC_ORDER;
   if (e) return;
   if (s.nb == 1 && s.ne == 0) {
     w0 |= REC_BLOCK << 10;

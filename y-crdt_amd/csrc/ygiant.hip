@@ -55,7 +55,7 @@ template <class FB, class FR>
 __device__ __forceinline__ uint32_t gs_visit(const GsArgs &a, uint32_t i, FB blk, FR rng) {
   uint32_t w[6];
   gs_rec(a, i, w);
-  if (w[0] & (REC_SLOW | 0xFF)) return GSB_SLOW;
+  if (w[0] & (REC_SLOW | REC_ORDER | 0xFF)) return GSB_SLOW; // (REC_ORDER: the exact engine)
   const uint32_t shape = (w[0] >> 10) & 3;
   if (shape == REC_BLOCK) {
     blk(w[1], w[2], w[3], w[4], w[5]);

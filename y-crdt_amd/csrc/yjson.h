@@ -63,13 +63,18 @@ constexpr int JBN = 40; // 1280 bits: r, s, m+, m- stay below 2^1140 for every d
 struct JBig {
   uint32_t w[JBN];
 };
+// (the loops stay rolled: a fully unrolled JBig lives in registers, and f64_shortest's five of
+// them took all 512 VGPRs, an allocation every kernel that can reach it inherited: one wave
+// per SIMD; rolled, they live in scratch, touched only by the rare non-integral JSON number)
 __device__ __forceinline__ void jb_set(JBig &a, uint64_t v) {
+#pragma unroll 1
   for (int i = 0; i < JBN; i++) a.w[i] = 0;
   a.w[0] = (uint32_t)v;
   a.w[1] = (uint32_t)(v >> 32);
 }
 __device__ __forceinline__ void jb_mul10(JBig &a) {
   uint64_t c = 0;
+#pragma unroll 1
   for (int i = 0; i < JBN; i++) {
     const uint64_t t = (uint64_t)a.w[i] * 10u + c;
     a.w[i] = (uint32_t)t;
@@ -78,6 +83,7 @@ __device__ __forceinline__ void jb_mul10(JBig &a) {
 }
 __device__ __forceinline__ void jb_shl(JBig &a, int k) {
   const int q = k >> 5, r = k & 31;
+#pragma unroll 1
   for (int i = JBN - 1; i >= 0; i--) {
     const uint32_t hi = i - q >= 0 ? a.w[i - q] : 0;
     const uint32_t lo = i - q - 1 >= 0 ? a.w[i - q - 1] : 0;
@@ -85,12 +91,14 @@ __device__ __forceinline__ void jb_shl(JBig &a, int k) {
   }
 }
 __device__ __forceinline__ int jb_cmp(const JBig &a, const JBig &b) {
+#pragma unroll 1
   for (int i = JBN - 1; i >= 0; i--)
     if (a.w[i] != b.w[i]) return a.w[i] < b.w[i] ? -1 : 1;
   return 0;
 }
 __device__ __forceinline__ void jb_add(JBig &r, const JBig &a, const JBig &b) {
   uint64_t c = 0;
+#pragma unroll 1
   for (int i = 0; i < JBN; i++) {
     const uint64_t t = (uint64_t)a.w[i] + b.w[i] + c;
     r.w[i] = (uint32_t)t;
@@ -99,6 +107,7 @@ __device__ __forceinline__ void jb_add(JBig &r, const JBig &a, const JBig &b) {
 }
 __device__ __forceinline__ void jb_sub(JBig &a, const JBig &b) {
   uint64_t br = 0;
+#pragma unroll 1
   for (int i = 0; i < JBN; i++) {
     const uint64_t t = (uint64_t)a.w[i] - b.w[i] - br;
     a.w[i] = (uint32_t)t;

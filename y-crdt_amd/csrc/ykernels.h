@@ -45,6 +45,8 @@ constexpr uint32_t LP_MIN_LEN = 8192;
 // the exact walk is one wavefront stepping serially (~1,800 cycles a varint), a 5 KB rich update
 // ~6 ms of one workgroup's time (env YMERGE_LP_MID)
 constexpr uint32_t LP_MID_LEN = 128;
+// and every update of >= LP_DIRECT_LEN bytes, without the fast lane walk first
+constexpr uint32_t LP_DIRECT_LEN = 1024;
 // k_decode workgroups with staged updates for the exact walk (k_decode_exact): count at word
 // EXQ_COUNT of `huge`, then (workgroup, overflow words used) pairs, one per decode workgroup
 constexpr uint32_t EXQ_COUNT = 4 + 2 * HUGE_LIST, EXQ_LIST = EXQ_COUNT + 4;
@@ -54,6 +56,11 @@ constexpr uint32_t REC_STAGED = 1u << 17; // with REC_SLOW: walked exactly by k_
 // client section without Skips, zero-length GC blocks, panicking splits or unsupported content,
 // and <= 1 DeleteSet entry; w5 = its LP entry + 1 (grid paths for single-update documents)
 constexpr uint32_t REC_LONG = 1u << 16;
+// a client section whose client is not below the previous section's: decoding appends a repeated
+// client's sections to one block queue in section order (yrs/src/update.rs:714-749), which the
+// sort-based paths (fast, tiled, grid) do not model; such documents go to the exact engine
+// (encoders write sections in descending client order, so valid updates never carry it)
+constexpr uint32_t REC_ORDER = 1u << 18;
 
 // ---- parallel parse of long updates (ylong.hip)
 constexpr uint32_t LP_CH = 8192;  // bytes per chunk
@@ -64,7 +71,7 @@ enum : uint32_t {                 // meta words
   LPM_NE, LPM_NR
 };
 enum : uint32_t { // flags
-  LPF_FALLBACK = 1, LPF_UNSUP = 2, LPF_SKIP = 4, LPF_ZGC = 8, LPF_PANIC = 16, LPF_MSEC = 32, LPF_RICH = 64
+  LPF_FALLBACK = 1, LPF_UNSUP = 2, LPF_SKIP = 4, LPF_ZGC = 8, LPF_PANIC = 16, LPF_MSEC = 32, LPF_RICH = 64, LPF_ORDER = 128
 };
 enum : uint32_t { LPG_CHUNKS = 0, LPG_SEGS, LPG_ORDS, LPG_SECS, LPG_N, LPG_WORDS = 8 };
 struct LpArgs {
@@ -202,13 +209,14 @@ void launch_big_count(const BatchIn &b, const FastOut &o, uint32_t *counts, uint
 void launch_big_merge(const BatchIn &b, const uint32_t *counts, const uint64_t *scr_off, uint32_t *scratch,
                       const FastOut &o, uint32_t n_list, hipStream_t s);
 
-// exact per-document engine; `path` (optional) restricts it to documents with path == 1
+// exact per-document engine; `path` (optional) restricts it to documents with path == 1; lpw
+// documents per wavefront (1..64)
 void launch_seq_count(const BatchIn &b, const uint8_t *path, uint8_t *status, uint32_t *counts, uint64_t *need,
-                      uint32_t *n_exact, hipStream_t s);
+                      uint32_t *n_exact, hipStream_t s, uint32_t lpw = 64);
 void launch_seq_merge(bool write, const BatchIn &b, const uint8_t *path, const uint8_t *status, const uint32_t *counts,
                       const uint64_t *scr_off, uint32_t *scratch, uint64_t *sizes, const uint64_t *out_off,
                       uint8_t *out, uint64_t out_base, uint64_t *out_start, uint64_t *out_len, uint8_t *status_out,
-                      hipStream_t s);
+                      hipStream_t s, uint32_t lpw = 64, uint64_t *dbg = nullptr);
 size_t scan_tmp_elems(uint32_t n);
 void launch_pack(const uint8_t *src, const uint64_t *start, const uint64_t *len, const uint64_t *pack_off,
                  uint8_t *dst, uint32_t n_docs, hipStream_t s);

@@ -378,10 +378,12 @@ __global__ void __launch_bounds__(64) k_lp_stitch(LpArgs a) {
       if (rd_var_u32(c, ncl, cn) || ncl > L / 3) return false; // (no try_reserve failure possible)
       const uint32_t sb = atomicAdd(&a.g[LPG_SECS], ncl);
       if ((uint64_t)sb + ncl > a.seccap) return false;
-      uint32_t ord = 0, st = 0, flags = ncl == 1 ? 0u : LPF_MSEC;
+      uint32_t ord = 0, st = 0, flags = ncl == 1 ? 0u : LPF_MSEC, prev = 0;
       for (uint32_t s = 0; s < ncl; s++) {
         uint32_t nb, client, clock;
         if (rd_var_u32(c, nb, cn) || rd_var_u32(c, client, cn) || rd_var_u32(c, clock, cn)) return false;
+        if (s && client >= prev) flags |= LPF_ORDER; // (REC_ORDER)
+        prev = client;
         if (nb > L / 2) return false;
         uint32_t *sw = a.sec + (size_t)(sb + s) * 4;
         sw[0] = client;
@@ -762,6 +764,7 @@ __global__ void __launch_bounds__(256) k_lp_final(LpArgs a) {
     s.nr = m[LPM_NR];
     s.unsupported = (fl & LPF_UNSUP) != 0;
     s.big_ds = s.ne > DS_SMALL;
+    s.misorder = (fl & LPF_ORDER) != 0;
     const uint32_t *ov = a.ovf + m[LPM_OVF];
     if (s.nb) {
       s.b_client = ov[0];

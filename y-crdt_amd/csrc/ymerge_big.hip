@@ -163,6 +163,7 @@ __global__ void __launch_bounds__(NT) k_big_count(BatchIn b, uint8_t *path, uint
     const uint32_t e = w0 & 0xFF, shape = (w0 >> 10) & 3;
     if (e) atomicMin(&s_err, ((unsigned long long)i << 8) | e);
     if (w0 & REC_BIGDS) flags |= 2;
+    if (w0 & REC_ORDER) flags |= 16;
     if (ulen >= (1u << 24)) flags |= 8;
     if (!e) {
       if (shape == REC_BLOCK) nb += 1;

@@ -112,7 +112,8 @@ __device__ __forceinline__ uint32_t ovf_global(uint32_t *huge, uint32_t need, ui
 // list keeps 16-bit lane / count fields)
 __global__ void __launch_bounds__(DEC_NT, 8) k_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_upd,
                                                       uint32_t *rec, uint32_t *ovf, uint32_t *huge, uint32_t v1x,
-                                                      uint32_t lp_min, uint32_t huge_base, uint64_t huge_cap) {
+                                                      uint32_t lp_min, uint32_t lp_direct, uint32_t huge_base,
+                                                      uint64_t huge_cap) {
   __shared__ __align__(16) uint32_t stage[DEC_STAGE / 4 + 4];
   __shared__ uint32_t ovf_top, n_cx, n_sl;
   ym_set_grammar(v1x); // (fast_walk bails on every content it does not restate)
@@ -153,7 +154,9 @@ __global__ void __launch_bounds__(DEC_NT, 8) k_decode(const uint8_t *bytes, cons
     s.unsupported = s.big_ds = false;
     s.ubase = 0;
     const bool staged = a1 - sbase <= 4 * nd;
-    const int e = staged ? fast_walk(stage, (uint32_t)(a0 - sbase), ulen, s) : -1;
+    // (an update of >= lp_direct bytes skips the lane walk: one lane stepping through KBs of
+    // blocks, twice for the overflow words, held the whole workgroup for ~1 ms)
+    const int e = staged && ulen < lp_direct ? fast_walk(stage, (uint32_t)(a0 - sbase), ulen, s) : -1;
     // a long update (or a medium one the fast walk cannot take): the parallel parse (ylong.hip)
     const bool lp_take = e < 0 && ulen >= lp_min;
     if (lp_take) {
@@ -416,7 +419,7 @@ void launch_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_upd
   hipMemsetAsync(huge + EXQ_COUNT, 0, 4, s);
   const uint32_t lp_min = lp ? (lp->mid < LP_MIN_LEN ? lp->mid : LP_MIN_LEN) : LP_MIN_LEN;
   hipLaunchKernelGGL(k_decode, dim3((unsigned)nwg), dim3(DEC_NT), 0, s, bytes, upd_off, n_updates, rec, ovf, huge,
-                     v1x, lp_min, (uint32_t)(nwg * DEC_OVF), (uint64_t)huge_cap);
+                     v1x, lp_min, lp ? LP_DIRECT_LEN : 0xFFFFFFFFu, (uint32_t)(nwg * DEC_OVF), (uint64_t)huge_cap);
   const uint32_t base = (uint32_t)(nwg * DEC_OVF);
   hipLaunchKernelGGL(k_decode_exact, dim3((unsigned)(nwg < 512 ? nwg : 512) * EX_SPLIT), dim3(EX_NT), 0, s, bytes, upd_off,
                      n_updates, rec, ovf, huge, v1x, (uint32_t)(nwg * DEC_OVF), (uint64_t)huge_cap, dbg);
@@ -554,6 +557,7 @@ __global__ void __launch_bounds__(NT, 3) k_fast_merge(BatchIn b, FastCaps caps, 
       if (e) atomicMin(&misc[0], (i << 8) | e);
       if (w0 & REC_UNSUP) flags |= 1;
       if (w0 & REC_BIGDS) flags |= 2;
+      if (w0 & REC_ORDER) flags |= 16;
       if (ulen >= (1u << 24)) flags |= 8;
       if (!e) {
         if (shape == REC_BLOCK) snb = 1;
@@ -643,8 +647,8 @@ __global__ void __launch_bounds__(NT, 3) k_fast_merge(BatchIn b, FastCaps caps, 
   YM_STAMP(1);
   {
     const uint32_t ek = misc[0], fl = misc[1];
-    if (ek == 0xFFFFFFFFu && (fl & 14)) { // capacity: tiled kernel; big DS table, huge block: exact engine
-      handover((fl & 4) ? 2 : 1);
+    if (ek == 0xFFFFFFFFu && (fl & 30)) { // capacity: tiled kernel; big DS table, huge block,
+      handover((fl & 4) && !(fl & 16) ? 2 : 1); // client sections out of order: exact engine
       return;
     }
     if (ek != 0xFFFFFFFFu || fl) {

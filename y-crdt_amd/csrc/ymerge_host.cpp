@@ -77,6 +77,8 @@ struct ymerge_ctx {
   DevBuf huge;              // k_decode's list of long updates, overflow bump counter
   DevBuf lp;                // the parallel parse of long updates (ylong.hip): scratch
   bool long_parse = true;   // env YMERGE_LONG_PARSE=0: every long update takes the exact walk
+  bool tiny_forced = false; // env YMERGE_TINY set
+  uint32_t seq_lpw = 0; // env YMERGE_SEQ_LPW: exact-engine documents per wavefront (0: by count)
   uint32_t lp_mid = ym::LP_MID_LEN; // env YMERGE_LP_MID: staged rich updates of >= this many bytes -> parallel parse
   bool long_grid = true;    // env YMERGE_LONG_GRID=0: single long update documents take the tiled kernel / planners
   uint32_t ls_min_diff = ym::LS_MIN_DIFF; // diff / SV documents on the long-update grid path (env YMERGE_LS_MIN)
@@ -133,7 +135,10 @@ static bool ctx_init(ymerge_ctx *c, int device) {
   // document through the exact engine (used by the parity tests to cover both engines)
   if (const char *v = getenv("YMERGE_FAST_THREADS")) c->fast_threads = atoi(v);
   if (const char *v = getenv("YMERGE_STAMPS")) c->want_stamps = atoi(v) != 0;
-  if (const char *v = getenv("YMERGE_TINY")) c->caps.in_cap = (uint32_t)atoi(v); // 0: no tiny path
+  if (const char *v = getenv("YMERGE_TINY")) { // 0: no tiny path; set: used at any batch size
+    c->caps.in_cap = (uint32_t)atoi(v);
+    c->tiny_forced = true;
+  }
   if (const char *v = getenv("YMERGE_LEAN")) c->lean = atoi(v) != 0;
   if (const char *v = getenv("YMERGE_COMPACT_LPW")) c->compact_lpw = (uint32_t)atoi(v);
   if (const char *v = getenv("YMERGE_GIANT_MIN")) c->giant_min = (uint32_t)atoi(v);
@@ -143,6 +148,7 @@ static bool ctx_init(ymerge_ctx *c, int device) {
     c->planner = strcmp(v, "ring") == 0 ? 1u : strcmp(v, "wave") == 0 ? 2u : 0u;
   if (const char *v = getenv("YMERGE_LEAN_SCR_MAX")) c->lean_scr_max = strtoull(v, nullptr, 10);
   if (const char *v = getenv("YMERGE_LONG_PARSE")) c->long_parse = atoi(v) != 0;
+  if (const char *v = getenv("YMERGE_SEQ_LPW")) c->seq_lpw = (uint32_t)std::min(64, std::max(0, atoi(v)));
   if (const char *v = getenv("YMERGE_LP_MID")) c->lp_mid = (uint32_t)std::max(1, atoi(v));
   if (const char *v = getenv("YMERGE_LONG_GRID")) c->long_grid = atoi(v) != 0;
   if (const char *v = getenv("YMERGE_LS_MIN")) c->ls_min_diff = (uint32_t)atoi(v);
@@ -298,6 +304,18 @@ static bool ensure_keep(ymerge_ctx *c, DevBuf &b, size_t bytes, size_t keep) {
   b.release();
   b = nb;
   return true;
+}
+
+// fewest documents handed to k_fast_merge for its tiny-document hand-over to the exact engine
+constexpr uint64_t TINY_MIN_DOCS = 65536;
+
+// Documents per wavefront of the exact engine (ymerge_seq.hip): 64 (env YMERGE_SEQ_LPW sets it).
+// One per wavefront was measured slower on the corpus (exact stage 2.35 vs 1.80 ms, r05t): the
+// slowest document's serial walk sets the stage time either way, and 64 to a wave keeps the
+// launch small.
+static uint32_t seq_lpw(const ymerge_ctx *c, uint64_t n) {
+  (void)n;
+  return c->seq_lpw ? c->seq_lpw : 64;
 }
 
 // overflow words for the long updates k_decode_huge decodes (5 per block, 2 per DeleteSet entry,
@@ -622,7 +640,12 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
       }
     }
     hipEventRecord(c->ev[5], c->s);
-    ym::launch_fast_merge(b, c->caps, fo, c->fast_threads, c->s);
+    // the tiny-document hand-over pays off only for many of them (C3: 645k documents of <= 4
+    // updates, 13.5 -> 4.5 ms): the exact engine's lane walks chase HBM scratch (~1 ms a
+    // wavefront of 64 tiny documents), a fast-path workgroup takes one in ~40 us
+    ym::FastCaps caps = c->caps;
+    if (n_rej < TINY_MIN_DOCS && !c->tiny_forced) caps.in_cap = 0;
+    ym::launch_fast_merge(b, caps, fo, c->fast_threads, c->s);
     if (hipGetLastError() != hipSuccess) return DEV_FAIL();
     hipEventRecord(c->ev[6], c->s);
   }
@@ -718,7 +741,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   uint32_t n_exact = 0, n_overlap = 0, n_tiny = 0, n_giant = 0;
   if (n_p1 || n_p2) {
     ym::launch_seq_count(b, path, status, c->counts.as<uint32_t>(), c->need.as<uint64_t>(), c->counter.as<uint32_t>(),
-                         c->s);
+                         c->s, seq_lpw(c, fast ? (uint64_t)n_p1 + n_p2 : n));
     ym::launch_scan_u64(c->need.as<uint64_t>(), c->scr_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
     hipMemcpyAsync(c->h_pinned + 8, c->scr_off.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, c->s);
     hipMemcpyAsync(c->h_pinned + 9, c->counter.p, 4, hipMemcpyDeviceToHost, c->s);
@@ -734,9 +757,16 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   }
   if (n_exact) {
     if (!c->scratch.ensure((size_t)words * 4 + 64)) return DEV_FAIL();
+    const uint32_t lpw = seq_lpw(c, n_exact);
+    static const bool seq_dbg = getenv("YMERGE_SEQ_DBG") != nullptr;
+    uint64_t *sdbg = nullptr;
+    if (seq_dbg && c->stamps.ensure((size_t)n * 8 + 64)) {
+      sdbg = c->stamps.as<uint64_t>();
+      hipMemsetAsync(sdbg, 0, (size_t)n * 8, c->s);
+    }
     ym::launch_seq_merge(false, b, path, status, c->counts.as<uint32_t>(), c->scr_off.as<uint64_t>(),
                          c->scratch.as<uint32_t>(), c->sizes.as<uint64_t>(), nullptr, nullptr, 0, nullptr, nullptr,
-                         status, c->s);
+                         status, c->s, lpw);
     ym::launch_scan_u64(c->sizes.as<uint64_t>(), c->spill_off.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
     uint64_t spill = 0;
     if (!read_words(c, c->spill_off.as<uint64_t>() + n, 8, &spill)) return DEV_FAIL();
@@ -744,8 +774,24 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     arena = c->arena.as<uint8_t>();
     ym::launch_seq_merge(true, b, path, status, c->counts.as<uint32_t>(), c->scr_off.as<uint64_t>(),
                          c->scratch.as<uint32_t>(), nullptr, c->spill_off.as<uint64_t>(), arena, slots, ostart, olen,
-                         nullptr, c->s);
+                         nullptr, c->s, lpw, sdbg);
     if (hipGetLastError() != hipSuccess) return DEV_FAIL();
+    if (sdbg) { // diagnostic (env YMERGE_SEQ_DBG): the exact engine's slowest documents to stderr
+      std::vector<uint64_t> h(n), du(n + 1);
+      hipStreamSynchronize(c->s);
+      hipMemcpy(h.data(), sdbg, n * 8, hipMemcpyDeviceToHost);
+      hipMemcpy(du.data(), b.doc_upd, (n + 1) * 8, hipMemcpyDeviceToHost);
+      std::vector<uint32_t> idx(n);
+      for (uint32_t q = 0; q < n; q++) idx[q] = q;
+      std::sort(idx.begin(), idx.end(), [&](uint32_t x, uint32_t y) { return h[x] > h[y]; });
+      for (uint32_t q = 0; q < std::min<uint32_t>(8, n) && h[idx[q]]; q++) {
+        uint64_t o0 = 0, o1 = 0;
+        hipMemcpy(&o0, b.upd_off + du[idx[q]], 8, hipMemcpyDeviceToHost);
+        hipMemcpy(&o1, b.upd_off + du[idx[q] + 1], 8, hipMemcpyDeviceToHost);
+        fprintf(stderr, "k_seq_merge doc %u: updates %lu bytes %lu cycles %lu\n", idx[q],
+                (unsigned long)(du[idx[q] + 1] - du[idx[q]]), (unsigned long)(o1 - o0), (unsigned long)h[idx[q]]);
+      }
+    }
   }
   hipEventRecord(c->ev[2], c->s);
   // total output bytes (and packed offsets for host copies); when k_lean wrote every

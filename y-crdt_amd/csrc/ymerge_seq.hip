@@ -32,11 +32,22 @@ struct CountSink {
   YM_INLINE int on_ds_done() { return 0; }
 };
 
-__global__ void k_seq_count(BatchIn b, const uint8_t *path, uint8_t *status, uint32_t *counts,
-                            uint64_t *need_words, uint32_t *n_exact) {
+// Documents per wavefront (lpw, 1..64): lane l < lpw of wave w takes document w * lpw + l.  A
+// wave's lanes walk different documents and diverge at every step, so a few hundred exact
+// documents run one per wavefront (lpw 1: a document's serial walk is the wave's whole time);
+// hundreds of thousands run 64 to a wave (ymerge_host.cpp seq_lpw).
+__device__ __forceinline__ uint32_t seq_doc(uint32_t lpw, bool &active) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x, lane = g & 63;
+  active = lane < lpw;
+  return (g >> 6) * lpw + lane;
+}
+
+__global__ void __launch_bounds__(64) k_seq_count(BatchIn b, const uint8_t *path, uint8_t *status, uint32_t *counts,
+                                                  uint64_t *need_words, uint32_t *n_exact, uint32_t lpw) {
   ym_set_grammar(b.v1x);
-  uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-  if (d >= b.n_docs) return;
+  bool active;
+  const uint32_t d = seq_doc(lpw, active);
+  if (!active || d >= b.n_docs) return;
   if (path && path[d] != 1) {
     need_words[d] = 0;
     return;
@@ -617,13 +628,16 @@ __device__ int seq_fill(SeqCtx &x, const BatchIn &b, uint64_t u0) {
 }
 
 template <bool WRITE>
-__global__ void k_seq_merge(BatchIn b, const uint8_t *path, const uint8_t *status, const uint32_t *counts,
-                            const uint64_t *scr_off, uint32_t *scratch, uint64_t *sizes, const uint64_t *out_off,
-                            uint8_t *out, uint64_t out_base, uint64_t *out_start, uint64_t *out_len,
-                            uint8_t *status_out) {
+__global__ void __launch_bounds__(64) k_seq_merge(BatchIn b, const uint8_t *path, const uint8_t *status,
+                                                  const uint32_t *counts, const uint64_t *scr_off, uint32_t *scratch,
+                                                  uint64_t *sizes, const uint64_t *out_off, uint8_t *out,
+                                                  uint64_t out_base, uint64_t *out_start, uint64_t *out_len,
+                                                  uint8_t *status_out, uint32_t lpw, uint64_t *dbg) {
   ym_set_grammar(b.v1x);
-  uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-  if (d >= b.n_docs) return;
+  bool active;
+  const uint32_t d = seq_doc(lpw, active);
+  if (!active || d >= b.n_docs) return;
+  const uint64_t t0 = dbg ? __builtin_amdgcn_s_memtime() : 0;
   if (path && path[d] != 1) {
     if (!WRITE) sizes[d] = 0;
     return;
@@ -656,6 +670,7 @@ __global__ void k_seq_merge(BatchIn b, const uint8_t *path, const uint8_t *statu
       out_start[d] = out_base + out_off[d];
       out_len[d] = w.n;
     }
+    if (dbg) dbg[d] = __builtin_amdgcn_s_memtime() - t0; // diagnostic (env YMERGE_SEQ_DBG): cycles
   } else {
     Counter c;
     if (!err) err = seq_encode_blocks(x, c);
@@ -670,21 +685,21 @@ __global__ void k_seq_merge(BatchIn b, const uint8_t *path, const uint8_t *statu
 // ------------------------------------------------------------------ launchers
 namespace ym {
 void launch_seq_count(const BatchIn &b, const uint8_t *path, uint8_t *status, uint32_t *counts, uint64_t *need,
-                      uint32_t *n_exact, hipStream_t s) {
-  uint32_t nb = (b.n_docs + 63) / 64;
-  if (nb) hipLaunchKernelGGL(k_seq_count, dim3(nb), dim3(64), 0, s, b, path, status, counts, need, n_exact);
+                      uint32_t *n_exact, hipStream_t s, uint32_t lpw) {
+  const uint32_t nb = (uint32_t)((b.n_docs + lpw - 1) / lpw); // one wavefront per workgroup
+  if (nb) hipLaunchKernelGGL(k_seq_count, dim3(nb), dim3(64), 0, s, b, path, status, counts, need, n_exact, lpw);
 }
 void launch_seq_merge(bool write, const BatchIn &b, const uint8_t *path, const uint8_t *status, const uint32_t *counts,
                       const uint64_t *scr_off, uint32_t *scratch, uint64_t *sizes, const uint64_t *out_off,
                       uint8_t *out, uint64_t out_base, uint64_t *out_start, uint64_t *out_len, uint8_t *status_out,
-                      hipStream_t s) {
-  uint32_t nb = (b.n_docs + 63) / 64;
+                      hipStream_t s, uint32_t lpw, uint64_t *dbg) {
+  const uint32_t nb = (uint32_t)((b.n_docs + lpw - 1) / lpw);
   if (!nb) return;
   if (write)
     hipLaunchKernelGGL(k_seq_merge<true>, dim3(nb), dim3(64), 0, s, b, path, status, counts, scr_off, scratch, sizes,
-                       out_off, out, out_base, out_start, out_len, status_out);
+                       out_off, out, out_base, out_start, out_len, status_out, lpw, dbg);
   else
     hipLaunchKernelGGL(k_seq_merge<false>, dim3(nb), dim3(64), 0, s, b, path, status, counts, scr_off, scratch,
-                       sizes, out_off, out, out_base, out_start, out_len, status_out);
+                       sizes, out_off, out, out_base, out_start, out_len, status_out, lpw, dbg);
 }
 } // namespace ym

@@ -18,6 +18,7 @@
 // a key-table hit beyond the first V2_KCAP keys of one update.
 #include "ycodec.h"
 #include "ykernels.h"
+#include "ywin.h"
 
 namespace ym {
 
@@ -588,7 +589,9 @@ template <class W> struct REnc {
     }
   }
 };
+// UTF-16 length of a validated string: ASCII runs 16 bytes at a time (independent loads)
 __device__ __forceinline__ uint32_t utf16_count(const uint8_t *s, uint32_t n) {
+  if (bytes_ascii(s, n)) return n;
   uint32_t k = 0, i = 0;
   while (i < n) k += ch_len16(utf8_next(s, n, i));
   return k;
@@ -615,27 +618,35 @@ template <class W> struct V2Enc {
     slen.flush(s[S_SLEN]);
   }
 };
-__device__ __forceinline__ uint32_t rv(Cur &c) {
-  uint32_t v;
+// the v1x document is read through a 64-byte register window (ywin.h): a lane walking a whole
+// document byte by byte over HBM waited one memory latency per byte (k_v2_encode 29.6 ms on C2)
+__device__ __forceinline__ uint32_t rv(WCur &c) {
+  uint32_t v = 0;
   bool cn;
-  rd_var_u32(c, v, cn);
+  wc_var_u32(c, v, cn);
   return v;
 }
-__device__ __forceinline__ uint64_t rv64(Cur &c) {
-  uint64_t v;
+__device__ __forceinline__ uint64_t rv64(WCur &c) {
+  uint64_t v = 0;
   bool cn;
-  rd_var_u64(c, v, cn);
+  wc_var_u64(c, v, cn);
   return v;
 }
-// copies one (validated) Any value / raw byte range of the v1x document into the rest stream
-template <class W> __device__ __forceinline__ void copy_any(Cur &c, W &rest) {
+__device__ __forceinline__ uint8_t ru8(WCur &c) {
+  uint8_t v = 0;
+  wc_u8(c, v);
+  return v;
+}
+// copies one (validated) Any value of the v1x document into the rest stream (the cold skip on
+// the plain pointer)
+template <class W> __device__ __forceinline__ void copy_any(WCur &c, W &rest) {
   const uint32_t st = c.i;
-  Cur cc = c; // (the out-of-line skip takes its cursor by reference: a copy keeps c in registers)
+  Cur cc{c.p, c.n, c.i};
   any_skip(cc);
   c.i = cc.i;
   rest.bytes(c.p + st, c.i - st);
 }
-template <class W> __device__ __forceinline__ void e_str(V2Enc<W> &e, Cur &c) {
+template <class W> __device__ __forceinline__ void e_str(V2Enc<W> &e, WCur &c) {
   const uint32_t l = rv(c);
   e.string(c.p + c.i, l);
   c.i += l;
@@ -643,7 +654,8 @@ template <class W> __device__ __forceinline__ void e_str(V2Enc<W> &e, Cur &c) {
 // encode_diff with an empty state vector over EncoderV2 (update.rs:490-535, slice.rs:199-251,
 // block.rs:1711-1754), reading the canonical v1x bytes the engine wrote
 template <class W> __device__ __forceinline__ void v1x_to_v2(const uint8_t *p, uint32_t n, V2Enc<W> &e) {
-  Cur c{p, n, 0};
+  WCur c;
+  wc_init(c, p, n);
   W &rest = e.s[S_REST];
   const uint32_t ncl = rv(c);
   w_var(rest, ncl);
@@ -655,8 +667,8 @@ template <class W> __device__ __forceinline__ void v1x_to_v2(const uint8_t *p, u
     e.cli.put(e.s[S_CLI], client);
     w_var(rest, clock);
     for (uint32_t j = 0; j < nb; j++) {
-      uint8_t info;
-      rd_u8(c, info);
+      wc_ensure(c, 32); // (the block's header in the window: one wait per block)
+      const uint8_t info = ru8(c);
       if (info == 10 || info == 0) {
         e.info.put(e.s[S_INFO], info);
         e.len.put(e.s[S_LEN], rv(c));
@@ -709,8 +721,7 @@ template <class W> __device__ __forceinline__ void v1x_to_v2(const uint8_t *p, u
         break;
       }
       case 7: {
-        uint8_t tr;
-        rd_u8(c, tr);
+        const uint8_t tr = ru8(c);
         e.tref.put(e.s[S_TREF], tr);
         if (tr == 3) {
           const uint32_t l = rv(c);
@@ -718,8 +729,7 @@ template <class W> __device__ __forceinline__ void v1x_to_v2(const uint8_t *p, u
           e.string(c.p + c.i, l);
           c.i += l;
         } else if (tr == 7) {
-          uint8_t f;
-          rd_u8(c, f);
+          const uint8_t f = ru8(c);
           rest.u8(f);
           w_var(rest, rv64(c));
           w_var(rest, rv(c));
@@ -738,8 +748,10 @@ template <class W> __device__ __forceinline__ void v1x_to_v2(const uint8_t *p, u
       }
       case 9: e_str(e, c); copy_any(c, rest); break;
       case 11: {
-        int64_t f;
-        rd_var_i64(c, f);
+        int64_t f = 0;
+        Cur cc{c.p, c.n, c.i};
+        rd_var_i64(cc, f);
+        c.i = cc.i;
         w_var_i64(rest, f);
         w_var(rest, rv64(c));
         w_var(rest, rv(c));
