@@ -287,13 +287,14 @@ def run_merge(a, rank, world, dev):
             traces = run_traces(eng, dev)
         except Exception as e:  # noqa: BLE001
             traces = {"error": repr(e)[:200]}
-    if a.workload == "c2" and not a.no_compact and rank == 0:
+    if a.workload == "c2" and rank == 0:
         # secondary measurements after the timed region: a failure is reported in the line,
         # it never costs the headline
-        try:
-            compact = run_compact(a, eng, batch, (t_b, t_u, t_d), dev, world)
-        except Exception as e:  # noqa: BLE001
-            compact = {"error": repr(e)[:200]}
+        if not a.no_compact:
+            try:
+                compact = run_compact(a, eng, batch, (t_b, t_u, t_d), dev, world)
+            except Exception as e:  # noqa: BLE001
+                compact = {"error": repr(e)[:200]}
         if not a.no_v2:
             try:
                 v2 = run_v2(a, eng, batch, dev, world)

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <vector>
+#include <cstring>
 #include "ycodec.h"
 #include "ykernels.h"
 #include "ysm.h"
@@ -56,7 +57,37 @@ __global__ void __launch_bounds__(64) k_blocks(const uint8_t *doc, uint32_t nbyt
   }
 }
 
+__global__ void __launch_bounds__(64) k_json(const uint8_t *js, uint32_t n, unsigned long long *out) {
+  if (threadIdx.x) return;
+  ym_set_grammar(0);
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  const bool pl = json_plain(js, n);
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  Counter c;
+  const int e = json_canon(js, n, c);
+  const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+  out[0] = pl;
+  out[1] = t1 - t0;
+  out[2] = t2 - t1;
+  out[3] = (unsigned long long)e;
+  out[4] = c.n;
+}
+
 int main(int argc, char **argv) {
+  if (argc > 3) { // json text timing
+    const uint32_t n = (uint32_t)strlen(argv[3]);
+    uint8_t *dj;
+    unsigned long long *dout, o[5];
+    hipMalloc(&dj, n + 64);
+    hipMalloc(&dout, 64);
+    hipMemcpy(dj, argv[3], n, hipMemcpyHostToDevice);
+    for (int it = 0; it < 3; it++) {
+      hipLaunchKernelGGL(k_json, dim3(1), dim3(64), 0, 0, dj, n, dout);
+      hipMemcpy(o, dout, 40, hipMemcpyDeviceToHost);
+      printf("json %u bytes: plain %llu (%llu cycles), json_canon %llu cycles err %llu size %llu\n", n, o[0], o[1],
+             o[2], o[3], o[4]);
+    }
+  }
   FILE *fp = fopen(argv[1], "rb");
   std::vector<uint8_t> h(1 << 22);
   const size_t n = fread(h.data(), 1, h.size(), fp);

@@ -713,14 +713,20 @@ __device__ __noinline__ SlowRes parse_content_slow(const uint8_t *p, uint32_t n,
     case 5: case 6: { // Embed (json) / Format (key, json): re-serialised on encode
       if (ref == 6) {
         YM_TRY(rd_var_u32(c, v, cn));
+        bi.reenc |= !cn;
         YM_TRY(rd_skip(c, v));
       }
       YM_TRY(rd_var_u32(c, v, cn));
+      bi.reenc |= !cn;
       YM_TRY(rd_skip(c, v));
-      Counter cnt;
-      YM_TRY(json_canon(c.p + c.i - v, v, cnt));
+      // a text that is its own canonical form (json_plain) keeps the block's bytes: the merge
+      // copies them instead of re-serialising the JSON in its sizes and write phases
+      if (!json_plain(c.p + c.i - v, v)) {
+        Counter cnt;
+        YM_TRY(json_canon(c.p + c.i - v, v, cnt));
+        bi.reenc = true;
+      }
       bi.len = 1;
-      bi.reenc = true;
       return 0;
     }
     case 7: {
