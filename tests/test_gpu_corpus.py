@@ -39,6 +39,23 @@ def test_small_dataset_merge(engine, oracle, dataset):
     print(f"fast {s['docs_fast']} exact {s['docs_exact']}")
 
 
+# Routing of the 5,320 corpus documents (round 5): k_lean takes the editor-shaped ones, the
+# workgroup fast path the rich-content ones, the tiled kernel the 18 above the fast path's LDS
+# capacities; none needs the exact engine (the tiny-document hand-over serves only batches of
+# >= 65,536 documents) or the grid paths.  Update with the routing when it changes on purpose.
+CORPUS_PATHS = {"docs_lean": 1385, "docs_fast": 3917, "docs_big": 18, "docs_exact": 0, "docs_tiny": 0,
+                "docs_giant": 0, "docs_error": 0}
+
+
+def test_small_dataset_paths(engine, oracle, dataset):
+    """Per-path document counts on the reference corpus (bit-exact output checked as well)."""
+    out, off, st = check_batch(engine, oracle, dataset)
+    s = engine.stats()
+    got = {k: int(s[k]) for k in CORPUS_PATHS}
+    assert got == CORPUS_PATHS, got
+    assert sum(got[k] for k in ("docs_lean", "docs_fast", "docs_big", "docs_exact", "docs_giant")) == dataset.n_docs
+
+
 def test_small_dataset_exact_engine(oracle, dataset):
     import ymerge
     os.environ["YMERGE_FAST_THREADS"] = "0"

@@ -15,7 +15,7 @@ fi
 i=0
 for cmd in "$@"; do
   i=$((i+1))
-  ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_$i -o p --output-format csv -- $(echo $cmd | sed "s,tools/,$GRAFT_REPO_ROOT/tools/,g") > $OUT/cmd_$i.log 2>&1 ) || { echo "cmd $i failed: $cmd"; tail -30 $OUT/cmd_$i.log; exit 1; }
+  ( cd $GRAFT_REPO_ROOT && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_$i -o p --output-format csv -- $cmd > $OUT/cmd_$i.log 2>&1 ) || { echo "cmd $i failed: $cmd"; tail -30 $OUT/cmd_$i.log; exit 1; }
   echo "== $cmd"; tail -6 $OUT/cmd_$i.log
   f=$(ls $OUT/prof_$i/*/p_kernel_stats.csv 2>/dev/null | head -1); [ -n "$f" ] && cut -d, -f1-4 "$f" | head -14
 done

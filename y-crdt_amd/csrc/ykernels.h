@@ -45,6 +45,7 @@ constexpr uint32_t LP_MIN_LEN = 8192;
 // the exact walk is one wavefront stepping serially (~1,800 cycles a varint), a 5 KB rich update
 // ~6 ms of one workgroup's time (env YMERGE_LP_MID)
 constexpr uint32_t LP_MID_LEN = 128;
+constexpr uint32_t LP_EXT_T = 1024; // positions per k_lp_ext tile
 // and every update of >= LP_DIRECT_LEN bytes, without the fast lane walk first
 constexpr uint32_t LP_DIRECT_LEN = 1024;
 // k_decode workgroups with staged updates for the exact walk (k_decode_exact): count at word
@@ -73,7 +74,7 @@ enum : uint32_t {                 // meta words
 enum : uint32_t { // flags
   LPF_FALLBACK = 1, LPF_UNSUP = 2, LPF_SKIP = 4, LPF_ZGC = 8, LPF_PANIC = 16, LPF_MSEC = 32, LPF_RICH = 64, LPF_ORDER = 128
 };
-enum : uint32_t { LPG_CHUNKS = 0, LPG_SEGS, LPG_ORDS, LPG_SECS, LPG_N, LPG_WORDS = 8 };
+enum : uint32_t { LPG_CHUNKS = 0, LPG_SEGS, LPG_ORDS, LPG_SECS, LPG_N, LPG_TILES, LPG_WORDS = 8 };
 struct LpArgs {
   const uint8_t *bytes;
   const uint64_t *upd_off;
@@ -88,8 +89,9 @@ struct LpArgs {
   uint64_t *blen, *sblen;    // [ocap] clock lengths in block order, scan [ocap + 1]
   uint32_t *omap;            // [ocap] record word + 1 of a stored block, 0 otherwise
   uint64_t *fb;              // updates left to the exact walker (k_decode_huge)
+  uint64_t *tmap;            // [tcap] k_lp_ext tiles: (entry << 32) | tile within the entry
   uint64_t *scan_tmp;
-  uint32_t pcap, ccap, scap, seccap, ocap;
+  uint32_t pcap, ccap, scap, seccap, ocap, tcap;
   uint32_t v1x;
   uint32_t mid; // k_decode lists updates of >= mid bytes its fast walk cannot take (LP_MID_LEN)
 };

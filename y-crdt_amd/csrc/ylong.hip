@@ -202,28 +202,30 @@ __device__ __forceinline__ void lp_fail(const LpArgs &a, uint32_t k) { atomicOr(
 // map; updates that do not fit the scratch (or are >= 1 GiB) go to the exact walker.
 __global__ void __launch_bounds__(1024) k_lp_plan(LpArgs a) {
   __shared__ uint64_t ws[1024 / 64 + 1];
-  __shared__ uint32_t s_nch;
+  __shared__ uint32_t s_nch, s_nt;
   const uint32_t n = a.huge[0] < HUGE_LIST ? a.huge[0] : HUGE_LIST;
   const uint64_t *list = (const uint64_t *)(a.huge + 4);
-  uint64_t cbase = 0, pbase = 0;
-  if (threadIdx.x == 0) s_nch = 0;
+  uint64_t cbase = 0, pbase = 0, tbase = 0;
+  if (threadIdx.x == 0) s_nch = s_nt = 0;
   __syncthreads();
   for (uint32_t k0 = 0; k0 < n; k0 += 1024) {
     const uint32_t k = k0 + threadIdx.x;
-    uint64_t L = 0, ch = 0;
+    uint64_t L = 0, ch = 0, nt = 0;
     if (k < n) {
       const uint64_t u = list[k];
       L = a.upd_off[u + 1] - a.upd_off[u];
       ch = (L + LP_CH - 1) / LP_CH;
+      nt = (L + LP_EXT_T - 1) / LP_EXT_T;
     }
-    uint64_t TL, TC;
+    uint64_t TL, TC, TT;
     const uint64_t preL = bscan_sum64<1024>(L < LP_UNST ? L : (uint64_t)LP_UNST, ws, TL);
     const uint64_t preC = bscan_sum64<1024>(ch, ws, TC);
-    const uint64_t pb = pbase + preL, cb = cbase + preC;
+    const uint64_t preT = bscan_sum64<1024>(nt, ws, TT);
+    const uint64_t pb = pbase + preL, cb = cbase + preC, tb = tbase + preT;
     if (k < n) {
       uint32_t *m = lp_meta(a, k);
       const uint64_t u = list[k];
-      bool fits = L < LP_UNST && pb + L <= a.pcap && cb + ch <= a.ccap;
+      bool fits = L < LP_UNST && pb + L <= a.pcap && cb + ch <= a.ccap && tb + nt <= a.tcap;
       m[LPM_U] = (uint32_t)u;
       m[LPM_U + 1] = (uint32_t)(u >> 32);
       m[LPM_L] = (uint32_t)L;
@@ -233,15 +235,19 @@ __global__ void __launch_bounds__(1024) k_lp_plan(LpArgs a) {
       m[LPM_FLAGS] = fits ? 0u : LPF_FALLBACK;
       if (fits) { // (the updates that fit are a prefix of the list: the bases only grow)
         for (uint32_t c = 0; c < ch; c++) a.c2e[cb + c] = k;
+        for (uint32_t q = 0; q < nt; q++) a.tmap[tb + q] = ((uint64_t)k << 32) | q;
         atomicMax(&s_nch, (uint32_t)(cb + ch));
+        atomicMax(&s_nt, (uint32_t)(tb + nt));
       }
     }
     pbase += TL;
     cbase += TC;
+    tbase += TT;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     a.g[LPG_CHUNKS] = s_nch; // chunks of the updates that fit (every c2e entry below is written)
+    a.g[LPG_TILES] = s_nt;   // k_lp_ext tiles of the updates that fit
     a.g[LPG_SEGS] = 0;
     a.g[LPG_ORDS] = 0;
     a.g[LPG_SECS] = 0;
@@ -252,24 +258,21 @@ __global__ void __launch_bounds__(1024) k_lp_plan(LpArgs a) {
 }
 
 // ------------------------------------------------------------------ k_lp_ext
-// workgroup per LP_EXT positions of a chunk (the whole GPU busy even for one update): the bytes
-// staged in LDS with a look-ahead, every position parsed speculatively
-constexpr uint32_t LPE_NT = 256, LP_EXT = 1024, LPE_LA = 512, LPE_PER = LP_EXT / LPE_NT;
+// workgroup per LP_EXT positions of an update (the whole GPU busy even for one update; tiles
+// listed per update by k_lp_plan, so a 200-byte update is one tile, not a chunk's eight): the
+// bytes staged in LDS with a look-ahead, every position parsed speculatively
+constexpr uint32_t LPE_NT = 256, LP_EXT = LP_EXT_T, LPE_LA = 512, LPE_PER = LP_EXT / LPE_NT;
 constexpr uint32_t LPE_STAGE_W = (LP_EXT + LPE_LA) / 4 + 4;
 __global__ void __launch_bounds__(LPE_NT) k_lp_ext(LpArgs a) {
   __shared__ __align__(16) uint32_t stage[LPE_STAGE_W];
-  __shared__ uint32_t s_k;
-  const uint32_t t = threadIdx.x, ntile = a.g[LPG_CHUNKS] * (LP_CH / LP_EXT);
+  const uint32_t t = threadIdx.x, ntile = a.g[LPG_TILES];
   for (uint32_t tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
-    const uint32_t c = tile / (LP_CH / LP_EXT);
-    __syncthreads();
-    if (t == 0) s_k = a.c2e[c];
-    __syncthreads();
-    const uint32_t *m = lp_meta(a, s_k);
+    const uint64_t tm = a.tmap[tile];
+    const uint32_t *m = lp_meta(a, (uint32_t)(tm >> 32));
     const uint64_t u = m[LPM_U] | ((uint64_t)m[LPM_U + 1] << 32);
     const uint32_t L = m[LPM_L], pb = m[LPM_PB];
-    const uint32_t ts = (c - m[LPM_CB]) * LP_CH + (tile % (LP_CH / LP_EXT)) * LP_EXT;
-    if (ts >= L) continue; // (uniform) past the update's end in its last chunk
+    const uint32_t ts = (uint32_t)tm * LP_EXT;
+    __syncthreads(); // (the previous tile's stage reads)
     const uint32_t te = ts + LP_EXT < L ? ts + LP_EXT : L;
     const uint8_t *ub = a.bytes + a.upd_off[u];
     const uint64_t abs0 = (uint64_t)(ub + ts);
@@ -362,10 +365,10 @@ __device__ __forceinline__ bool lp_seg(const LpArgs &a, uint32_t k, uint32_t sta
 }
 
 __global__ void __launch_bounds__(64) k_lp_stitch(LpArgs a) {
-  if (threadIdx.x) return;
   ym_set_grammar(a.v1x);
   const uint32_t n = a.g[LPG_N];
-  for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
+  // a lane per update (the hops are serial within an update; medium updates are one chunk)
+  for (uint32_t k = blockIdx.x * 64 + threadIdx.x; k < n; k += gridDim.x * 64) {
     uint32_t *m = lp_meta(a, k);
     if (m[LPM_FLAGS] & LPF_FALLBACK) continue;
     const uint64_t u = m[LPM_U] | ((uint64_t)m[LPM_U + 1] << 32);
@@ -806,11 +809,11 @@ void launch_long_decode(const LpArgs &a, hipStream_t s) {
   const uint32_t gch = a.ccap < 1024 ? a.ccap : 1024;
   hipLaunchKernelGGL(k_lp_ext, dim3(2048), dim3(LPE_NT), 0, s, a);
   hipLaunchKernelGGL(k_lp_chunk, dim3(gch ? gch : 1), dim3(LP_NT), 0, s, a);
-  hipLaunchKernelGGL(k_lp_stitch, dim3(256), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(k_lp_stitch, dim3(1024), dim3(64), 0, s, a);
   hipLaunchKernelGGL(k_lp_expand, dim3(1024), dim3(LPX_NT), 0, s, a);
   launch_scan_u64(a.blen, a.sblen, a.ocap, a.scan_tmp, s, a.g + LPG_ORDS);
   hipLaunchKernelGGL(k_lp_clock, dim3(1024), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(k_lp_ds, dim3(256), dim3(LPD_NT), 0, s, a);
+  hipLaunchKernelGGL(k_lp_ds, dim3(2048), dim3(LPD_NT), 0, s, a);
   hipLaunchKernelGGL(k_lp_final, dim3(16), dim3(256), 0, s, a);
 }
 

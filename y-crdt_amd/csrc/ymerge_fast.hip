@@ -227,6 +227,7 @@ __global__ void __launch_bounds__(DEC_NT, 8) k_decode(const uint8_t *bytes, cons
 // (each stages on its own), and take overflow words from the tile's bump in the exact list (a
 // global atomic)
 constexpr uint32_t EX_NT = 256, EX_NW = EX_NT / 64, EX_SPLIT = 8;
+template <bool LANE>
 __global__ void __launch_bounds__(EX_NT) k_decode_exact(const uint8_t *bytes, const uint64_t *upd_off,
                                                        uint64_t n_upd, uint32_t *rec, uint32_t *ovf,
                                                        uint32_t *huge, uint32_t v1x, uint32_t huge_base,
@@ -237,8 +238,9 @@ __global__ void __launch_bounds__(EX_NT) k_decode_exact(const uint8_t *bytes, co
   __shared__ uint16_t sl_lane[DEC_NT], go_lane[DEC_NT];
   ym_set_grammar(v1x);
   const uint32_t t = threadIdx.x, wv = t >> 6, lane = t & 63, ntiles = huge[EXQ_COUNT];
-  const uint32_t part = blockIdx.x % EX_SPLIT, nslot = gridDim.x / EX_SPLIT; // (grid: a multiple of EX_SPLIT)
-  for (uint32_t k = blockIdx.x / EX_SPLIT; k < ntiles; k += nslot) {
+  constexpr uint32_t SPLIT = LANE ? 1 : EX_SPLIT; // (lane mode: a workgroup walks 256 pending updates at once)
+  const uint32_t part = blockIdx.x % SPLIT, nslot = gridDim.x / SPLIT; // (grid: a multiple of SPLIT)
+  for (uint32_t k = blockIdx.x / SPLIT; k < ntiles; k += nslot) {
     const uint32_t b = huge[EXQ_LIST + 2 * k];
     uint32_t *ovf_top = huge + EXQ_LIST + 2 * k + 1;
     const uint64_t g0 = (uint64_t)b * DEC_NT;
@@ -252,7 +254,7 @@ __global__ void __launch_bounds__(EX_NT) k_decode_exact(const uint8_t *bytes, co
       s_max = 0;
     }
     __syncthreads();
-    for (uint32_t u = part + EX_SPLIT * t; u < rl; u += EX_SPLIT * EX_NT) // this workgroup's share of the tile
+    for (uint32_t u = part + SPLIT * t; u < rl; u += SPLIT * EX_NT) // this workgroup's share of the tile
       if ((rec[(g0 + u) * REC_WORDS] & (REC_SLOW | REC_STAGED)) == (REC_SLOW | REC_STAGED))
         sl_lane[atomicAdd(&n_sl, 1u)] = (uint16_t)u;
     __syncthreads();
@@ -282,6 +284,42 @@ __global__ void __launch_bounds__(EX_NT) k_decode_exact(const uint8_t *bytes, co
       }
       __syncthreads();
       nround++;
+      if (LANE) { // one update per lane (updates here are short: the long ones took the parallel parse)
+        for (uint32_t q = t; q < n_go; q += EX_NT) {
+          const uint64_t tw0 = dbg ? __builtin_amdgcn_s_memtime() : 0;
+          const uint64_t j = g0 + go_lane[q];
+          const uint64_t a0 = upd_off[j], a1 = upd_off[j + 1];
+          RegSink s;
+          s.nb = s.ne = s.nr = 0;
+          s.unsupported = s.big_ds = false;
+          s.ubase = 0;
+          const uint32_t base = (uint32_t)(a0 - sbase), len = (uint32_t)(a1 - a0);
+          SCur c{(const uint8_t *)stage + base, len, 0, stage, base};
+          const int e = smwalk_update(c, s);
+          uint32_t w0, w1, w2, w3, w4, w5;
+          rec_pack(s, e, w0, w1, w2, w3, w4, w5);
+          if (e == 0 && ((w0 >> 10) & 3) == REC_COMPLEX && !s.big_ds) {
+            const uint32_t need = 5 * s.nb + 2 * s.ne + 3 * s.nr;
+            const uint32_t off = need <= DEC_OVF ? atomicAdd(ovf_top, need) : DEC_OVF;
+            const uint32_t at = off + need <= DEC_OVF ? b * DEC_OVF + off : ovf_global(huge, need, huge_base, huge_cap);
+            if (at != 0xFFFFFFFFu) { // second walk: the overflow words
+              OvfFill f{ovf + at, s.nb, s.ne, 0, 0, 0};
+              SCur c2{(const uint8_t *)stage + base, len, 0, stage, base};
+              smwalk_update(c2, f);
+              w0 |= REC_OVF;
+              w4 = at;
+            } else {
+              w0 = REC_SLOW; // no overflow room: the merge kernels walk it
+              w1 = w2 = w3 = w4 = w5 = 0;
+            }
+          }
+          uint2 *o = (uint2 *)(rec + j * REC_WORDS);
+          o[0] = make_uint2(w0, w1);
+          o[1] = make_uint2(w2, w3);
+          o[2] = make_uint2(w4, w5);
+          if (dbg) atomicMax(&s_max, ((__builtin_amdgcn_s_memtime() - tw0) << 24) | (j & 0xFFFFFF));
+        }
+      } else
       for (uint32_t q = wv; q < n_go; q += EX_NW) { // one update per wavefront (uniform in it)
         const uint64_t tw0 = dbg ? __builtin_amdgcn_s_memtime() : 0;
         const uint64_t j = g0 + go_lane[q];
@@ -421,8 +459,15 @@ void launch_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_upd
   hipLaunchKernelGGL(k_decode, dim3((unsigned)nwg), dim3(DEC_NT), 0, s, bytes, upd_off, n_updates, rec, ovf, huge,
                      v1x, lp_min, lp ? LP_DIRECT_LEN : 0xFFFFFFFFu, (uint32_t)(nwg * DEC_OVF), (uint64_t)huge_cap);
   const uint32_t base = (uint32_t)(nwg * DEC_OVF);
-  hipLaunchKernelGGL(k_decode_exact, dim3((unsigned)(nwg < 512 ? nwg : 512) * EX_SPLIT), dim3(EX_NT), 0, s, bytes, upd_off,
-                     n_updates, rec, ovf, huge, v1x, (uint32_t)(nwg * DEC_OVF), (uint64_t)huge_cap, dbg);
+  static const bool lockstep = getenv("YMERGE_EXACT_LOCKSTEP") != nullptr; // (A/B: one update per wavefront)
+  if (lockstep)
+    hipLaunchKernelGGL(k_decode_exact<false>, dim3((unsigned)(nwg < 512 ? nwg : 512) * EX_SPLIT), dim3(EX_NT), 0, s,
+                       bytes, upd_off, n_updates, rec, ovf, huge, v1x, (uint32_t)(nwg * DEC_OVF), (uint64_t)huge_cap,
+                       dbg);
+  else // a workgroup per listed tile (the list is shorter than nwg)
+    hipLaunchKernelGGL(k_decode_exact<true>, dim3((unsigned)(nwg < 65536 ? nwg : 65536)), dim3(EX_NT), 0, s,
+                       bytes, upd_off, n_updates, rec, ovf, huge, v1x, (uint32_t)(nwg * DEC_OVF), (uint64_t)huge_cap,
+                       dbg);
   if (lp) {
     LpArgs a = *lp;
     a.bytes = bytes;

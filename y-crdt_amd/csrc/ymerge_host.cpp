@@ -332,10 +332,10 @@ static const ym::LpArgs *lp_args(ymerge_ctx *c, uint64_t n_bytes, uint32_t v1x) 
   if (!c->long_parse) return nullptr;
   const uint64_t pcap = std::min<uint64_t>(n_bytes + 16, LP_PMAX);
   const uint64_t ccap = pcap / ym::LP_CH + ym::HUGE_LIST, scap = 4 * ccap + 65536, seccap = pcap / 3 + 16,
-                 ocap = pcap / 2 + ym::HUGE_LIST;
+                 ocap = pcap / 2 + ym::HUGE_LIST, tcap = pcap / ym::LP_EXT_T + ym::HUGE_LIST;
   const uint64_t tmp = ym::scan_tmp_elems((uint32_t)ocap) + 2;
   const uint64_t bytes = 64ull * ym::HUGE_LIST + 64 + 4 * ccap + 4 * pcap + 8 * pcap + 4 * ym::LP_SEGW * scap +
-                         16 * seccap + 8 * ocap + 8 * (ocap + 1) + 4 * ocap + 8ull * ym::HUGE_LIST + 8 * tmp + 256;
+                         16 * seccap + 8 * ocap + 8 * (ocap + 1) + 4 * ocap + 8ull * ym::HUGE_LIST + 8 * tmp + 8 * tcap + 512;
   if (!c->lp.ensure(bytes)) {
     (void)hipGetLastError();
     return nullptr;
@@ -359,11 +359,13 @@ static const ym::LpArgs *lp_args(ymerge_ctx *c, uint64_t n_bytes, uint32_t v1x) 
   a.omap = (uint32_t *)take(4 * ocap);
   a.fb = (uint64_t *)take(8ull * ym::HUGE_LIST);
   a.scan_tmp = (uint64_t *)take(8 * tmp);
+  a.tmap = (uint64_t *)take(8 * tcap);
   a.pcap = (uint32_t)pcap;
   a.ccap = (uint32_t)ccap;
   a.scap = (uint32_t)scap;
   a.seccap = (uint32_t)seccap;
   a.ocap = (uint32_t)ocap;
+  a.tcap = (uint32_t)tcap;
   a.v1x = v1x;
   a.mid = c->lp_mid;
   return &a;
