@@ -139,16 +139,34 @@ struct Writer {
     n += k;
   }
 };
-// no byte >= 0x80 in s[0, n) (independent loads, 16 in flight)
+// no byte >= 0x80 in s[0, n): 16-byte aligned vector loads, 128 bytes in flight per step (the
+// aligned chunks covering s[0, n) stay inside the padded arena); a lane checking a 100 KB
+// pasted string byte by byte held k_lp_expand for 17 ms on the editing traces
 __device__ __forceinline__ bool bytes_ascii(const uint8_t *s, uint32_t n) {
-  uint32_t hi = 0, i = 0;
-  for (; i + 16 <= n; i += 16) {
+  if (n == 0) return true;
+  const uint64_t lo = (uint64_t)s, hi = lo + n;
+  for (uint64_t a = lo & ~15ull; a < hi; a += 128) {
+    uint4 x[8];
 #pragma unroll
-    for (uint32_t j = 0; j < 16; j++) hi |= s[i + j];
-    if (hi & 0x80) return false;
+    for (int k = 0; k < 8; k++)
+      if (a + 16 * k < hi) x[k] = *(const uint4 *)(a + 16 * k);
+    uint32_t orw = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      if (a + 16 * k >= hi) break;
+      const uint32_t w[4] = {x[k].x, x[k].y, x[k].z, x[k].w};
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint64_t wb = a + 16 * k + 4 * j;
+        uint32_t m = 0x80808080u;
+        if (wb < lo) m = lo - wb >= 4 ? 0u : m & (~0u << (8 * (uint32_t)(lo - wb)));
+        if (wb + 4 > hi) m = hi <= wb ? 0u : m & ((1u << (8 * (uint32_t)(hi - wb))) - 1u);
+        orw |= w[j] & m;
+      }
+    }
+    if (orw) return false;
   }
-  for (; i < n; i++) hi |= s[i];
-  return !(hi & 0x80);
+  return true;
 }
 template <class W> __device__ __forceinline__ void w_var(W &w, uint64_t v) {
   while (v >= 0x80) {
@@ -196,10 +214,60 @@ __device__ __forceinline__ uint32_t ch_len16(uint32_t c) { return (c & 0xFFFF) =
 __device__ __forceinline__ uint32_t ch_len8(uint32_t c) {
   return c < 0x80 ? 1 : c < 0x800 ? 2 : c < 0x10000 ? 3 : 4;
 }
+// UTF-16 length of s[0, n) when every sequence is complete and shortest-form (then utf8_next
+// consumes exactly the sequence a lead announces, ch_len8 of every char is its byte count, and
+// the split at the full UTF-16 length is n): non-continuation bytes + 4-byte leads.  false =
+// something else: the serial walk decides.  16-byte aligned vector loads, 64 bytes a step, the
+// bytes checked in registers (a 69 KB pasted string of the editing traces walked byte by byte
+// over HBM took k_lp_expand 17 ms).
+__device__ __forceinline__ bool str_fast16(const uint8_t *s, uint32_t n, uint32_t &len) {
+  const uint64_t lo = (uint64_t)s, hi = lo + n;
+  uint32_t units = 0, pend = 0, min2 = 0; // continuation bytes still due; lower bound of the next one
+  for (uint64_t a = lo & ~15ull; a < hi; a += 64) {
+    uint4 x[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (a + 16 * k < hi) x[k] = *(const uint4 *)(a + 16 * k);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t w[4] = {x[k].x, x[k].y, x[k].z, x[k].w};
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        const uint64_t at = a + 16 * k + j;
+        if (at < lo || at >= hi) continue;
+        const uint32_t b = (w[j >> 2] >> (8 * (j & 3))) & 0xFF;
+        if (pend) {
+          if ((b & 0xC0) != 0x80 || b < min2) return false;
+          min2 = 0;
+          pend--;
+        } else if (b < 0x80) {
+          units++;
+        } else if (b < 0xC2) { // a continuation byte at a lead, or an overlong 2-byte lead
+          return false;
+        } else if (b < 0xE0) {
+          units++;
+          pend = 1;
+        } else if (b < 0xF0) {
+          units++;
+          pend = 2;
+          min2 = b == 0xE0 ? 0xA0 : 0;
+        } else {
+          units += 2;
+          pend = 3;
+          min2 = (b & 7) == 0 ? 0x90 : 0;
+        }
+      }
+    }
+  }
+  len = units;
+  return pend == 0;
+}
 // SplittableString::len(Utf16) (block.rs:1391-1401)
 __device__ __forceinline__ uint32_t str_len16(const uint8_t *s, uint32_t n) {
   if (n == 1) return 1;
   uint32_t k = 0, i = 0;
+  if (n >= 64 && str_fast16(s, n, k)) return k;
+  k = 0;
   while (i < n) k += ch_len16(utf8_next(s, n, i));
   return k;
 }
@@ -596,6 +664,22 @@ struct BlockInfo {
   uint32_t len;     // clock length (0 => dropped Item)
   uint32_t canon;   // canonical encoded size (valid after measure)
 };
+// a non-ASCII String content of n bytes: its UTF-16 length and the encode_slice split at that
+// length (block.rs:1718-1729): panics off a char boundary, re-encodes when shorter
+__device__ __forceinline__ void str_info16(const uint8_t *s, uint32_t n, BlockInfo &bi) {
+  uint32_t l16;
+  if (n >= 64 && str_fast16(s, n, l16)) { // (complete shortest-form sequences: the split is s)
+    bi.len = l16;
+    return;
+  }
+  bi.len = str_len16(s, n);
+  if (bi.len > 1) {
+    uint32_t bo;
+    if (str_split16(s, n, bi.len, bo)) bi.enc_panic = true;
+    else if (bo != n) bi.reenc = true;
+  }
+}
+
 struct DocOpts {
   bool skip_gc, auto_load, has_cid, enc_bytes;
   uint32_t cid_pos, cid_len;
@@ -702,12 +786,7 @@ __device__ __noinline__ SlowRes parse_content_slow(const uint8_t *p, uint32_t n,
       bi.reenc |= !cn;
       YM_TRY(rd_skip(c, v));
       const uint8_t *s = c.p + c.i - v;
-      bi.len = str_len16(s, v);
-      if (bi.len > 1) { // encode_slice splits at len UTF-16 units (block.rs:1718-1729)
-        uint32_t bo;
-        if (str_split16(s, v, bi.len, bo)) bi.enc_panic = true;
-        else if (bo != v) bi.reenc = true;
-      }
+      str_info16(s, v, bi);
       return 0;
     }
     case 5: case 6: { // Embed (json) / Format (key, json): re-serialised on encode
@@ -884,18 +963,11 @@ YM_INLINE int parse_block(Cur &c, BlockInfo &bi) {
       return 0;
     }
     // ASCII fast check: UTF-16 length = byte length and the full split is the whole string
-    bool ascii = true;
-    for (uint32_t q = 0; q < v; q++) ascii &= s[q] < 0x80;
-    if (ascii) {
+    if (bytes_ascii(s, v)) {
       bi.len = v;
       return 0;
     }
-    bi.len = str_len16(s, v);
-    if (bi.len > 1) { // encode_slice splits at len UTF-16 units (block.rs:1718-1729)
-      uint32_t bo;
-      if (str_split16(s, v, bi.len, bo)) bi.enc_panic = true;
-      else if (bo != v) bi.reenc = true;
-    }
+    str_info16(s, v, bi);
     return 0;
   }
   SlowRes r = parse_content_slow(c.p, c.n, c.i, ref, bi.reenc);

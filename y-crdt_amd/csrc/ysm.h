@@ -337,12 +337,7 @@ template <class S, class C> YM_INLINE int smwalk_update(C &c, S &s) {
         break;
       }
       const uint8_t *sp = c.p + s0; // non-ASCII: UTF-16 length on the plain pointer (cold)
-      bi.len = str_len16(sp, v);
-      if (bi.len > 1) {
-        uint32_t bo;
-        if (str_split16(sp, v, bi.len, bo)) bi.enc_panic = true;
-        else if (bo != v) bi.reenc = true;
-      }
+      str_info16(sp, v, bi);
       break;
     }
     case W_NDS:

@@ -232,12 +232,7 @@ YM_INLINE int wparse_block(WCur &c, BlockInfo &bi) {
       return 0;
     }
     const uint8_t *s = c.p + s0; // non-ASCII: UTF-16 length on the plain pointer (cold)
-    bi.len = str_len16(s, v);
-    if (bi.len > 1) {
-      uint32_t bo;
-      if (str_split16(s, v, bi.len, bo)) bi.enc_panic = true;
-      else if (bo != v) bi.reenc = true;
-    }
+    str_info16(s, v, bi);
     return 0;
   }
   SlowRes r = parse_content_slow(c.p, c.n, c.i, ref, bi.reenc);
