@@ -19,6 +19,9 @@ struct dim3 {
   unsigned x, y, z;
   dim3(unsigned a = 1, unsigned b = 1, unsigned c = 1) : x(a), y(b), z(c) {}
 };
+struct uint4 {
+  uint32_t x, y, z, w;
+};
 struct emu_idx {
   unsigned x, y, z;
 };

@@ -20,7 +20,11 @@ BIG_NAMES = ["gather", "sort", "classify", "write", "deleteset"]
 
 def main_big(n, kind="c3"):
     """Tiled-kernel documents (k_big_merge, marker 0xB16 in slot 7) of a C3-style (or C4) batch."""
-    b = workloads.zipf_docs(n, seed=0x5EED) if kind == "c3" else workloads.delete_heavy_docs(n)
+    if kind == "traces":
+        b = workloads.traces_batch()
+        n = b.n_docs
+    else:
+        b = workloads.zipf_docs(n, seed=0x5EED) if kind == "c3" else workloads.delete_heavy_docs(n)
     e = ymerge.Engine(0)
     e.merge_host(b.data, b.upd_off, b.doc_upd)
     L = ymerge.lib()
@@ -198,6 +202,8 @@ def main():
         return main_zipf(int(sys.argv[2]) if len(sys.argv) > 2 else 20000)
     if len(sys.argv) > 1 and sys.argv[1] == "big":
         return main_big(int(sys.argv[2]) if len(sys.argv) > 2 else 20000)
+    if len(sys.argv) > 1 and sys.argv[1] == "traces":
+        return main_big(0, "traces")
     if len(sys.argv) > 1 and sys.argv[1] == "c4":
         return main_big(int(sys.argv[2]) if len(sys.argv) > 2 else 2000, "c4")
     if len(sys.argv) > 1 and sys.argv[1] == "c1":

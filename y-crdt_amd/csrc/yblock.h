@@ -176,19 +176,23 @@ template <int NT> YM_INLINE void bitonic(uint64_t *k, uint32_t *v, uint32_t n) {
 // One walk per update.  The common shapes (<= 1 block, <= 1 DeleteSet entry with <= 2
 // ranges) are kept in registers until the round's scan places them; any other update
 // is re-walked once by FastFill at its scanned positions.
-struct RegSink {
+// TRACK: the section-order check (REC_ORDER); k_decode's fast walk leaves it to the second walk
+// of its multi-record updates (OvfFill), which keeps its own walk within 64 VGPRs
+template <bool TRACK> struct RegSinkT {
   uint32_t nb, ne, nr;
   bool unsupported, big_ds;
   bool misorder = false;                            // REC_ORDER
-  uint32_t nsec = 0, last_cl = 0;
+  uint32_t last_cl = 0xFFFFFFFFu;                   // (a first section of client 2^32 - 1 is flagged too)
   uint32_t b_client, b_clock, b_len, b_pos, b_meta; // first block
   uint32_t e_client;                                // first DeleteSet entry
   uint32_t r0s, r0e, r1s, r1e;                      // its first two ranges
   const uint8_t *doc;
   uint32_t doc_len, ubase;
   YM_INLINE void on_section(uint32_t client) {
-    if (nsec++ && client >= last_cl) misorder = true;
-    last_cl = client;
+    if (TRACK) {
+      misorder |= client >= last_cl;
+      last_cl = client;
+    }
   }
   YM_INLINE int on_block(uint32_t client, uint32_t clock, const BlockInfo &bi, uint32_t bpos, uint32_t blen) {
     if (bi.unsupported) unsupported = true;
@@ -224,6 +228,7 @@ struct RegSink {
   }
   YM_INLINE int on_ds_done() { return 0; }
 };
+using RegSink = RegSinkT<true>;
 
 struct FastFill {
   uint32_t *bc, *bk, *bl, *bp, *bm, *ec, *et, *rs, *re, *ri;
@@ -275,7 +280,12 @@ struct OvfFill {
   uint32_t NBt, NEt; // totals of this update (RegSink pass)
   uint32_t nb, ne, nr;
   bool on = true; // writes (a wave walking one update in lockstep: lane 0 only)
-  YM_INLINE void on_section(uint32_t) {}
+  bool misorder = false; // REC_ORDER (RegSinkT)
+  uint32_t last_cl = 0xFFFFFFFFu;
+  YM_INLINE void on_section(uint32_t client) {
+    misorder |= client >= last_cl;
+    last_cl = client;
+  }
   YM_INLINE int on_block(uint32_t client, uint32_t clock, const BlockInfo &bi, uint32_t bpos, uint32_t blen) {
     if (bi.kind == BK_SKIP) return 0;
     if (on) {
@@ -314,7 +324,8 @@ struct OvfFill {
 };
 
 // sink -> record (ykernels.h REC_*); positions stay relative to the update
-YM_INLINE void rec_pack(const RegSink &s, int e, uint32_t &w0, uint32_t &w1, uint32_t &w2, uint32_t &w3, uint32_t &w4,
+template <bool T>
+YM_INLINE void rec_pack(const RegSinkT<T> &s, int e, uint32_t &w0, uint32_t &w1, uint32_t &w2, uint32_t &w3, uint32_t &w4,
                         uint32_t &w5) {
   w0 = (uint32_t)e & 0xFF;
   w1 = w2 = w3 = w4 = w5 = 0;

@@ -134,7 +134,8 @@ void launch_ls_collect(const LpArgs &a, uint32_t *list, hipStream_t s);
 void launch_ls_doc(const LsArgs &a, int phase, hipStream_t s);
 void launch_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_updates, uint32_t *rec, uint32_t *ovf,
                    uint32_t *huge, uint32_t huge_cap, hipStream_t s, const LpArgs *lp = nullptr, uint32_t v1x = 0,
-                   uint64_t *dbg = nullptr);
+                   uint64_t *dbg = nullptr,
+                   uint32_t *h_probe = nullptr);
 
 // LDS capacities of the one-workgroup-per-document fast path (per document)
 struct FastCaps {

@@ -715,6 +715,7 @@ template <int NT> struct BigShared {
   __align__(16) uint8_t un[BIG_UNION + 64];
 };
 
+constexpr uint32_t BIG_COPY_MIN = 1024, BIG_COPY_N = 32;
 template <int NT, int OCC>
 __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t *counts, const uint64_t *scr_off,
                                                        uint32_t *scratch, FastOut o) {
@@ -722,6 +723,10 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
   const uint32_t d = o.big_list[blockIdx.x];
   if (d >= b.n_docs || o.path[d] != 2) return;
   __shared__ BigShared<NT> S;
+  // verbatim blocks of >= BIG_COPY_MIN bytes of a write tile: copied by the whole workgroup
+  // after the tile (one lane copying a 69 KB pasted string held a trace document ~4 M cycles)
+  __shared__ uint32_t s_nbig, s_bl[BIG_COPY_N];
+  __shared__ uint64_t s_bd[BIG_COPY_N], s_bs[BIG_COPY_N];
   const uint32_t t = threadIdx.x;
   uint32_t *ws = S.ws, *sc = S.sc;
   const uint32_t NB = counts[4 * d + 1], NE = counts[4 * d + 2], NR = counts[4 * d + 3];
@@ -1251,6 +1256,8 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
       const uint32_t phase = (uint32_t)((uintptr_t)(out + o0) & 15);
       const bool staged = phase + TT <= BIG_UNION;
       uint8_t *dst = staged ? S.un + phase : out + o0;
+      if (t == 0) s_nbig = 0;
+      __syncthreads();
       if (valid && s) {
         Writer w{dst, pre};
         if (hd) {
@@ -1270,7 +1277,33 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
             Writer w2 = w;
             emit_block(in, nbytes, p, c, k, l, 0, w2);
           } else {
-            copy_bytes16(w.p + w.n, in + p, mt >> 8);
+            const uint32_t bl = mt >> 8;
+            uint32_t q = BIG_COPY_N;
+            if (bl >= BIG_COPY_MIN) q = atomicAdd(&s_nbig, 1u);
+            if (q < BIG_COPY_N) {
+              s_bd[q] = (uint64_t)(w.p + w.n);
+              s_bs[q] = (uint64_t)(in + p);
+              s_bl[q] = bl;
+            } else {
+              copy_bytes16(w.p + w.n, in + p, bl);
+            }
+          }
+        }
+      }
+      __syncthreads();
+      {
+        const uint32_t nbig = s_nbig < BIG_COPY_N ? s_nbig : BIG_COPY_N;
+        for (uint32_t e = 0; e < nbig; e++) { // 4 bytes a lane: the loads, then the stores
+          uint8_t *d = (uint8_t *)s_bd[e];
+          const uint8_t *sp = (const uint8_t *)s_bs[e];
+          const uint32_t bl = s_bl[e];
+          for (uint32_t o = 4 * t; o < bl; o += 4 * NT) {
+            const uint32_t b0 = sp[o], b1 = o + 1 < bl ? sp[o + 1] : 0, b2 = o + 2 < bl ? sp[o + 2] : 0,
+                           b3 = o + 3 < bl ? sp[o + 3] : 0;
+            d[o] = (uint8_t)b0;
+            if (o + 1 < bl) d[o + 1] = (uint8_t)b1;
+            if (o + 2 < bl) d[o + 2] = (uint8_t)b2;
+            if (o + 3 < bl) d[o + 3] = (uint8_t)b3;
           }
         }
       }

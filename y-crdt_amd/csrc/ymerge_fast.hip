@@ -149,7 +149,7 @@ __global__ void __launch_bounds__(DEC_NT, 8) k_decode(const uint8_t *bytes, cons
   if (i < n_upd) {
     const uint64_t a0 = upd_off[i], a1 = upd_off[i + 1];
     const uint32_t ulen = (uint32_t)(a1 - a0);
-    RegSink s;
+    RegSinkT<false> s; // (sections checked by the second walk)
     s.nb = s.ne = s.nr = 0;
     s.unsupported = s.big_ds = false;
     s.ubase = 0;
@@ -211,6 +211,7 @@ __global__ void __launch_bounds__(DEC_NT, 8) k_decode(const uint8_t *bytes, cons
     const uint64_t a0 = upd_off[j], a1 = upd_off[j + 1];
     OvfFill f{ovf + cx_at[q], cx_nb[q], cx_ne[q], 0, 0, 0};
     fast_walk(stage, (uint32_t)(a0 - sbase), (uint32_t)(a1 - a0), f);
+    if (f.misorder) rec[j * REC_WORDS] |= REC_ORDER; // (written by this workgroup before the barrier)
   }
 }
 
@@ -450,7 +451,7 @@ __global__ void __launch_bounds__(64) k_decode_huge(const uint8_t *bytes, const 
 // given, the exact lockstep walk for the ones it leaves (errors, bounds); without it every listed
 // update takes the exact walk
 void launch_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_updates, uint32_t *rec, uint32_t *ovf,
-                   uint32_t *huge, uint32_t huge_cap, hipStream_t s, const LpArgs *lp, uint32_t v1x, uint64_t *dbg) {
+                   uint32_t *huge, uint32_t huge_cap, hipStream_t s, const LpArgs *lp, uint32_t v1x, uint64_t *dbg, uint32_t *h_probe) {
   if (!n_updates) return;
   const uint64_t nwg = (n_updates + DEC_NT - 1) / DEC_NT;
   hipMemsetAsync(huge, 0, 16, s);
@@ -459,8 +460,20 @@ void launch_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_upd
   hipLaunchKernelGGL(k_decode, dim3((unsigned)nwg), dim3(DEC_NT), 0, s, bytes, upd_off, n_updates, rec, ovf, huge,
                      v1x, lp_min, lp ? LP_DIRECT_LEN : 0xFFFFFFFFu, (uint32_t)(nwg * DEC_OVF), (uint64_t)huge_cap);
   const uint32_t base = (uint32_t)(nwg * DEC_OVF);
+  // (h_probe, pinned host words: one round trip reads whether k_decode listed anything for the
+  // exact walk or the long-update path; a batch with neither skips their ~12 launches, ~60 us)
+  bool any_exact = true, any_long = true;
+  if (h_probe) {
+    hipMemcpyAsync(h_probe, huge, 4, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(h_probe + 1, huge + EXQ_COUNT, 4, hipMemcpyDeviceToHost, s);
+    if (hipStreamSynchronize(s) == hipSuccess) {
+      any_long = h_probe[0] != 0;
+      any_exact = h_probe[1] != 0;
+    }
+  }
   static const bool lockstep = getenv("YMERGE_EXACT_LOCKSTEP") != nullptr; // (A/B: one update per wavefront)
-  if (lockstep)
+  if (!any_exact) {
+  } else if (lockstep)
     hipLaunchKernelGGL(k_decode_exact<false>, dim3((unsigned)(nwg < 512 ? nwg : 512) * EX_SPLIT), dim3(EX_NT), 0, s,
                        bytes, upd_off, n_updates, rec, ovf, huge, v1x, (uint32_t)(nwg * DEC_OVF), (uint64_t)huge_cap,
                        dbg);
@@ -468,7 +481,8 @@ void launch_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_upd
     hipLaunchKernelGGL(k_decode_exact<true>, dim3((unsigned)(nwg < 65536 ? nwg : 65536)), dim3(EX_NT), 0, s,
                        bytes, upd_off, n_updates, rec, ovf, huge, v1x, (uint32_t)(nwg * DEC_OVF), (uint64_t)huge_cap,
                        dbg);
-  if (lp) {
+  if (!any_long) {
+  } else if (lp) {
     LpArgs a = *lp;
     a.bytes = bytes;
     a.upd_off = upd_off;

@@ -534,7 +534,8 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     hipEventRecord(c->ev[7], c->s);
     hipEventRecord(c->ev[0], c->s);
     ym::launch_decode(d_bytes, d_upd_off, n_updates, c->rec.as<uint32_t>(), c->ovf.as<uint32_t>(), c->huge.as<uint32_t>(),
-                      huge_words(n_bytes), c->s, lp_args(c, n_bytes, b.v1x), b.v1x);
+                      huge_words(n_bytes), c->s, lp_args(c, n_bytes, b.v1x), b.v1x, nullptr,
+                      (uint32_t *)(c->h_pinned + 24));
     hipEventRecord(c->ev[5], c->s);
     decoded = true;
     const int rc = run_giant(c, b, fo, 0, (uint32_t)n_updates, 0, n_bytes);
@@ -626,7 +627,8 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     }
     if (!decoded) // (the grid lane's records are still valid)
       ym::launch_decode(d_bytes, d_upd_off, n_updates, c->rec.as<uint32_t>(), c->ovf.as<uint32_t>(),
-                        c->huge.as<uint32_t>(), huge_words(n_bytes), c->s, lp_args(c, n_bytes, b.v1x), b.v1x, dbg);
+                        c->huge.as<uint32_t>(), huge_words(n_bytes), c->s, lp_args(c, n_bytes, b.v1x), b.v1x, dbg,
+                        (uint32_t *)(c->h_pinned + 24));
     if (dbg) {
       std::vector<uint64_t> h(nwg * 8);
       hipStreamSynchronize(c->s);
