@@ -218,11 +218,13 @@ __device__ __forceinline__ uint32_t ch_len8(uint32_t c) {
 // consumes exactly the sequence a lead announces, ch_len8 of every char is its byte count, and
 // the split at the full UTF-16 length is n): non-continuation bytes + 4-byte leads.  false =
 // something else: the serial walk decides.  16-byte aligned vector loads, 64 bytes a step, the
-// bytes checked in registers (a 69 KB pasted string of the editing traces walked byte by byte
-// over HBM took k_lp_expand 17 ms).
+// bytes checked four at a time in registers (SWAR: lead / continuation / overlong flags per
+// byte, the expected continuations shifted in from the previous word); a 69 KB pasted string of
+// the editing traces walked byte by byte over HBM took k_lp_expand 17 ms.
 __device__ __forceinline__ bool str_fast16(const uint8_t *s, uint32_t n, uint32_t &len) {
   const uint64_t lo = (uint64_t)s, hi = lo + n;
-  uint32_t units = 0, pend = 0, min2 = 0; // continuation bytes still due; lower bound of the next one
+  uint32_t units = 0, pl = 0, p3 = 0, p4 = 0, pe0 = 0, pf0 = 0, bad = 0; // previous word's flags
+  const uint32_t H = 0x80808080u;
   for (uint64_t a = lo & ~15ull; a < hi; a += 64) {
     uint4 x[4];
 #pragma unroll
@@ -230,37 +232,36 @@ __device__ __forceinline__ bool str_fast16(const uint8_t *s, uint32_t n, uint32_
       if (a + 16 * k < hi) x[k] = *(const uint4 *)(a + 16 * k);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      const uint32_t w[4] = {x[k].x, x[k].y, x[k].z, x[k].w};
+      const uint32_t ws[4] = {x[k].x, x[k].y, x[k].z, x[k].w};
 #pragma unroll
-      for (int j = 0; j < 16; j++) {
-        const uint64_t at = a + 16 * k + j;
-        if (at < lo || at >= hi) continue;
-        const uint32_t b = (w[j >> 2] >> (8 * (j & 3))) & 0xFF;
-        if (pend) {
-          if ((b & 0xC0) != 0x80 || b < min2) return false;
-          min2 = 0;
-          pend--;
-        } else if (b < 0x80) {
-          units++;
-        } else if (b < 0xC2) { // a continuation byte at a lead, or an overlong 2-byte lead
-          return false;
-        } else if (b < 0xE0) {
-          units++;
-          pend = 1;
-        } else if (b < 0xF0) {
-          units++;
-          pend = 2;
-          min2 = b == 0xE0 ? 0xA0 : 0;
-        } else {
-          units += 2;
-          pend = 3;
-          min2 = (b & 7) == 0 ? 0x90 : 0;
-        }
+      for (int j = 0; j < 4; j++) {
+        const uint64_t wb = a + 16 * k + 4 * j;
+        uint32_t vm = H; // valid bytes of this word (none past the end: its expectations fail there)
+        if (wb < lo) vm = lo - wb >= 4 ? 0u : vm & (~0u << (8 * (uint32_t)(lo - wb)));
+        if (wb >= hi) vm = 0;
+        else if (wb + 4 > hi) vm &= (1u << (8 * (uint32_t)(hi - wb))) - 1u;
+        const uint32_t w = ws[j];
+        const uint32_t b7 = w & vm, b6 = (w << 1) & vm, b5 = (w << 2) & vm, b4 = (w << 3) & vm;
+        const uint32_t cont = b7 & ~b6, lead = b7 & b6, ge3 = lead & b5, ge4 = ge3 & b4;
+        const uint32_t nz1e = ((w & 0x1E1E1E1Eu) + 0x7F7F7F7Fu) & H; // bits 4..1 (5..1 of the byte) any set
+        const uint32_t nz0f = ((w & 0x0F0F0F0Fu) + 0x7F7F7F7Fu) & H;
+        const uint32_t nz07 = ((w & 0x07070707u) + 0x7F7F7F7Fu) & H;
+        const uint32_t e0 = ge3 & ~ge4 & ~nz0f, f0 = ge4 & ~nz07;
+        const uint32_t exp = (lead << 8) | (pl >> 24) | (ge3 << 16) | (p3 >> 16) | (ge4 << 24) | (p4 >> 8);
+        const uint32_t e0n = (e0 << 8) | (pe0 >> 24), f0n = (f0 << 8) | (pf0 >> 24);
+        bad |= (exp ^ cont) | (lead & ~b5 & ~nz1e) | (e0n & ~b5) | (f0n & ~(b5 | b4));
+        units += __builtin_popcount((~b7 & vm) | lead) + __builtin_popcount(ge4);
+        pl = lead;
+        p3 = ge3;
+        p4 = ge4;
+        pe0 = e0;
+        pf0 = f0;
       }
     }
   }
+  bad |= (pl >> 24) | (p3 >> 16) | (p4 >> 8); // a sequence running past the end
   len = units;
-  return pend == 0;
+  return bad == 0;
 }
 // SplittableString::len(Utf16) (block.rs:1391-1401)
 __device__ __forceinline__ uint32_t str_len16(const uint8_t *s, uint32_t n) {
