@@ -429,10 +429,17 @@ def run_compact(a, eng, batch, tensors, dev, world):
         ct = time.perf_counter() - t
         cpu = {"value": s.n_bytes / ct / 1e9, "unit": "GB/s", "docs_per_s": k / ct, "cores": threads, "kind": "port",
                "sample": f"oracle/yrs_oracle_store.c compact_updates_v1 on the first {k} documents"}
+    # roofline of the dominant kernel: algorithmic bytes (input + output) over k_compact's
+    # HIP-event time (the count pass and scans are k_compact_count_ms beside it)
+    alg = batch.n_bytes + int(r.out_bytes)
+    kms = max(float(st_k["ms_exact"]), 1e-6)
     return {"value": batch.n_bytes / dt / 1e9, "unit": "GB/s", "docs_per_s": batch.n_docs / dt, "ms": dt * 1e3,
             "k_compact_ms": st_k["ms_exact"], "count_scan_ms": st_k["ms_decode"],
             "out_bytes": int(r.out_bytes), "docs_device": int((st == 0).sum()),
             "docs_unsupported": int((st == 21).sum()),
+            "roofline": {"bound": "hbm", "achieved": alg / (kms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None, "kernel": "k_compact",
+                         "alg_bytes_per_launch": alg},
             "kernel": "k_compact_count + k_compact (lane per document)", "cpu_baseline": cpu}
 
 

@@ -17,7 +17,7 @@ def engine():
     # would for shapes k_lean hands over (tests/test_gpu_lean.py covers k_lean's BIG mode)
     # (and the grid-wide long-document path off, so that C1 keeps exercising the tiled kernel;
     # tests/test_gpu_giant.py covers that path); the tiny-document route forced on (by default
-    # it serves only batches of >= 65,536 documents handed to the fast path)
+    # it serves only batches of >= 262,144 documents handed to the fast path)
     from test_gpu_parity import engine_with
     e = engine_with(YMERGE_LEAN=0, YMERGE_GIANT_MIN=0, YMERGE_TINY=4)
     yield e

@@ -42,7 +42,7 @@ def test_small_dataset_merge(engine, oracle, dataset):
 # Routing of the 5,320 corpus documents (round 5): k_lean takes the editor-shaped ones, the
 # workgroup fast path the rich-content ones, the tiled kernel the 18 above the fast path's LDS
 # capacities; none needs the exact engine (the tiny-document hand-over serves only batches of
-# >= 65,536 documents) or the grid paths.  Update with the routing when it changes on purpose.
+# >= 262,144 documents) or the grid paths.  Update with the routing when it changes on purpose.
 CORPUS_PATHS = {"docs_lean": 1385, "docs_fast": 3917, "docs_big": 18, "docs_exact": 0, "docs_tiny": 0,
                 "docs_giant": 0, "docs_error": 0}
 

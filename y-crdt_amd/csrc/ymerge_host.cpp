@@ -307,7 +307,7 @@ static bool ensure_keep(ymerge_ctx *c, DevBuf &b, size_t bytes, size_t keep) {
 }
 
 // fewest documents handed to k_fast_merge for its tiny-document hand-over to the exact engine
-constexpr uint64_t TINY_MIN_DOCS = 65536;
+constexpr uint64_t TINY_MIN_DOCS = 262144;
 
 // Documents per wavefront of the exact engine (ymerge_seq.hip): 64 (env YMERGE_SEQ_LPW sets it).
 // One per wavefront was measured slower on the corpus (exact stage 2.35 vs 1.80 ms, r05t): the
@@ -534,8 +534,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     hipEventRecord(c->ev[7], c->s);
     hipEventRecord(c->ev[0], c->s);
     ym::launch_decode(d_bytes, d_upd_off, n_updates, c->rec.as<uint32_t>(), c->ovf.as<uint32_t>(), c->huge.as<uint32_t>(),
-                      huge_words(n_bytes), c->s, lp_args(c, n_bytes, b.v1x), b.v1x, nullptr,
-                      (uint32_t *)(c->h_pinned + 24));
+                      huge_words(n_bytes), c->s, lp_args(c, n_bytes, b.v1x), b.v1x); // (no probe: one sync less)
     hipEventRecord(c->ev[5], c->s);
     decoded = true;
     const int rc = run_giant(c, b, fo, 0, (uint32_t)n_updates, 0, n_bytes);
