@@ -10,10 +10,10 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 case $WL in c1) S="--steps 2 --warmup 1" ;; *) S="--steps 5 --warmup 2" ;; esac
 timeout -k 10 420 python bench.py --workload $WL $S > $OUT/bench_$WL.log 2>&1 \
-&& timeout -k 10 420 rocprofv3 --kernel-trace --stats -d $OUT/kt_$WL -o kt --output-format csv -- python3 bench.py --workload $WL --no-cpu-baseline --no-e2e $S > $OUT/kt_$WL.log 2>&1 \
+&& timeout -k 10 420 rocprofv3 --kernel-trace --stats -d $OUT/kt_$WL -o kt --output-format csv -- python3 bench.py --workload $WL --no-cpu-baseline --no-e2e --no-compact --no-v2 $S > $OUT/kt_$WL.log 2>&1 \
 && if [ -n "$PMC" ]; then \
-  timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch_$WL -o pmc --output-format csv -- python3 bench.py --workload $WL --no-cpu-baseline --no-e2e --steps 2 --warmup 1 > $OUT/pmc_fetch_$WL.log 2>&1 \
-  && timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write_$WL -o pmc --output-format csv -- python3 bench.py --workload $WL --no-cpu-baseline --no-e2e --steps 2 --warmup 1 > $OUT/pmc_write_$WL.log 2>&1; fi
+  timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch_$WL -o pmc --output-format csv -- python3 bench.py --workload $WL --no-cpu-baseline --no-e2e --no-compact --no-v2 --steps 2 --warmup 1 > $OUT/pmc_fetch_$WL.log 2>&1 \
+  && timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write_$WL -o pmc --output-format csv -- python3 bench.py --workload $WL --no-cpu-baseline --no-e2e --no-compact --no-v2 --steps 2 --warmup 1 > $OUT/pmc_write_$WL.log 2>&1; fi
 rc=$?
 echo "exit $rc ($WL)"
 tail -1 $OUT/bench_$WL.log | cut -c1-300
