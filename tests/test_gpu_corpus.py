@@ -56,6 +56,24 @@ def test_small_dataset_paths(engine, oracle, dataset):
     assert sum(got[k] for k in ("docs_lean", "docs_fast", "docs_big", "docs_exact", "docs_giant")) == dataset.n_docs
 
 
+@pytest.mark.parametrize("env", [
+    {"YMERGE_EXACT_LOCKSTEP": "1"},                            # exact decode one update per wavefront
+    {"YMERGE_LP_MID": "100000", "YMERGE_EXACT_LOCKSTEP": "1"},  # rich updates on the exact walk only
+    {"YMERGE_LP_MID": "16"},                                   # nearly every rich update on the parallel parse
+    {"YMERGE_LONG_PARSE": "0"},                                # no parallel parse: the lockstep walker
+    {"YMERGE_TINY": "4"},                                      # tiny documents on the exact engine's lanes
+])
+def test_small_dataset_decode_routes(oracle, dataset, env):
+    """The corpus through every decode route the knobs select: the same bytes each time."""
+    from test_gpu_parity import engine_with
+    e = engine_with(**env)
+    try:
+        out, off, st = check_batch(e, oracle, dataset)
+        assert not st.any()
+    finally:
+        e.close()
+
+
 def test_small_dataset_exact_engine(oracle, dataset):
     import ymerge
     os.environ["YMERGE_FAST_THREADS"] = "0"

@@ -119,3 +119,15 @@ def test_bench_gpus_flag_starts_ranks(tmp_path):
     bad = subprocess.run([sys.executable, str(script), "2"], env=dict(env, WORLD_SIZE="1"), capture_output=True,
                          text=True, timeout=120)
     assert bad.returncode != 0 and "WORLD_SIZE=1" in bad.stderr
+
+
+def test_visible_gpus_without_hip(monkeypatch):
+    """dist.visible_gpus counts GPUs from the KFD topology and the visibility variables only (no
+    HIP call in the parent of the rank processes)."""
+    import dist
+    n = dist.visible_gpus()
+    assert n >= 0
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0")
+    assert dist.visible_gpus() == min(n, 1)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
+    assert dist.visible_gpus() == 0
