@@ -178,7 +178,9 @@ def _trace_merge(oracle, name, n, client=1):
 
 @pytest.fixture(scope="module")
 def engine():
-    e = engine_with(YMERGE_LS_MIN=2048)  # diff / SV grid path from 2 KB (default 64 KB)
+    # diff / SV grid path from 2 KB (default 64 KB); the single-update identity copy off, so the
+    # grid paths see the canonical single-update documents (test_identity_copy covers it)
+    e = engine_with(YMERGE_LS_MIN=2048, YMERGE_IDENTITY=0)
     yield e
     e.close()
 
@@ -222,6 +224,17 @@ def test_long_merge_single_update_docs(engine, oracle, longs):
     # rich, rich_big_client, zero_item, gc_last, ds_adjacent, ds_many, no_blocks, b4 (and the
     # DeleteSet shapes the grid path declines went on to the tiled kernel)
     assert st["docs_giant"] >= 7, (st["docs_giant"], st["docs_big"], st["docs_fast"], st["docs_exact"])
+
+
+def test_identity_copy(oracle, longs):
+    """With the identity copy on (the default), canonical single-update documents are copied by
+    k_fast_merge: the same bytes as yrs' merge of the one update."""
+    e = engine_with()
+    try:
+        docs = [[v] for v in longs.values()]
+        check_batch(e, oracle, batch_of(docs))
+    finally:
+        e.close()
 
 
 def test_long_merge_errors(engine, oracle, longs):

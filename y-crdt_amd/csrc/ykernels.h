@@ -140,6 +140,7 @@ void launch_decode(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_upd
 // LDS capacities of the one-workgroup-per-document fast path (per document)
 struct FastCaps {
   uint32_t in_cap, u_cap, b_cap, e_cap, r_cap;
+  uint32_t ident = 1; // single-update identity copy (env YMERGE_IDENTITY=0: off)
 };
 // per-document results; path 0 = written, 1 = needs the exact engine, 2 = needs the tiled
 // kernel for documents above the LDS capacities

@@ -148,6 +148,7 @@ static bool ctx_init(ymerge_ctx *c, int device) {
     c->planner = strcmp(v, "ring") == 0 ? 1u : strcmp(v, "wave") == 0 ? 2u : 0u;
   if (const char *v = getenv("YMERGE_LEAN_SCR_MAX")) c->lean_scr_max = strtoull(v, nullptr, 10);
   if (const char *v = getenv("YMERGE_LONG_PARSE")) c->long_parse = atoi(v) != 0;
+  if (const char *v = getenv("YMERGE_IDENTITY")) c->caps.ident = atoi(v) != 0;
   if (const char *v = getenv("YMERGE_SEQ_LPW")) c->seq_lpw = (uint32_t)std::min(64, std::max(0, atoi(v)));
   if (const char *v = getenv("YMERGE_LP_MID")) c->lp_mid = (uint32_t)std::max(1, atoi(v));
   if (const char *v = getenv("YMERGE_LONG_GRID")) c->long_grid = atoi(v) != 0;
