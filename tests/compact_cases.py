@@ -119,3 +119,177 @@ def edge_docs():
     # map entry (parent_sub): outside the shape
     docs.append([upd(1, 0, [bytes([0x24]) + t + vstr("k") + vstr("v")])]); reasons.append(CU["PARENT"])
     return batch_of(docs), reasons
+
+
+# ---------------------------------------------------------------- an independent shape check
+# A plain restatement of the lib0 v1 grammar (yrs/src/update.rs:433-488, 714-749) used to
+# confirm, from the bytes alone, the reason the device gives for refusing a document (the
+# status comparison against tools/hostemu is the same kernel source; this is not).
+
+def _rv(b, i):
+    r = s = 0
+    while True:
+        x = b[i]
+        i += 1
+        r |= (x & 0x7F) << s
+        s += 7
+        if x < 0x80:
+            return r, i
+
+
+def _str(b, i):
+    n, i = _rv(b, i)
+    return b[i:i + n], i + n
+
+
+def _any(b, i):
+    t = b[i]
+    i += 1
+    if t in (127, 126, 121, 120):
+        return i
+    if t == 125:
+        return _rv(b, i)[1]
+    if t == 124:
+        return i + 4
+    if t in (123, 122):
+        return i + 8
+    if t in (119, 116):
+        return _str(b, i)[1]
+    if t == 118:
+        n, i = _rv(b, i)
+        for _ in range(n):
+            i = _any(b, _str(b, i)[1])
+        return i
+    if t == 117:
+        n, i = _rv(b, i)
+        for _ in range(n):
+            i = _any(b, i)
+        return i
+    raise ValueError(t)
+
+
+def parse_v1(u):
+    """(blocks, ds): blocks as dicts (client, clock, len, ref, skip, origin, rorigin, id_parent,
+    psub); ds as [(client, [(start, len)])].  Raises on malformed input."""
+    b = bytes(u)
+    blocks, ds = [], []
+    ncl, i = _rv(b, 0)
+    for _ in range(ncl):
+        nb, i = _rv(b, i)
+        client, i = _rv(b, i)
+        clock, i = _rv(b, i)
+        for _ in range(nb):
+            info = b[i]
+            i += 1
+            blk = dict(client=client, clock=clock, ref=info & 15, skip=info == 10, gc=info == 0, origin=None,
+                       rorigin=None, id_parent=None, psub=False)
+            if info in (0, 10):
+                ln, i = _rv(b, i)
+            else:
+                if info & 0x80:
+                    oc, i = _rv(b, i)
+                    ok, i = _rv(b, i)
+                    blk["origin"] = (oc, ok)
+                if info & 0x40:
+                    rc, i = _rv(b, i)
+                    rk, i = _rv(b, i)
+                    blk["rorigin"] = (rc, rk)
+                if info & 0xC0 == 0:
+                    pi, i = _rv(b, i)
+                    if pi == 1:
+                        i = _str(b, i)[1]
+                    else:
+                        pc, i = _rv(b, i)
+                        pk, i = _rv(b, i)
+                        blk["id_parent"] = (pc, pk)
+                    if info & 0x20:
+                        blk["psub"] = True
+                        i = _str(b, i)[1]
+                ref = info & 15
+                if ref == 1:
+                    ln, i = _rv(b, i)
+                elif ref == 4:
+                    s, i = _str(b, i)
+                    ln = len(s.decode("utf-8", "surrogatepass").encode("utf-16-le")) // 2
+                elif ref == 2:
+                    n, i = _rv(b, i)
+                    for _ in range(n + 1):
+                        i = _str(b, i)[1]
+                    ln = n + 1
+                elif ref in (3, 5):
+                    i = _str(b, i)[1]
+                    ln = 1
+                elif ref == 6:
+                    i = _str(b, _str(b, i)[1])[1]
+                    ln = 1
+                elif ref == 7:
+                    tr = b[i]
+                    i += 1
+                    if tr == 3:
+                        i = _str(b, i)[1]
+                    ln = 1
+                elif ref == 8:
+                    n, i = _rv(b, i)
+                    for _ in range(n):
+                        i = _any(b, i)
+                    ln = n
+                elif ref == 9:
+                    i = _any(b, _str(b, i)[1])
+                    ln = 1
+                else:
+                    raise ValueError(ref)
+            blk["len"] = ln
+            blocks.append(blk)
+            clock += ln
+    ne, i = _rv(b, i)
+    for _ in range(ne):
+        c, i = _rv(b, i)
+        nr, i = _rv(b, i)
+        rs = []
+        for _ in range(nr):
+            s, i = _rv(b, i)
+            ln, i = _rv(b, i)
+            rs.append((s, ln))
+        ds.append((c, rs))
+    return blocks, ds
+
+
+def exhibits(updates, reason):
+    """True when the document's bytes show the shape `reason` (a CU code) names, False when they
+    do not, None for the capacity reasons (scratch sizes) a byte-level check cannot restate."""
+    try:
+        parsed = [parse_v1(u) for u in updates]
+    except (ValueError, IndexError):
+        return None
+    if reason == CU["CLIENTS"]:
+        cls = {b["client"] for bl, _ in parsed for b in bl}
+        cls_ds = cls | {c for _, ds in parsed for c, _ in ds}
+        return len(cls) > 8 or len(cls_ds) > 8
+    if reason == CU["PARENT"]:
+        return any(b["id_parent"] is not None or b["psub"] for bl, _ in parsed for b in bl)
+    if reason == CU["UPDATE_SHAPE"]:
+        return any(not b["gc"] and not b["skip"] and b["ref"] not in (1, 4) for bl, _ in parsed for b in bl) or \
+            any(len(ds) > 16 for _, ds in parsed)
+    if reason in (CU["GAP"], CU["PENDING"], CU["PENDING_DS"]):
+        nxt, gap, pend, pds = {}, False, False, False
+        for bl, ds in parsed:
+            for b in bl:
+                if b["skip"]:
+                    gap = True
+                    continue
+                c = b["client"]
+                if b["clock"] > nxt.get(c, 0):
+                    gap = True
+                    continue
+                for dep in (b["origin"], b["rorigin"], b["id_parent"]):
+                    if dep is not None and dep[1] >= nxt.get(dep[0], 0) and dep[0] != c:
+                        pend = True
+                    if dep is not None and dep[0] == c and dep[1] >= b["clock"] and b["clock"] >= nxt.get(c, 0):
+                        pend = True
+                nxt[c] = max(nxt.get(c, 0), b["clock"] + b["len"])
+            for c, rs in ds:
+                for s, ln in rs:
+                    if c in nxt and s + ln > nxt[c]:
+                        pds = True
+        return gap or pend or pds  # (delivery out of order shows as any of the three)
+    return None

@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 import workloads
-from compact_cases import CU, edge_docs, fixture_reason, fixtures, regrouped
+from compact_cases import exhibits, CU, edge_docs, fixture_reason, fixtures, regrouped
 from conftest import ROOT
 
 EMU_DIR = os.path.join(ROOT, "tools", "hostemu")
@@ -52,6 +52,8 @@ def check(emu, oracle, b, reasons=None, min_device=1.0):
             assert r is None or r == why[d], f"doc {d}: refused ({why[d]}), expected reason {r}"
             assert reasons is not None or why[d] in (CU["GAP"], CU["PENDING"], CU["PENDING_DS"], CU["CLIENTS"]), \
                 f"doc {d}: unexpected refusal {why[d]}"
+            # the bytes show the refused shape (compact_cases.exhibits: an independent parse)
+            assert exhibits(b.doc_updates(d), int(why[d])) is not False, f"doc {d}: reason {why[d]} not in its bytes"
             continue
         assert r in (0, None), f"doc {d}: written, expected refusal {r}"
         assert st[d] == est[d], f"doc {d}: status {st[d]} oracle {est[d]}"

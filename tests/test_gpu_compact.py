@@ -1,12 +1,14 @@
 """GPU parity of store-based compaction (ycompact_updates_v1_batch[_device]: k_compact_count +
 k_compact on gfx950) against the oracle (oracle/yrs_oracle_store.c) and against the same
 kernel source built for the CPU (tools/hostemu): statuses equal the CPU build's for every
-document, bytes equal the oracle's for every document the device writes."""
+document, bytes equal the oracle's for every document the device writes, and every document the
+device refuses (UNSUPPORTED, 21) shows the refused shape in its own bytes by an independent
+parse (compact_cases.exhibits: client count, parent form, content kinds, out-of-order delivery)."""
 import numpy as np
 import pytest
 
 import workloads
-from compact_cases import edge_docs, fixtures, regrouped
+from compact_cases import edge_docs, exhibits, fixtures, regrouped
 from test_compact_emu import emu  # noqa: F401 (fixture)
 from test_gpu_parity import engine  # noqa: F401 (fixture)
 
@@ -27,6 +29,9 @@ def check_gpu(engine, emu, oracle, b, min_device=1.0, host_entry=False):
         g = out[int(off[d]):int(off[d + 1])].tobytes()
         if st[d] == 21 and ost[d] != 21:
             assert not g
+            # not a comparison with the same kernel source: the document's bytes, parsed
+            # independently, show the shape the device names for refusing it
+            assert exhibits(b.doc_updates(d), int(ewhy[d])) is not False, f"doc {d}: reason {ewhy[d]} not in its bytes"
             continue
         assert st[d] == ost[d], f"doc {d}: status {st[d]} oracle {ost[d]}"
         e = arena[int(aoff[d]):int(aoff[d + 1])]
