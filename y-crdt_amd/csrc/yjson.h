@@ -676,12 +676,9 @@ __device__ __forceinline__ bool json_plain(const uint8_t *s, uint32_t n) {
   return st == PA && depth == 0;
 }
 
-// serde_json::from_str::<Any>(s[0..n]) then Any::to_json into w; 0 or E_JSON.
-template <class W> __device__ __noinline__ int json_canon(const uint8_t *s, uint32_t n, W &w) {
-  if (json_plain(s, n)) {
-    w.bytes(s, n);
-    return 0;
-  }
+// serde_json::from_str::<Any>(s[0..n]) then Any::to_json into w, by the general walk (every
+// text; json_canon takes the json_plain shortcut first); 0 or E_JSON.
+template <class W> __device__ __noinline__ int json_canon_walk(const uint8_t *s, uint32_t n, W &w) {
   JOut<W> o{w, false};
   uint32_t isobj[4] = {0, 0, 0, 0}, first[4] = {0, 0, 0, 0};
   int depth = 0;      // open containers (serde_json allows 127)
@@ -784,4 +781,15 @@ template <class W> __device__ __noinline__ int json_canon(const uint8_t *s, uint
     }
     want_value = true;
   }
+}
+
+// serde_json::from_str::<Any>(s[0..n]) then Any::to_json into w; 0 or E_JSON.  A text that is
+// its own canonical form (json_plain) is copied; tests/test_codec_emu.py checks that every text
+// json_plain accepts comes out of the general walk byte for byte.
+template <class W> __device__ __noinline__ int json_canon(const uint8_t *s, uint32_t n, W &w) {
+  if (json_plain(s, n)) {
+    w.bytes(s, n);
+    return 0;
+  }
+  return json_canon_walk(s, n, w);
 }

@@ -224,6 +224,8 @@ void launch_seq_merge(bool write, const BatchIn &b, const uint8_t *path, const u
 size_t scan_tmp_elems(uint32_t n);
 void launch_pack(const uint8_t *src, const uint64_t *start, const uint64_t *len, const uint64_t *pack_off,
                  uint8_t *dst, uint32_t n_docs, hipStream_t s);
+// a[i] -= sub for i < n (offset tables of a pipelined host group, rebased to the group's slice)
+void launch_rebase_u64(uint64_t *a, uint64_t n, uint64_t sub, hipStream_t s);
 } // namespace ym
 
 namespace ym {

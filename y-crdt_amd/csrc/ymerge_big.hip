@@ -706,6 +706,210 @@ __device__ __noinline__ bool big_run_order(const BatchIn &b, uint64_t u0, uint32
   return true;
 }
 
+// ------------------------------------------------------------------ DeleteSet union by bitmap
+// IdSet::merge then squash (yrs/src/id_set.rs:129-164, 385-395) leaves, per client, the
+// maximal unions of overlapping or adjacent ranges: exactly the maximal runs of set bits once
+// every range is set in a bitmap over the client's clock window (k_lean's DeleteSet,
+// ymerge_lean.hip phase 4).  For the few-client documents whose windows fit LDS (C4: 1-4
+// clients, windows of a few thousand clocks) this replaces the key pass, the range sort over
+// HBM tables and the two union passes: one pass sets the windows, one sets the bits, one
+// finds the runs, one sizes them and one writes them.
+// d_client: the D (<= 64) distinct live clients ascending; d_ord: ranks in yrs' table order.
+// pc: >= 9 * 64 LDS words; bm: BIG_BM_WORDS LDS words; cl: BIG_BM_COMP component pairs in
+// LDS; chead / cend: the same in HBM when there are more components.
+// Returns 0: not this shape (the sort path runs); DSB_ROOM: the DeleteSet does not fit the
+// slot's `room` bytes (exact engine); else 1 + the DeleteSet's bytes, written at dso.
+constexpr uint32_t BIG_BM_WORDS = 6144, BIG_BM_COMP = 2048, DSB_ROOM = 0xFFFFFFFFu;
+template <int NT>
+__device__ __noinline__ uint32_t big_ds_bitmap(const uint32_t *ri, const uint32_t *rs, const uint32_t *re,
+                                               const uint32_t *et, const uint32_t *ec, uint32_t NR, uint32_t D,
+                                               const uint32_t *d_client, const uint32_t *d_ord, uint32_t *pc,
+                                               uint32_t *bm, uint32_t *cl, uint32_t *chead, uint32_t *cend,
+                                               uint32_t *ws, uint8_t *dso, uint64_t room) {
+  const uint32_t t = threadIdx.x;
+  uint32_t *lo = pc, *hi = pc + 64, *woff = pc + 128, *nw = pc + 192, *ncomp = pc + 256, *cbase = pc + 320,
+           *bytes = pc + 384, *bpre = pc + 448, *eoff = pc + 512, *misc = pc + 576;
+  auto rank_of = [&](uint32_t c) -> uint32_t {
+    uint32_t a = 0, z = D;
+    while (a < z) {
+      const uint32_t mid = (a + z) >> 1;
+      if (d_client[mid] < c) a = mid + 1;
+      else z = mid;
+    }
+    return a;
+  };
+  if (t < 64) {
+    lo[t] = 0xFFFFFFFFu;
+    hi[t] = 0;
+    ncomp[t] = 0;
+    bytes[t] = 0;
+  }
+  __syncthreads();
+  // 1 windows: [min start, max end) of every client's live ranges; an empty range -> sort path
+  uint32_t bad = 0;
+  for (uint32_t j = t; j < NR; j += NT) {
+    const uint32_t x = ri[j];
+    if (!(et[x] & 0x80000000u)) continue;
+    const uint32_t s = rs[j], e = re[j];
+    if (e <= s) {
+      bad = 1;
+      continue;
+    }
+    const uint32_t r = rank_of(ec[x]);
+    atomicMin(&lo[r], s);
+    atomicMax(&hi[r], e);
+  }
+  if (__syncthreads_or(bad)) return 0;
+  if (t == 0) { // word offsets, a zero word after every window (runs never cross clients)
+    uint32_t acc = 0;
+    for (uint32_t r = 0; r < D; r++) {
+      const uint32_t n = lo[r] < hi[r] ? ((hi[r] - 1) >> 5) - (lo[r] >> 5) + 1 : 0;
+      lo[r] &= ~31u;
+      woff[r] = acc;
+      nw[r] = n;
+      acc += n + 1;
+    }
+    misc[0] = acc;
+  }
+  __syncthreads();
+  const uint32_t W = misc[0];
+  if (W > BIG_BM_WORDS) return 0;
+  for (uint32_t q = t; q < W; q += NT) bm[q] = 0;
+  __syncthreads();
+  // 2 every live range into its client's window
+  for (uint32_t j = t; j < NR; j += NT) {
+    const uint32_t x = ri[j];
+    if (!(et[x] & 0x80000000u)) continue;
+    const uint32_t r = rank_of(ec[x]), wo = woff[r];
+    uint32_t a = rs[j] - lo[r];
+    const uint32_t z = re[j] - lo[r];
+    while (a < z) {
+      const uint32_t wi = a >> 5, bo = a & 31, nb = (z - a < 32 - bo) ? z - a : 32 - bo;
+      atomicOr(&bm[wo + wi], (nb == 32 ? 0xFFFFFFFFu : ((1u << nb) - 1)) << bo);
+      a += nb;
+    }
+  }
+  __syncthreads();
+  // word -> client rank (the window holding word q; gap words have no bits)
+  auto word_rank = [&](uint32_t q) -> uint32_t {
+    uint32_t a = 0, z = D;
+    while (a + 1 < z) {
+      const uint32_t mid = (a + z) >> 1;
+      if (woff[mid] <= q) a = mid;
+      else z = mid;
+    }
+    return a;
+  };
+  // 3 runs: count per client, then starts / ends at their global component index
+  for (uint32_t q = t; q < W; q += NT) {
+    const uint32_t bits = bm[q], prev = q ? bm[q - 1] >> 31 : 0;
+    const uint32_t stb = bits & ~((bits << 1) | prev);
+    if (stb) atomicAdd(&ncomp[word_rank(q)], (uint32_t)__builtin_popcount(stb));
+  }
+  __syncthreads();
+  if (t == 0) {
+    uint32_t acc = 0;
+    for (uint32_t r = 0; r < D; r++) {
+      cbase[r] = acc;
+      acc += ncomp[r];
+    }
+    misc[1] = acc;
+  }
+  __syncthreads();
+  const uint32_t NCOMP = misc[1];
+  uint32_t *cs = NCOMP <= BIG_BM_COMP ? cl : chead, *ce = NCOMP <= BIG_BM_COMP ? cl + BIG_BM_COMP : cend;
+  {
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < W; base += NT) {
+      const uint32_t q = base + t;
+      const bool v = q < W;
+      const uint32_t bits = v ? bm[q] : 0, prev = v && q ? bm[q - 1] >> 31 : 0;
+      const uint32_t nxt = v && q + 1 < W ? bm[q + 1] & 1 : 0;
+      const uint32_t stb = bits & ~((bits << 1) | prev), enb = bits & ~((bits >> 1) | (nxt << 31));
+      uint32_t T;
+      const uint32_t cb = carry + bscan_sum<NT>((uint32_t)__builtin_popcount(stb), ws, T);
+      carry += T;
+      if (bits) {
+        const uint32_t r = word_rank(q), clk0 = lo[r] + 32 * (q - woff[r]);
+        uint32_t x = stb;
+        while (x) {
+          const uint32_t bp = (uint32_t)__builtin_ctz(x);
+          cs[cb + (uint32_t)__builtin_popcount(stb & ((1u << bp) - 1))] = clk0 + bp;
+          x &= x - 1;
+        }
+        x = enb;
+        while (x) {
+          const uint32_t bp = (uint32_t)__builtin_ctz(x);
+          const uint32_t upto = bp == 31 ? stb : (stb & ((2u << bp) - 1));
+          ce[cb + (uint32_t)__builtin_popcount(upto) - 1] = clk0 + bp + 1;
+          x &= x - 1;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  auto comp_rank = [&](uint32_t k) -> uint32_t { // the client of component k (last r with cbase <= k, ncomp > 0)
+    uint32_t a = 0, z = D;
+    while (a + 1 < z) {
+      const uint32_t mid = (a + z) >> 1;
+      if (cbase[mid] <= k) a = mid;
+      else z = mid;
+    }
+    while (a + 1 < D && cbase[a + 1] <= k) a++; // (ties: clients without components)
+    return a;
+  };
+  // 4 bytes per client, entry offsets in yrs' table order (IdSet encode, id_set.rs:398-410)
+  for (uint32_t k = t; k < NCOMP; k += NT) {
+    const uint32_t a = cs[k];
+    atomicAdd(&bytes[comp_rank(k)], (uint32_t)(varlen(a) + varlen(ce[k] - a)));
+  }
+  __syncthreads();
+  if (t == 0) {
+    uint32_t acc = 0;
+    for (uint32_t r = 0; r < D; r++) {
+      bpre[r] = acc;
+      acc += bytes[r];
+    }
+    uint32_t pos = varlen(D);
+    for (uint32_t i = 0; i < D; i++) {
+      const uint32_t r = d_ord[i];
+      eoff[r] = pos;
+      pos += varlen(d_client[r]) + varlen(ncomp[r]) + bytes[r];
+    }
+    misc[2] = pos;
+  }
+  __syncthreads();
+  const uint32_t dsz = misc[2];
+  if (dsz > room) return DSB_ROOM;
+  // 5 write: D, per client (client, ranges), the components at their offsets
+  if (t == 0) {
+    Writer w{dso, 0};
+    w_var(w, D);
+  }
+  if (t < D) {
+    Writer w{dso, eoff[t]};
+    w_var(w, d_client[t]);
+    w_var(w, ncomp[t]);
+  }
+  uint32_t carry = 0;
+  for (uint32_t base = 0; base < NCOMP; base += NT) {
+    const uint32_t k = base + t;
+    const bool v = k < NCOMP;
+    const uint32_t a = v ? cs[k] : 0, ln = v ? ce[k] - a : 0;
+    const uint32_t sz = v ? varlen(a) + varlen(ln) : 0;
+    uint32_t T;
+    const uint32_t P = carry + bscan_sum<NT>(sz, ws, T);
+    carry += T;
+    if (v) {
+      const uint32_t r = comp_rank(k);
+      Writer w{dso, eoff[r] + varlen(d_client[r]) + varlen(ncomp[r]) + (P - bpre[r])};
+      w_var(w, a);
+      w_var(w, ln);
+    }
+  }
+  return 1 + dsz;
+}
+
 // ------------------------------------------------------------------ k_big_merge
 template <int NT> struct BigShared {
   uint32_t ws[2 * (NT / 64) + 8];
@@ -718,7 +922,8 @@ template <int NT> struct BigShared {
 constexpr uint32_t BIG_COPY_MIN = 1024, BIG_COPY_N = 32;
 template <int NT, int OCC>
 __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t *counts, const uint64_t *scr_off,
-                                                       uint32_t *scratch, FastOut o) {
+                                                       uint32_t *scratch, FastOut o, uint32_t flags) {
+  const bool big_ds_bm = !(flags & 1); // DeleteSet union by bitmap when it fits (env YMERGE_BIG_DSBM=0: off)
   ym_set_grammar(b.v1x);
   const uint32_t d = o.big_list[blockIdx.x];
   if (d >= b.n_docs || o.path[d] != 2) return;
@@ -1467,6 +1672,20 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
   }
   __syncthreads();
   mark(10);
+  if (D >= 1 && D <= 64 && big_ds_bm) {
+    const uint32_t rb = big_ds_bitmap<NT>(m.ri, m.rs, m.re, m.et, m.ec, NR, D, d_client, d_ord, d_first,
+                                          (uint32_t *)lscr, (uint32_t *)dtab, m.chead, m.cend, ws, out + blocks_size,
+                                          cap - blocks_size);
+    if (rb == DSB_ROOM) {
+      finish(1, 0, 0);
+      return;
+    }
+    if (rb) {
+      stamp(5);
+      finish(0, 0, blocks_size + (rb - 1));
+      return;
+    }
+  }
   // live ranges sorted by (client, start, index).  One pass builds the keys, counts the
   // live ones and checks the order; four ranges per lane per trip with every load of the
   // trip issued before the first use (the loop was a chain of dependent HBM round trips)
@@ -1713,10 +1932,11 @@ void launch_big_merge(const BatchIn &b, const uint32_t *counts, const uint64_t *
   // documents in flight of one 1024-lane workgroup per CU (C4: tiled 9.05 -> 6.81 ms);
   // env YMERGE_BIG_NT=1024 selects the single-workgroup build (A/B)
   static const int nt = getenv("YMERGE_BIG_NT") ? atoi(getenv("YMERGE_BIG_NT")) : 512;
+  static const uint32_t flags = (getenv("YMERGE_BIG_DSBM") && atoi(getenv("YMERGE_BIG_DSBM")) == 0) ? 1u : 0u;
   if (nt == 1024)
-    hipLaunchKernelGGL((k_big_merge<1024, 4>), dim3(n_list), dim3(1024), 0, s, b, counts, scr_off, scratch, o);
+    hipLaunchKernelGGL((k_big_merge<1024, 4>), dim3(n_list), dim3(1024), 0, s, b, counts, scr_off, scratch, o, flags);
   else
-    hipLaunchKernelGGL((k_big_merge<512, 4>), dim3(n_list), dim3(512), 0, s, b, counts, scr_off, scratch, o);
+    hipLaunchKernelGGL((k_big_merge<512, 4>), dim3(n_list), dim3(512), 0, s, b, counts, scr_off, scratch, o, flags);
 }
 
 } // namespace ym

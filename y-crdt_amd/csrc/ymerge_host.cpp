@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <atomic>
+#include <chrono>
 #include <map>
 #include <mutex>
 #include <thread>
@@ -1354,45 +1355,55 @@ static int host_merge_pipelined(ymerge_ctx *c, const uint8_t *bytes, const uint6
     return DEV_FAIL();
   // rebased tables of every group: its documents index its slice of the update offsets, and
   // those count from the group's first byte rounded down to 16 (the kernels' aligned loads), so
-  // each merge_device call sizes its slots and scratch by the group, not the whole batch
-  std::vector<uint64_t> gdu(n_docs + G + 1), guo(n_updates + G + 1);
+  // each merge_device call sizes its slots and scratch by the group, not the whole batch.  The
+  // producer stages each group's slices of the caller's tables with its bytes and rebases them
+  // on the device (k_rebase_u64): rebasing on the host and uploading the tables up front
+  // (8 B per update, C2: 80 MB) serialised ~25 ms before the first H2D (round 4-5: C-ABI
+  // entry 31 -> 8 GB/s on C2).
   std::vector<uint64_t> gdu_off(G + 1, 0), guo_off(G + 1, 0), gbase(G);
   for (size_t k = 0; k < G; k++) {
     gdu_off[k + 1] = gdu_off[k] + (gd[k + 1] - gd[k]) + 1;
-    for (uint64_t d = gd[k]; d <= gd[k + 1]; d++) gdu[gdu_off[k] + d - gd[k]] = doc_upd[d] - doc_upd[gd[k]];
     const uint64_t u0 = doc_upd[gd[k]], u1 = doc_upd[gd[k + 1]];
     gbase[k] = upd_off[u0] & ~15ull;
     guo_off[k + 1] = guo_off[k] + (u1 - u0) + 1;
-    for (uint64_t u = u0; u <= u1; u++) guo[guo_off[k] + u - u0] = upd_off[u] - gbase[k];
   }
-  if (hipMemcpyAsync(c->in_upd_off.p, guo.data(), guo_off[G] * 8, hipMemcpyHostToDevice, c->s_in) != hipSuccess ||
-      hipMemcpyAsync(c->grp_doc_upd.p, gdu.data(), gdu_off[G] * 8, hipMemcpyHostToDevice, c->s_in) != hipSuccess ||
-      hipStreamSynchronize(c->s_in) != hipSuccess)
-    return DEV_FAIL();
-  // producer: stage every group's bytes through the pinned ring on s_in, one event per group
+  static const bool trace = getenv("YMERGE_HOST_TRACE") != nullptr;
+  const auto t0 = std::chrono::steady_clock::now();
+  auto ms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
+  // producer: stage every group's tables and bytes through the pinned ring on s_in, one event per group
   std::atomic<int> prod_rc{0};
   std::atomic<size_t> recorded{0}; // groups whose ev_in the producer has recorded
   std::thread producer([&] {
     hipSetDevice(c->device);
     size_t i = 0;
-    for (size_t k = 0; k < G && !prod_rc; k++) {
-      const uint64_t a = upd_off[doc_upd[gd[k]]], z = upd_off[doc_upd[gd[k + 1]]];
-      for (uint64_t off = a; off < z; off += STAGE_CHUNK, i++) {
+    auto stage = [&](uint8_t *dst, const uint8_t *src, uint64_t n) {
+      for (uint64_t off = 0; off < n; off += STAGE_CHUNK, i++) {
         const int b = (int)(i & 1);
-        const size_t len = std::min<uint64_t>(STAGE_CHUNK, z - off);
-        if (i >= 2 && hipEventSynchronize(c->stage_ev[b]) != hipSuccess) {
-          prod_rc = DEV_FAIL();
-          break;
-        }
-        par_memcpy(c->stage[b], bytes + off, len);
-        if (hipMemcpyAsync(c->in_bytes.as<uint8_t>() + off, c->stage[b], len, hipMemcpyHostToDevice, c->s_in) !=
-                hipSuccess ||
-            hipEventRecord(c->stage_ev[b], c->s_in) != hipSuccess) {
-          prod_rc = DEV_FAIL();
-          break;
-        }
+        const size_t len = std::min<uint64_t>(STAGE_CHUNK, n - off);
+        if (i >= 2 && hipEventSynchronize(c->stage_ev[b]) != hipSuccess) return false;
+        par_memcpy(c->stage[b], src + off, len);
+        if (hipMemcpyAsync(dst + off, c->stage[b], len, hipMemcpyHostToDevice, c->s_in) != hipSuccess ||
+            hipEventRecord(c->stage_ev[b], c->s_in) != hipSuccess)
+          return false;
       }
-      if (!prod_rc && hipEventRecord(c->ev_in[k], c->s_in) != hipSuccess) prod_rc = DEV_FAIL();
+      return true;
+    };
+    for (size_t k = 0; k < G && !prod_rc; k++) {
+      const uint64_t d0 = gd[k], nd = gd[k + 1] - gd[k], u0 = doc_upd[d0], nu = doc_upd[gd[k + 1]] - u0;
+      uint64_t *guo = c->in_upd_off.as<uint64_t>() + guo_off[k], *gdu = c->grp_doc_upd.as<uint64_t>() + gdu_off[k];
+      const uint64_t a = upd_off[u0], z = upd_off[u0 + nu];
+      if (!stage((uint8_t *)guo, (const uint8_t *)(upd_off + u0), (nu + 1) * 8) ||
+          !stage((uint8_t *)gdu, (const uint8_t *)(doc_upd + d0), (nd + 1) * 8)) {
+        prod_rc = DEV_FAIL();
+        break;
+      }
+      ym::launch_rebase_u64(guo, nu + 1, gbase[k], c->s_in);
+      ym::launch_rebase_u64(gdu, nd + 1, u0, c->s_in);
+      if (!stage(c->in_bytes.as<uint8_t>() + a, bytes + a, z - a) || hipEventRecord(c->ev_in[k], c->s_in) != hipSuccess) {
+        prod_rc = DEV_FAIL();
+        break;
+      }
+      if (trace) fprintf(stderr, "ymerge host: group %zu staged at %.2f ms\n", k, ms());
       recorded.store(k + 1);
     }
   });
@@ -1454,6 +1465,7 @@ static int host_merge_pipelined(ymerge_ctx *c, const uint8_t *bytes, const uint6
       break;
     }
     obase += dr.out_bytes;
+    if (trace) fprintf(stderr, "ymerge host: group %zu merged + packed at %.2f ms\n", k, ms());
   }
   producer.join();
   if (!rc && prod_rc) rc = prod_rc;
@@ -1463,6 +1475,7 @@ static int host_merge_pipelined(ymerge_ctx *c, const uint8_t *bytes, const uint6
     return rc;
   }
   r->out_bytes = obase;
+  if (trace) fprintf(stderr, "ymerge host: %zu groups done at %.2f ms\n", G, ms());
   *out = r;
   return 0;
 }

@@ -124,4 +124,13 @@ void launch_pack(const uint8_t *src, const uint64_t *start, const uint64_t *len,
   const uint32_t ys = n_docs <= 64 ? 256 : n_docs <= 1024 ? 16 : 1;
   hipLaunchKernelGGL(k_pack, dim3(g, ys), dim3(256), 0, s, src, start, len, pack_off, dst, n_docs);
 }
+
+__global__ void __launch_bounds__(256) k_rebase_u64(uint64_t *a, uint64_t n, uint64_t sub) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) a[i] -= sub;
+}
+void launch_rebase_u64(uint64_t *a, uint64_t n, uint64_t sub, hipStream_t s) {
+  if (!n || !sub) return;
+  const uint64_t g = (n + 255) / 256;
+  hipLaunchKernelGGL(k_rebase_u64, dim3(g < 4096 ? (uint32_t)g : 4096u), dim3(256), 0, s, a, n, sub);
+}
 } // namespace ym
