@@ -65,7 +65,8 @@ FIXTURE_REASONS = {
     "_rev": CU["GAP"], "_shuf": CU["GAP"],  # out-of-order delivery: pending structs
     "utf16_text": CU["SURROGATE"], "utf16_log_then_snapshot": CU["SURROGATE"],
     "map_array_any": CU["UPDATE_SHAPE"], "map_array_xml_nested": CU["UPDATE_SHAPE"], "numbers": CU["UPDATE_SHAPE"],
-    "rich_text": CU["UPDATE_SHAPE"], "subdoc": None,  # subdoc: the oracle reports UNSUPPORTED too
+    "subdoc": None,  # subdoc: the oracle reports UNSUPPORTED too
+    # rich_text (Format / Embed items) is on the device since round 6
 }
 
 
@@ -268,7 +269,7 @@ def exhibits(updates, reason):
     if reason == CU["PARENT"]:
         return any(b["id_parent"] is not None or b["psub"] for bl, _ in parsed for b in bl)
     if reason == CU["UPDATE_SHAPE"]:
-        return any(not b["gc"] and not b["skip"] and b["ref"] not in (1, 4) for bl, _ in parsed for b in bl) or \
+        return any(not b["gc"] and not b["skip"] and b["ref"] not in (1, 3, 4, 5, 6) for bl, _ in parsed for b in bl) or \
             any(len(ds) > 16 for _, ds in parsed)
     if reason in (CU["GAP"], CU["PENDING"], CU["PENDING_DS"]):
         nxt, gap, pend, pds = {}, False, False, False

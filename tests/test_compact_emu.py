@@ -63,6 +63,16 @@ def check(emu, oracle, b, reasons=None, min_device=1.0):
     return st, why
 
 
+def test_reference_corpus(emu, oracle):
+    """The reference corpus (assets/bench-input/small-test-dataset.bin, 5,320 real Yjs documents):
+    every document the device writes equals the oracle byte for byte; every refusal shows its
+    shape in the document's bytes; the device share is pinned (round 6: Binary / Embed / Format
+    content on the device, 4,225 of 5,320)."""
+    b = workloads.dataset_docs()
+    st, why = check(emu, oracle, b, reasons=[None] * b.n_docs, min_device=0.79)
+    assert (st == 21).sum() <= 1095
+
+
 def test_text_docs(emu, oracle):
     for seed, mc, df in ((1, 4, 0.2), (2, 8, 0.4), (3, 2, 0.05)):
         check(emu, oracle, workloads.text_docs(80, 300, seed=seed, max_clients=mc, del_frac=df))

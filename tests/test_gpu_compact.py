@@ -79,3 +79,11 @@ def test_mixed_shapes_and_pending(engine, emu, oracle):
 
 def test_host_entry(engine, emu, oracle):
     check_gpu(engine, emu, oracle, workloads.text_docs(200, 200, seed=9), host_entry=True)
+
+
+def test_reference_corpus(engine, emu, oracle):
+    """All 5,320 documents of the reference corpus through k_compact: statuses equal the CPU
+    build's, written bytes equal the oracle's, refusals show their shape; device share pinned."""
+    b = workloads.dataset_docs()
+    st = check_gpu(engine, emu, oracle, b, min_device=0.79)
+    assert (st == 21).sum() <= 1095

@@ -332,3 +332,61 @@ def test_long_paths_off(oracle, longs, env):
         check_sv(e, oracle, vals)
     finally:
         e.close()
+
+
+def _upd(sections, ds):
+    """A v1 update: sections [(client, clock, [block bytes])], ds [(client, [(start, len)])]."""
+    b = _var(len(sections))
+    for client, clock, blocks in sections:
+        b += _var(len(blocks)) + _var(client) + _var(clock) + b"".join(blocks)
+    b += _var(len(ds))
+    for client, ranges in ds:
+        b += _var(client) + _var(len(ranges)) + b"".join(_var(s) + _var(n) for s, n in ranges)
+    return b
+
+
+def identity_reject_docs():
+    """Single-update documents whose canonical-size check could pass although the merge writes
+    other bytes: each must be merged, not copied.  The first ones are canonical
+    (copied); the rest are shapes the identity copy must refuse."""
+    t = item(text("abc"))
+    o = item(text("xy"), origin=(7, 2))
+    gc = bytes([0]) + _var(4)
+    docs = {
+        "canonical_one_block": [_upd([(7, 0, [t])], [])],
+        "canonical_two_sections": [_upd([(9, 0, [t, o]), (7, 0, [t])], [(7, [(0, 2)])])],
+        "canonical_ds_two_ranges": [_upd([], [(7, [(0, 2), (5, 1)])])],
+        "ds_unsorted": [_upd([], [(7, [(5, 1), (0, 2)])])],
+        "ds_adjacent": [_upd([], [(7, [(0, 2), (2, 3)])])],
+        "ds_overlapping": [_upd([], [(7, [(0, 4), (2, 3)])])],
+        "ds_unsorted_with_block": [_upd([(7, 0, [t])], [(7, [(2, 1), (0, 1)])])],
+        "ds_adjacent_many": [_upd([(7, 0, [t, o])], [(7, [(0, 1), (1, 1), (3, 1), (4, 1)])])],
+        "ds_two_entries": [_upd([], [(7, [(0, 2)]), (9, [(1, 1)])])],
+        "ds_empty_entry": [_upd([(7, 0, [t])], [(7, [])])],
+        "ds_zero_range": [_upd([(7, 0, [t])], [(7, [(1, 0)])])],
+        "sections_ascending": [_upd([(7, 0, [t]), (9, 0, [t])], [])],
+        "section_repeated_gap": [_upd([(7, 0, [t]), (7, 10, [t])], [])],
+        "section_repeated_overlap": [_upd([(7, 0, [t, o]), (7, 2, [t])], [])],
+        "section_repeated_contiguous": [_upd([(7, 0, [t]), (7, 3, [o])], [])],
+        "skip_in_section": [_upd([(7, 0, [t, bytes([10]) + _var(3), o])], [])],
+        "gc_blocks": [_upd([(7, 0, [gc, gc, t])], [])],
+        "zero_length_item": [_upd([(7, 0, [t, item(text("")), o])], [])],
+        "noncanonical_clock": [bytes([1, 1, 7, 0x80, 0x00]) + t + bytes([0])],  # clock 0 in two bytes
+    }
+    return docs
+
+
+@pytest.mark.parametrize("env", [{}, {"YMERGE_LEAN": 0}, {"YMERGE_LEAN": 0, "YMERGE_IDENTITY": 0}],
+                         ids=["default", "no_lean", "no_identity"])
+def test_identity_copy_rejects(oracle, env):
+    """Every identity-refused shape merges like yrs with the identity copy on and off, and the
+    canonical ones are byte-identical to their input."""
+    docs = identity_reject_docs()
+    e = engine_with(**env)
+    try:
+        out, off, st = check_batch(e, oracle, batch_of(list(docs.values())))
+        for k, name in enumerate(docs):
+            if name.startswith("canonical"):
+                assert st[k] == 0 and out[int(off[k]):int(off[k + 1])].tobytes() == docs[name][0], name
+    finally:
+        e.close()

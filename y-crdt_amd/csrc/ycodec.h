@@ -894,7 +894,10 @@ __device__ __noinline__ SlowRes parse_content_slow(const uint8_t *p, uint32_t n,
 }
 
 // Parses one block (Update::decode_block, update.rs:433-488) starting at c.i.
-YM_INLINE int parse_block(Cur &c, BlockInfo &bi) {
+// defer (optional): a String content of >= defer[1] bytes is not measured here: defer[0] gets
+// its byte offset in c (bi.len = its byte count as a placeholder), and the caller's workgroup
+// measures it together (str16_coop); defer[0] stays ~0 otherwise.
+YM_INLINE int parse_block(Cur &c, BlockInfo &bi, uint32_t *defer = nullptr) {
   uint8_t info;
   bool cn;
   YM_TRY(rd_u8(c, info));
@@ -961,6 +964,11 @@ YM_INLINE int parse_block(Cur &c, BlockInfo &bi) {
     const uint8_t *s = c.p + c.i - v;
     if (v == 1) {
       bi.len = 1;
+      return 0;
+    }
+    if (defer && v >= defer[1]) {
+      defer[0] = c.i - v;
+      bi.len = v;
       return 0;
     }
     // ASCII fast check: UTF-16 length = byte length and the full split is the whole string

@@ -13,7 +13,7 @@
 //   DeleteSet built from the store in hashbrown order (id_set.rs:448-468).
 //
 // Device shape (documents outside it get status UNSUPPORTED; the CPU oracle covers them):
-// Item contents String / Deleted, GC and Skip blocks; named root parents (<= 4 roots), no
+// Item contents String / Deleted / Binary / Embed / Format, GC and Skip blocks; named root parents (<= 4 roots), no
 // parent_sub, no nested types; <= 8 clients; every block integrates when it arrives (no
 // missing dependency, no clock gap, no partially known block) and every deleted range is
 // known (no pending structs or delete sets); no String split inside a surrogate pair; per
@@ -54,7 +54,10 @@ enum : uint32_t {
   I_MKC,
   I_W
 };
-constexpr uint32_t F_ORIGIN = 1, F_RO = 2, F_DEL = 4, F_DELC = 8, F_GC = 16; // bits 8-11 root, 24-31 client
+// F_OPQ: an Item of one clock whose content is neither split nor squashed (Binary / Embed /
+// Format, content ref in bits 12-15): one segment over its content bytes, re-encoded by
+// cp_opaque (until GC turns it into Deleted(1))
+constexpr uint32_t F_ORIGIN = 1, F_RO = 2, F_DEL = 4, F_DELC = 8, F_GC = 16, F_OPQ = 32; // bits 8-11 root, 24-31 client
 // misc area layout (words)
 enum : uint32_t {
   M_CLID = 0,                      // client ids [8]
@@ -444,8 +447,8 @@ __device__ bool cp_try_squash(CDoc &D, uint32_t l, uint32_t r) { // squash r int
   const uint32_t c = fl >> 24;
   if (!(D.I(l, I_CLOCK) + D.I(l, I_LEN) == D.I(r, I_CLOCK) && (fr & F_ORIGIN) && D.I(r, I_OC) == D.m[M_CLID + c] &&
         D.I(r, I_OK) == D.I(l, I_CLOCK) + D.I(l, I_LEN) - 1 && cp_same_ro(D, l, r) && D.I(l, I_RIGHT) == r &&
-        (fl & F_DEL) == (fr & F_DEL) && (fl & F_DELC) == (fr & F_DELC)))
-    return false;
+        (fl & F_DEL) == (fr & F_DEL) && (fl & F_DELC) == (fr & F_DELC) && !((fl | fr) & F_OPQ)))
+    return false; // (ItemContent::try_squash: String, Deleted; Binary / Embed / Format never)
   if (!(fl & F_DELC)) { // String + String: segment lists concatenated
     D.sg[3 * D.I(l, I_SEG1) + 2] = D.I(r, I_SEG0);
     D.I(l, I_SEG1) = D.I(r, I_SEG1);
@@ -514,7 +517,7 @@ __device__ void cp_commit(CDoc &D) {
       if (start > re) break;
       uint32_t &fl = D.I(x, I_FLAGS);
       if (!(fl & F_GC) && (fl & F_DEL)) { // Item::gc(collector, false)
-        fl |= F_DELC;
+        fl = (fl & ~(F_OPQ | 0xF000u)) | F_DELC;
         D.I(x, I_SEG0) = D.I(x, I_SEG1) = CNIL;
       }
     }
@@ -576,7 +579,7 @@ struct CpSink {
   bool over; // beyond the per-update buffers: outside the device shape
   __device__ void on_section(uint32_t) {}
   __device__ int on_block(uint32_t client, uint32_t clock, const BlockInfo &bi, uint32_t bpos, uint32_t) {
-    if (bi.kind == BK_ITEM && bi.ref != 1 && bi.ref != 4) over = true;
+    if (bi.kind == BK_ITEM && bi.ref != 1 && bi.ref != 4 && bi.ref != 3 && bi.ref != 5 && bi.ref != 6) over = true;
     if (D->nub == D->mB) {
       over = true;
       return 0;
@@ -697,8 +700,22 @@ __device__ int cp_block(CDoc &D, const uint32_t *ub, uint32_t &dep) {
     return -1;
   }
   if (D.st) return -1;
-  if ((info & 15) == 1) {
+  const uint32_t ref = info & 15;
+  if (ref == 1) {
     fl |= F_DELC;
+  } else if (ref != 4) { // Binary (buf) / Embed (json) / Format (key, json): the content's bytes
+    const uint32_t c0 = r.i;
+    uint32_t v;
+    if (ref == 6) {
+      rd_var_u32(r, v, cn);
+      r.i += v;
+    }
+    rd_var_u32(r, v, cn);
+    r.i += v;
+    const uint32_t sg = cp_new_seg(D, D.uoff + c0, r.i - c0);
+    if (sg == CNIL) return -1;
+    D.I(x, I_SEG0) = D.I(x, I_SEG1) = sg;
+    fl |= F_OPQ | (ref << 12);
   } else { // String: one segment over the update's bytes
     uint32_t sl;
     rd_var_u32(r, sl, cn);
@@ -803,6 +820,28 @@ struct CpWriter {
     n += k;
   }
 };
+// ItemContent::encode of Binary / Embed / Format (block.rs:1731-1785; encoder.rs:170-179): the
+// buffer and the key as they are (canonical length varints), the JSON values re-serialised
+// (serde_json::from_str then Any::to_json: json_canon, already validated by the decode)
+template <class W> __device__ void cp_opaque(const uint8_t *p, uint32_t ref, W &w) {
+  Cur c{p, 0xFFFFFFFFu, 0};
+  bool cn;
+  uint32_t v;
+  if (ref == 6) {
+    rd_var_u32(c, v, cn);
+    w_str(w, p + c.i, v);
+    c.i += v;
+  }
+  rd_var_u32(c, v, cn);
+  if (ref == 3) {
+    w_str(w, p + c.i, v);
+    return;
+  }
+  Counter cnt;
+  json_canon(p + c.i, v, cnt);
+  w_var(w, cnt.n);
+  json_canon(p + c.i, v, w);
+}
 template <class W> __device__ void cp_encode(CDoc &D, W &w) {
   // clients with blocks, descending
   uint32_t ord[CP_MAXCL], n = 0;
@@ -830,7 +869,8 @@ template <class W> __device__ void cp_encode(CDoc &D, W &w) {
         w_var(w, D.I(x, I_LEN));
         continue;
       }
-      w.u8((uint8_t)(((fl & F_ORIGIN) ? 0x80 : 0) | ((fl & F_RO) ? 0x40 : 0) | ((fl & F_DELC) ? 1 : 4)));
+      const uint32_t ref = (fl & F_DELC) ? 1 : (fl & F_OPQ) ? (fl >> 12) & 15 : 4;
+      w.u8((uint8_t)(((fl & F_ORIGIN) ? 0x80 : 0) | ((fl & F_RO) ? 0x40 : 0) | ref));
       if (fl & F_ORIGIN) {
         w_var(w, D.I(x, I_OC));
         w_var(w, D.I(x, I_OK));
@@ -846,6 +886,9 @@ template <class W> __device__ void cp_encode(CDoc &D, W &w) {
       }
       if (fl & F_DELC) {
         w_var(w, D.I(x, I_LEN));
+      } else if (fl & F_OPQ) {
+        const uint32_t sg = D.I(x, I_SEG0);
+        cp_opaque(D.p + D.sg[3 * sg], ref, w);
       } else {
         uint32_t tb = 0;
         for (uint32_t s = D.I(x, I_SEG0); s != CNIL; s = D.sg[3 * s + 2]) tb += D.sg[3 * s + 1] & SEG_LEN;

@@ -454,15 +454,87 @@ __global__ void __launch_bounds__(64) k_lp_stitch(LpArgs a) {
   }
 }
 
+// str_fast16 (ycodec.h) over s[0, n) by a whole workgroup of NT lanes (a lane per aligned 16-byte chunk,
+// each starting from the flags of the word before its chunk): ok = every sequence complete
+// and shortest-form, units = the UTF-16 length (then str_info16 gives exactly that length, no
+// re-encode, no panic); red = NT / 64 + 2 LDS words.  Uniform call, barriers inside.
+template <int NT>
+__device__ __forceinline__ void str16_coop(const uint8_t *s, uint32_t n, uint32_t *red, uint32_t &units, bool &ok) {
+  const uint64_t lo = (uint64_t)s, hi = lo + n, a0 = lo & ~15ull;
+  const uint32_t H = 0x80808080u;
+  auto valid = [&](uint64_t wb) -> uint32_t {
+    uint32_t vm = H;
+    if (wb < lo) vm = lo - wb >= 4 ? 0u : vm & (~0u << (8 * (uint32_t)(lo - wb)));
+    if (wb >= hi) vm = 0;
+    else if (wb + 4 > hi) vm &= (1u << (8 * (uint32_t)(hi - wb))) - 1u;
+    return vm;
+  };
+  uint32_t u = 0, bad = 0;
+  // chunks [a0, hi + 4): the word after the last byte checks the expectations of the last one
+  for (uint64_t a = a0 + 16ull * threadIdx.x; a < hi + 4; a += 16ull * NT) {
+    const uint4 x = *(const uint4 *)a;
+    uint32_t pl = 0, p3 = 0, p4 = 0, pe0 = 0, pf0 = 0;
+    if (a > a0) { // flags of the word before the chunk
+      const uint32_t w = *(const uint32_t *)(a - 4), vm = valid(a - 4);
+      const uint32_t b7 = w & vm, b6 = (w << 1) & vm, b5 = (w << 2) & vm, b4 = (w << 3) & vm;
+      const uint32_t nz0f = ((w & 0x0F0F0F0Fu) + 0x7F7F7F7Fu) & H, nz07 = ((w & 0x07070707u) + 0x7F7F7F7Fu) & H;
+      pl = b7 & b6;
+      p3 = pl & b5;
+      p4 = p3 & b4;
+      pe0 = p3 & ~p4 & ~nz0f;
+      pf0 = p4 & ~nz07;
+    }
+    const uint32_t ws[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t vm = valid(a + 4 * j), w = ws[j];
+      const uint32_t b7 = w & vm, b6 = (w << 1) & vm, b5 = (w << 2) & vm, b4 = (w << 3) & vm;
+      const uint32_t cont = b7 & ~b6, lead = b7 & b6, ge3 = lead & b5, ge4 = ge3 & b4;
+      const uint32_t nz1e = ((w & 0x1E1E1E1Eu) + 0x7F7F7F7Fu) & H;
+      const uint32_t nz0f = ((w & 0x0F0F0F0Fu) + 0x7F7F7F7Fu) & H;
+      const uint32_t nz07 = ((w & 0x07070707u) + 0x7F7F7F7Fu) & H;
+      const uint32_t e0 = ge3 & ~ge4 & ~nz0f, f0 = ge4 & ~nz07;
+      const uint32_t exp = (lead << 8) | (pl >> 24) | (ge3 << 16) | (p3 >> 16) | (ge4 << 24) | (p4 >> 8);
+      const uint32_t e0n = (e0 << 8) | (pe0 >> 24), f0n = (f0 << 8) | (pf0 >> 24);
+      bad |= (exp ^ cont) | (lead & ~b5 & ~nz1e) | (e0n & ~b5) | (f0n & ~(b5 | b4));
+      u += __builtin_popcount((~b7 & vm) | lead) + __builtin_popcount(ge4);
+      pl = lead;
+      p3 = ge3;
+      p4 = ge4;
+      pe0 = e0;
+      pf0 = f0;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    u += __shfl_xor(u, o, 64);
+    bad |= __shfl_xor(bad, o, 64);
+  }
+  const uint32_t lane = threadIdx.x & 63;
+  if (threadIdx.x == 0) red[NT / 64] = red[NT / 64 + 1] = 0;
+  __syncthreads();
+  if (lane == 0) {
+    atomicAdd(&red[NT / 64], u);
+    atomicOr(&red[NT / 64 + 1], bad);
+  }
+  __syncthreads();
+  units = red[NT / 64];
+  ok = red[NT / 64 + 1] == 0;
+  __syncthreads();
+}
+
 // ------------------------------------------------------------------ k_lp_expand
 constexpr uint32_t LPX_NT = 256;
 constexpr uint32_t LPX_LA = 1024, LPX_STAGE_W = (LP_CH + LPX_LA) / 4 + 4;
+// Strings of >= LPX_COOP bytes are measured by the whole workgroup (str16_coop), up to LPX_DEF
+// per tile: one lane walking the editing traces' 69 KB pasted string held k_lp_expand 3.2 ms
+constexpr uint32_t LPX_COOP = 2048, LPX_DEF = 16;
 __global__ void __launch_bounds__(LPX_NT) k_lp_expand(LpArgs a) {
   __shared__ uint32_t extl[LP_CH];
   __shared__ uint32_t pos[LP_CH / 2 + 1];
   __shared__ __align__(16) uint32_t stage[LPX_STAGE_W]; // the chunk's bytes (+ look-ahead)
-  __shared__ uint32_t ws[LPX_NT / 64 + 1];
+  __shared__ uint32_t ws[LPX_NT / 64 + 2];
   __shared__ uint32_t s_flags;
+  __shared__ uint32_t s_ndef, s_doff[LPX_DEF], s_dn[LPX_DEF], s_dlen[LPX_DEF];
   ym_set_grammar(a.v1x);
   const uint32_t t = threadIdx.x, nseg = a.g[LPG_SEGS] < a.scap ? a.g[LPG_SEGS] : a.scap;
   for (uint32_t s = blockIdx.x; s < nseg; s += gridDim.x) {
@@ -512,15 +584,46 @@ __global__ void __launch_bounds__(LPX_NT) k_lp_expand(LpArgs a) {
       BlockInfo bi;
       bi.len = 0;
       uint32_t p = 0, end = 0;
+      if (t == 0) s_ndef = 0;
+      __syncthreads();
+      uint32_t dfr[2] = {~0u, LPX_COOP}, dq = LPX_DEF;
+      int perr = 0;
       if (i < nb) {
         p = pos[i];
         const uint32_t x0 = extl[p - cs];
         const bool in_lds = x0 < LP_COLD && (x0 & LP_OFF) <= se;
         Cur cc = in_lds ? Cur{lb, L - cs, p - cs} : Cur{ub, L, p};
-        if (parse_block(cc, bi)) {
+        perr = parse_block(cc, bi, dfr);
+        end = cc.i + (in_lds ? cs : 0u);
+        if (!perr && dfr[0] != ~0u) { // a long String: measured below by the workgroup
+          dfr[0] += in_lds ? cs : 0u;
+          dq = atomicAdd(&s_ndef, 1u);
+          if (dq < LPX_DEF) {
+            s_doff[dq] = dfr[0];
+            s_dn[dq] = dfr[1] = bi.len;
+          }
+        }
+      }
+      __syncthreads();
+      {
+        const uint32_t nd = s_ndef < LPX_DEF ? s_ndef : LPX_DEF;
+        for (uint32_t q = 0; q < nd; q++) {
+          uint32_t units;
+          bool ok;
+          str16_coop<LPX_NT>(ub + s_doff[q], s_dn[q], ws, units, ok);
+          if (t == 0) s_dlen[q] = ok ? units : ~0u;
+        }
+        __syncthreads();
+      }
+      if (i < nb) {
+        if (!perr && dfr[0] != ~0u) {
+          const uint32_t r = dq < LPX_DEF ? s_dlen[dq] : ~0u;
+          if (r != ~0u) bi.len = r;
+          else str_info16(ub + dfr[0], bi.len, bi); // not complete shortest-form (or a 17th): the serial walk
+        }
+        if (perr) {
           flags |= LPF_FALLBACK;
         } else {
-          end = cc.i + (in_lds ? cs : 0u);
           stored = !(bi.kind == BK_SKIP || (bi.kind == BK_ITEM && bi.len == 0));
           const uint32_t x = extl[p - cs];
           if (x != LP_COLD && (x == LP_BAD || (x & LP_OFF) != end || !(x & LP_UNST) != stored))

@@ -185,7 +185,7 @@ __global__ void __launch_bounds__(DEC_NT, 8) k_decode(const uint8_t *bytes, cons
         const uint32_t q = atomicAdd(&n_cx, 1u);
         cx_lane[q] = t;
         cx_at[q] = at;
-        cx_nb[q] = (uint16_t)s.nb; // need <= DEC_OVF words: counts < 2^16
+        cx_nb[q] = (uint16_t)s.nb; // a staged update is <= DEC_STAGE (16 KB): its counts are < 2^16
         cx_ne[q] = (uint16_t)s.ne;
       }
     }
