@@ -64,9 +64,9 @@ def fixtures():
 FIXTURE_REASONS = {
     "_rev": CU["GAP"], "_shuf": CU["GAP"],  # out-of-order delivery: pending structs
     "utf16_text": CU["SURROGATE"], "utf16_log_then_snapshot": CU["SURROGATE"],
-    "map_array_any": CU["UPDATE_SHAPE"], "map_array_xml_nested": CU["UPDATE_SHAPE"], "numbers": CU["UPDATE_SHAPE"],
     "subdoc": None,  # subdoc: the oracle reports UNSUPPORTED too
-    # rich_text (Format / Embed items) is on the device since round 6
+    # rich_text (Format / Embed items), map_array_any, map_array_xml_nested and numbers (maps,
+    # nested types, Any content) are on the device since round 6
 }
 
 
@@ -117,9 +117,75 @@ def edge_docs():
     docs.append([u0, u0, upd(1, 3, [s_after(1, 2, "d")]), u0]); reasons.append(0)
     # GC block then items
     docs.append([upd(1, 0, [b"\x00" + var(4)]), upd(1, 4, [s_after(1, 3, "x")])]); reasons.append(0)
-    # map entry (parent_sub): outside the shape
-    docs.append([upd(1, 0, [bytes([0x24]) + t + vstr("k") + vstr("v")])]); reasons.append(CU["PARENT"])
+    # map entry (parent_sub) with a String value
+    docs.append([upd(1, 0, [bytes([0x24]) + t + vstr("k") + vstr("v")])]); reasons.append(0)
+    docs += nested_docs()
+    reasons += [0] * (len(docs) - len(reasons) - 1) + [None]
     return batch_of(docs), reasons
+
+
+def _anys(vals):
+    """ItemContent::Any (ref 8): strings (tag 119), ints (125), null (126)."""
+    b = var(len(vals))
+    for v in vals:
+        if v is None:
+            b += bytes([126])
+        elif isinstance(v, int):
+            b += bytes([125]) + var(2 * v)  # (non-negative: the sign bit 6 clear; v < 64)
+        else:
+            b += bytes([119]) + vstr(v)
+    return b
+
+
+def nested_docs():
+    """Maps, nested types and list contents (round 6): a key written twice, concurrent writes of
+    one key from two clients in both delivery orders, a nested array with Any items squashed,
+    split by a delete and then deleted with its type (children become GC structs), XmlElement
+    / XmlText nesting, a JSON list split by a delete, and (last) an ID parent that is not a
+    type (yrs panics)."""
+    t = var(1) + vstr("t")
+
+    def upd(client, clock, blocks, ds=b"\x00"):
+        return var(1) + var(len(blocks)) + var(client) + var(clock) + b"".join(blocks) + ds
+
+    def dsu(client, ranges):
+        return b"\x00" + var(1) + var(client) + var(len(ranges)) + b"".join(var(a) + var(n) for a, n in ranges)
+
+    def idp(c, k):
+        return var(0) + var(c) + var(k)
+
+    docs = []
+    # a key written twice: the second value (origin = the first) deletes the first
+    docs.append([upd(1, 0, [bytes([0x28]) + t + vstr("k") + _anys(["a"])]),
+                 upd(1, 1, [bytes([0x88]) + var(1) + var(0) + _anys(["b", 7])])])
+    # two clients write the same key concurrently (no origins): both delivery orders
+    k1 = upd(1, 0, [bytes([0x28]) + t + vstr("k") + _anys(["one"])])
+    k2 = upd(2, 0, [bytes([0x28]) + t + vstr("k") + _anys(["two"])])
+    docs.append([k1, k2])
+    docs.append([k2, k1])
+    # a nested array under a map key; Any items appended (squashed), one element deleted (split),
+    # then the array deleted: its children become GC structs
+    arr = upd(1, 0, [bytes([0x27]) + t + vstr("arr") + bytes([0])])
+    c1 = upd(1, 1, [bytes([0x08]) + idp(1, 0) + _anys([1, 2, 3])])
+    c2 = upd(1, 4, [bytes([0x88]) + var(1) + var(3) + _anys([4, None])])
+    docs.append([arr, c1, c2])
+    docs.append([arr, c1, c2, dsu(1, [(2, 1)])])
+    docs.append([arr, c1, c2, dsu(1, [(2, 1)]), dsu(1, [(0, 1)])])
+    docs.append([arr, c1, c2, dsu(1, [(0, 1)])])
+    # XmlElement "p" in root "x", an XmlText in it, a String in that; a second client types after it
+    x = var(1) + vstr("x")
+    e1 = upd(1, 0, [bytes([0x07]) + x + bytes([3]) + vstr("p")])
+    e2 = upd(1, 1, [bytes([0x07]) + idp(1, 0) + bytes([6])])
+    e3 = upd(1, 2, [bytes([0x04]) + idp(1, 1) + vstr("hi")])
+    e4 = upd(2, 0, [bytes([0x84]) + var(1) + var(3) + vstr("!")])
+    docs.append([e1, e2, e3, e4])
+    docs.append([e1, e2, e3, e4, dsu(1, [(3, 1)]), dsu(1, [(1, 1)])])
+    # a JSON list (ref 2: L + 1 JSON texts) split by deleting its middle element
+    j = upd(1, 0, [bytes([0x02]) + t + var(2) + vstr('"a"') + vstr("1") + vstr("null")])
+    docs.append([j, dsu(1, [(1, 1)])])
+    # an ID parent that is a String item: "parent points to a block which is not a shared type"
+    docs.append([upd(1, 0, [bytes([0x04]) + t + vstr("ab")]), upd(1, 2, [bytes([0x04]) + idp(1, 0) + vstr("z")])])
+    return docs
 
 
 # ---------------------------------------------------------------- an independent shape check

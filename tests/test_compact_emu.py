@@ -66,11 +66,11 @@ def check(emu, oracle, b, reasons=None, min_device=1.0):
 def test_reference_corpus(emu, oracle):
     """The reference corpus (assets/bench-input/small-test-dataset.bin, 5,320 real Yjs documents):
     every document the device writes equals the oracle byte for byte; every refusal shows its
-    shape in the document's bytes; the device share is pinned (round 6: Binary / Embed / Format
-    content on the device, 4,225 of 5,320)."""
+    shape in the document's bytes; the device share is pinned (round 6: every content kind but
+    Doc / Move / WeakLink, maps and nested types on the device: all 5,320)."""
     b = workloads.dataset_docs()
-    st, why = check(emu, oracle, b, reasons=[None] * b.n_docs, min_device=0.79)
-    assert (st == 21).sum() <= 1095
+    st, why = check(emu, oracle, b, reasons=[None] * b.n_docs, min_device=1.0)
+    assert (st == 21).sum() == 0
 
 
 def test_text_docs(emu, oracle):

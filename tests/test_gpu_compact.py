@@ -85,5 +85,5 @@ def test_reference_corpus(engine, emu, oracle):
     """All 5,320 documents of the reference corpus through k_compact: statuses equal the CPU
     build's, written bytes equal the oracle's, refusals show their shape; device share pinned."""
     b = workloads.dataset_docs()
-    st = check_gpu(engine, emu, oracle, b, min_device=0.79)
-    assert (st == 21).sum() <= 1095
+    st = check_gpu(engine, emu, oracle, b, min_device=1.0)
+    assert (st == 21).sum() == 0

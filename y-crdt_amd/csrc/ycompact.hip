@@ -13,23 +13,25 @@
 //   DeleteSet built from the store in hashbrown order (id_set.rs:448-468).
 //
 // Device shape (documents outside it get status UNSUPPORTED; the CPU oracle covers them):
-// Item contents String / Deleted / Binary / Embed / Format, GC and Skip blocks; named root parents (<= 4 roots), no
-// parent_sub, no nested types; <= 8 clients; every block integrates when it arrives (no
-// missing dependency, no clock gap, no partially known block) and every deleted range is
-// known (no pending structs or delete sets); no String split inside a surrogate pair; per
-// update <= 16 blocks and <= 64 deleted ranges; the output fits the document's slot.
+// Item contents Deleted / JSON / Binary / String / Embed / Format / Type (not WeakLink) / Any,
+// GC and Skip blocks; named roots (<= 8) and nested types (ID parents) with parent_sub map
+// entries; <= 8 clients; every block integrates when it arrives (no missing dependency, no
+// clock gap, no partially known block) and every deleted range is known (no pending structs
+// or delete sets); no String split inside a surrogate pair; per update <= 16 blocks and <= 64
+// deleted ranges; the output fits the document's slot.
 //
-// Per-document HBM scratch (u32 words at 92 u0 + 2304 d): items (16 words, 4U + 64 of
-// them), String segments (3 words: byte offset in the document, length, next), per-client
-// arrays of the blocks as they arrived (start clock, item; lookups binary-search them and walk
-// the clock chain), and a 2 KB area for the client table, roots and per-update buffers.
+// Per-document HBM scratch (cp_words): items (I_W words), content segments (3 words: byte
+// offset in the document, length / element count, next), per-client arrays of the blocks as
+// they arrived (start clock, item; lookups binary-search them and walk the clock chain),
+// per-update buffers, the transaction DeleteSet, branches (root and nested types) with their
+// map entries (parent_sub -> current item), and a work stack for recursive deletes / GC.
 #include "ycodec.h"
 #include "ykernels.h"
 #include "ywalk.h"
 
 namespace ym {
 
-constexpr uint32_t CP_MAXCL = 8, CP_MAXROOT = 4;
+constexpr uint32_t CP_MAXCL = 8, CP_MAXROOT = 8;
 constexpr uint32_t CP_STAGE = 256; // per-lane LDS copy of the current update (bytes)
 constexpr uint32_t CP_IS = 16, CP_IN = 64; // arrival index: one sample per 16 arrivals, 64 samples
 constexpr uint32_t CP_LANES = 16;          // documents per wavefront at most (LDS sized for them)
@@ -52,12 +54,19 @@ enum : uint32_t {
   I_SEG1,
   I_MKI,
   I_MKC,
+  I_PAR, // parent branch (CNIL: TypePtr::Unknown)
+  I_PSO, // parent_sub key: byte offset in the document
+  I_PSL, // its length | PS_HAS (0: no parent_sub)
   I_W
 };
-// F_OPQ: an Item of one clock whose content is neither split nor squashed (Binary / Embed /
-// Format, content ref in bits 12-15): one segment over its content bytes, re-encoded by
-// cp_opaque (until GC turns it into Deleted(1))
-constexpr uint32_t F_ORIGIN = 1, F_RO = 2, F_DEL = 4, F_DELC = 8, F_GC = 16, F_OPQ = 32; // bits 8-11 root, 24-31 client
+constexpr uint32_t PS_HAS = 0x80000000u, PS_LEN = 0x7FFFFFFFu;
+// Content: ItemContent ref in bits 12-15 (cp_ref); F_DELC = Deleted; F_OPQ: one clock, never
+// split nor squashed (Binary / Embed / Format / Type): one segment over its content bytes,
+// re-encoded by cp_opaque (a Type item keeps its own branch in I_SEG1); String / Any / JSON:
+// a segment list (String: byte ranges; Any / JSON: element runs).  F_GCM: marked by the GC of
+// a deleted parent type (becomes a GC struct at the end of the commit).  Bits 24-31: client.
+constexpr uint32_t F_ORIGIN = 1, F_RO = 2, F_DEL = 4, F_DELC = 8, F_GC = 16, F_OPQ = 32, F_GCM = 64;
+__host__ __device__ inline uint32_t cp_ref(uint32_t fl) { return (fl >> 12) & 15; }
 // misc area layout (words)
 enum : uint32_t {
   M_CLID = 0,                      // client ids [8]
@@ -67,8 +76,8 @@ enum : uint32_t {
   M_BEFORE = M_NBLK + CP_MAXCL,    // clock before the transaction [8]
   M_ROOTOFF = M_BEFORE + CP_MAXCL, // root name byte offset [4]
   M_ROOTLEN = M_ROOTOFF + CP_MAXROOT,
-  M_ROOTSTART = M_ROOTLEN + CP_MAXROOT,
-  M_CBK = M_ROOTSTART + CP_MAXROOT, // client -> its arrival array (index into the count header)
+  M_ROOTBR = M_ROOTLEN + CP_MAXROOT, // its branch
+  M_CBK = M_ROOTBR + CP_MAXROOT,     // client -> its arrival array (index into the count header)
   M_UE = M_CBK + CP_MAXCL,          // update DS entry clients [16] (table order)
   M_UEN = M_UE + 16,               // ranges per entry [16]
   M_HCL = M_UEN + 16,               // the count header's block clients [8]
@@ -87,7 +96,10 @@ static_assert(CP_LANES * (M_END * 4 + CP_STAGE) <= 48 * 1024, "three workgroups 
 enum : uint32_t { H_NB = 0, H_NR, H_MB, H_MR, H_NCL, H_OVER, H_CL = 8, H_CN = 16, H_CO = 24, CP_HDR = 32 };
 __device__ __forceinline__ uint64_t cp_words(const uint32_t *h) { // scratch words of one document
   const uint64_t items = 3ull * h[H_NB] + 2ull * h[H_NR] + 64;
-  return 1024 + items * (I_W + 6) + 2ull * (h[H_NB] + 8) + 9ull * h[H_MB] + 3ull * h[H_MR] + 4ull * h[H_MR] + 64;
+  // misc, items + segments + transaction, arrivals, update buffers, branches, map entries +
+  // work stack + GC marks
+  return 1024 + items * (I_W + 6) + 2ull * (h[H_NB] + 8) + 9ull * h[H_MB] + 3ull * h[H_MR] + 4ull * h[H_MR] + 64 +
+         4ull * (h[H_NB] + CP_MAXROOT + 8) + 6ull * items;
 }
 // why a document is outside the device shape (written to FastOut::path)
 enum : uint32_t {
@@ -98,11 +110,11 @@ enum : uint32_t {
   CU_ARRIVALS,       // per-client arrival array full
   CU_GAP,            // clock gap: pending structs
   CU_PARTIAL,        // partially known block (integrate with an offset)
-  CU_PARENT,         // ID parent or parent_sub
+  CU_PARENT,         // (unused since round 6: nested types and parent_sub are on the device)
   CU_ROOTS,          // more than CP_MAXROOT root types
   CU_PENDING_DS,     // deleted range beyond the known state: pending delete set
   CU_PENDING,        // missing dependency: pending structs
-  CU_UPDATE_SHAPE,   // update over DS_SMALL delete-set entries, or content other than String / Deleted
+  CU_UPDATE_SHAPE,   // update over DS_SMALL delete-set entries, or Doc / Move / WeakLink content
   CU_OUTPUT          // output over the document's slot
 };
 
@@ -114,8 +126,10 @@ struct CDoc {
   uint32_t *ubr, *ub, *stk, *ur, *mb; // update blocks (stream order, integration order), stack,
                                       // DS ranges, merge blocks
   uint32_t *tx;                       // transaction DeleteSet (client index, start, end), cap_i
+  uint32_t *bt, *me, *wk, *gm;        // branches (BR_W), map entries (ME_W), work stack, GC marks
   const uint32_t *h;                  // the document's count header
   uint32_t ni, cap_i, ns, cap_s, mB, mR;
+  uint32_t nbr, cap_b, nme, ngm;
   uint32_t ncl, nroot, nub, nur, nue, nt, nm;
   uint32_t gen_i, gen_c;
   int st;      // status (first error / unsupported)
@@ -206,7 +220,7 @@ __device__ uint32_t cp_new_item(CDoc &D) {
   const uint32_t x = D.ni++;
   for (uint32_t f = 0; f < I_W; f++) D.I(x, f) = 0;
   D.I(x, I_FWD) = D.I(x, I_LEFT) = D.I(x, I_RIGHT) = D.I(x, I_CPREV) = D.I(x, I_CNEXT) = CNIL;
-  D.I(x, I_SEG0) = D.I(x, I_SEG1) = CNIL;
+  D.I(x, I_SEG0) = D.I(x, I_SEG1) = D.I(x, I_PAR) = CNIL;
   return x;
 }
 // segment words: byte offset in the document, length | SEG_ASCII (every char one byte: UTF-16
@@ -268,6 +282,100 @@ __device__ uint32_t cp_str_split(CDoc &D, uint32_t x, uint32_t off) {
   D.st = E_PANIC; // offset past the content: yrs' splice unwraps None
   return CNIL;
 }
+// ItemContent::splice(off) of an Any / JSON list (block.rs:1837-1879): element runs, split
+// inside a run at the byte offset of its (off - u)-th element (Any values: any_skip; JSON:
+// strings); returns the right part's first segment
+__device__ uint32_t cp_el_split(CDoc &D, uint32_t x, uint32_t off, bool any) {
+  uint32_t u = 0, s = D.I(x, I_SEG0);
+  while (s != CNIL) {
+    const uint32_t n = D.sg[3 * s + 1];
+    if (off - u <= n) {
+      const uint32_t k = off - u;
+      uint32_t r;
+      if (k == n) { // boundary at the end of run s
+        r = D.sg[3 * s + 2];
+        D.sg[3 * s + 2] = CNIL;
+      } else {
+        Cur c{D.p, 0xFFFFFFFFu, D.sg[3 * s]};
+        for (uint32_t q = 0; q < k; q++) {
+          if (any) {
+            any_skip(c);
+          } else {
+            uint32_t v;
+            bool cn;
+            rd_var_u32(c, v, cn);
+            c.i += v;
+          }
+        }
+        r = cp_new_seg(D, c.i, n - k);
+        if (r == CNIL) return CNIL;
+        D.sg[3 * r + 2] = D.sg[3 * s + 2];
+        D.sg[3 * s + 1] = k;
+        D.sg[3 * s + 2] = CNIL;
+      }
+      D.I(x, I_SEG1) = s;
+      return r;
+    }
+    u += n;
+    s = D.sg[3 * s + 2];
+  }
+  D.st = E_PANIC;
+  return CNIL;
+}
+
+// ------------------------------------------------------------------ branches (types) and maps
+// A branch: root type (name in the misc root table) or the nested type of a Type item; its
+// sequence start and its map (parent_sub -> current item: entries in insertion order).
+enum : uint32_t { B_START = 0, B_ITEM, B_MAP, B_ROOT, BR_W };
+enum : uint32_t { E_KOFF = 0, E_KLEN, E_VAL, E_NEXT, ME_W };
+__device__ uint32_t cp_new_branch(CDoc &D, uint32_t item, uint32_t root) {
+  if (D.nbr == D.cap_b) {
+    cp_unsup(D, CU_ITEMS);
+    return CNIL;
+  }
+  uint32_t *b = D.bt + (size_t)BR_W * D.nbr;
+  b[B_START] = CNIL;
+  b[B_ITEM] = item;
+  b[B_MAP] = CNIL;
+  b[B_ROOT] = root;
+  return D.nbr++;
+}
+__device__ uint32_t &cp_bw(CDoc &D, uint32_t b, uint32_t f) { return D.bt[(size_t)BR_W * b + f]; }
+// the map entry of x's parent_sub key in branch b (CNIL: none)
+__device__ uint32_t cp_map_entry(CDoc &D, uint32_t b, uint32_t x) {
+  const uint32_t ko = D.I(x, I_PSO), kn = D.I(x, I_PSL) & PS_LEN;
+  for (uint32_t e = cp_bw(D, b, B_MAP); e != CNIL; e = D.me[ME_W * e + E_NEXT])
+    if (D.me[ME_W * e + E_KLEN] == kn && bytes_eq(D.p + D.me[ME_W * e + E_KOFF], D.p + ko, kn)) return e;
+  return CNIL;
+}
+__device__ uint32_t cp_map_get(CDoc &D, uint32_t b, uint32_t x) {
+  const uint32_t e = cp_map_entry(D, b, x);
+  return e == CNIL ? CNIL : D.me[ME_W * e + E_VAL];
+}
+__device__ void cp_map_set(CDoc &D, uint32_t b, uint32_t x, uint32_t v) { // key of x -> v
+  uint32_t e = cp_map_entry(D, b, x);
+  if (e == CNIL) {
+    if (D.nme == D.cap_i) {
+      cp_unsup(D, CU_ITEMS);
+      return;
+    }
+    e = D.nme++;
+    D.me[ME_W * e + E_KOFF] = D.I(x, I_PSO);
+    D.me[ME_W * e + E_KLEN] = D.I(x, I_PSL) & PS_LEN;
+    D.me[ME_W * e + E_NEXT] = CNIL;
+    uint32_t *link = &cp_bw(D, b, B_MAP);
+    while (*link != CNIL) link = &D.me[ME_W * *link + E_NEXT];
+    *link = e;
+  }
+  D.me[ME_W * e + E_VAL] = v;
+}
+// the leftmost item of x's key in branch b (the YATA scan start / relink point of a map entry)
+__device__ uint32_t cp_map_first(CDoc &D, uint32_t b, uint32_t x) {
+  uint32_t o = cp_map_get(D, b, x);
+  for (uint32_t g = D.ni; o != CNIL && D.I(o, I_LEFT) != CNIL && g; g--) o = D.I(o, I_LEFT);
+  return o;
+}
+
 // ItemPtr::splice + BlockStore::split_block (block.rs:435-478, block_store.rs:456-475)
 __device__ uint32_t cp_split(CDoc &D, uint32_t x, uint32_t off) {
   if (off == 0) return CNIL;
@@ -276,9 +384,13 @@ __device__ uint32_t cp_split(CDoc &D, uint32_t x, uint32_t off) {
   const uint32_t fl = D.I(x, I_FLAGS);
   if (fl & F_DELC) {
     D.I(r, I_LEN) = D.I(x, I_LEN) - off;
+  } else if (fl & F_OPQ) { // one-clock content: splice returns None, yrs unwraps
+    D.st = E_PANIC;
+    return CNIL;
   } else {
     const uint32_t seg1 = D.I(x, I_SEG1); // the right part ends where the item did
-    const uint32_t rs = cp_str_split(D, x, off);
+    const uint32_t ref = cp_ref(fl);
+    const uint32_t rs = ref == 4 ? cp_str_split(D, x, off) : cp_el_split(D, x, off, ref == 8);
     if (D.st) return CNIL;
     D.I(r, I_SEG0) = rs;
     // the split segment was the last one: the new right segment is the last; else the old last
@@ -292,9 +404,13 @@ __device__ uint32_t cp_split(CDoc &D, uint32_t x, uint32_t off) {
   D.I(r, I_OK) = D.I(x, I_CLOCK) + off - 1;
   D.I(r, I_RC) = D.I(x, I_RC);
   D.I(r, I_RK) = D.I(x, I_RK);
+  D.I(r, I_PAR) = D.I(x, I_PAR);
+  D.I(r, I_PSO) = D.I(x, I_PSO);
+  D.I(r, I_PSL) = D.I(x, I_PSL);
   D.I(x, I_LEN) = off;
-  // list links
+  // list links (the right part of a parent's current map value becomes the value)
   const uint32_t xr = D.I(x, I_RIGHT);
+  if ((D.I(x, I_PSL) & PS_HAS) && xr == CNIL && D.I(x, I_PAR) != CNIL) cp_map_set(D, D.I(x, I_PAR), x, r);
   D.I(r, I_LEFT) = x;
   D.I(r, I_RIGHT) = xr;
   if (xr != CNIL) D.I(xr, I_LEFT) = r;
@@ -337,12 +453,43 @@ __device__ void cp_txn_insert(CDoc &D, uint32_t c, uint32_t s, uint32_t e) {
   D.tx[3 * D.nt + 2] = e;
   D.nt++;
 }
-__device__ bool cp_delete(CDoc &D, uint32_t x) { // TransactionMut::delete (no nested types here)
-  uint32_t &fl = D.I(x, I_FLAGS);
-  if (fl & F_DEL) return false;
-  fl |= F_DEL;
-  cp_txn_insert(D, fl >> 24, D.I(x, I_CLOCK), D.I(x, I_CLOCK) + D.I(x, I_LEN));
-  return true;
+__device__ void cp_merge_block(CDoc &D, uint32_t c, uint32_t clock);
+// TransactionMut::delete (transaction.rs:579-662): the item; a Type's children (its sequence's
+// live items, then every current map value) depth first, in that order (an explicit stack);
+// a child already deleted goes to merge_blocks
+__device__ bool cp_delete(CDoc &D, uint32_t x0) {
+  uint32_t sp = 0;
+  bool result = false, top = true;
+  D.wk[sp++] = x0;
+  while (sp && !D.st) {
+    const uint32_t x = D.wk[--sp];
+    uint32_t &fl = D.I(x, I_FLAGS);
+    if (fl & F_DEL) {
+      if (!top) cp_merge_block(D, fl >> 24, D.I(x, I_CLOCK));
+      top = false;
+      continue;
+    }
+    if (top) result = true;
+    top = false;
+    fl |= F_DEL;
+    cp_txn_insert(D, fl >> 24, D.I(x, I_CLOCK), D.I(x, I_CLOCK) + D.I(x, I_LEN));
+    if (cp_ref(fl) != 7 || (fl & F_DELC)) continue;
+    const uint32_t b = D.I(x, I_SEG1);
+    uint32_t n = 0;
+    for (uint32_t p = cp_bw(D, b, B_START), g = D.ni; p != CNIL && g; p = D.I(p, I_RIGHT), g--)
+      n += !(D.I(p, I_FLAGS) & F_DEL);
+    for (uint32_t e = cp_bw(D, b, B_MAP); e != CNIL; e = D.me[ME_W * e + E_NEXT]) n++;
+    if (sp + n > D.cap_i) {
+      cp_unsup(D, CU_ITEMS);
+      return result;
+    }
+    uint32_t k = sp + n; // children popped in order: the first on top
+    for (uint32_t p = cp_bw(D, b, B_START), g = D.ni; p != CNIL && g; p = D.I(p, I_RIGHT), g--)
+      if (!(D.I(p, I_FLAGS) & F_DEL)) D.wk[--k] = p;
+    for (uint32_t e = cp_bw(D, b, B_MAP); e != CNIL; e = D.me[ME_W * e + E_NEXT]) D.wk[--k] = D.me[ME_W * e + E_VAL];
+    sp += n;
+  }
+  return result;
 }
 __device__ void cp_merge_block(CDoc &D, uint32_t c, uint32_t clock) {
   if (D.nm == 2 * D.mR + 2) {
@@ -363,14 +510,18 @@ __device__ bool cp_same_ro(CDoc &D, uint32_t a, uint32_t b) {
   const uint32_t fa = D.I(a, I_FLAGS) & F_RO, fb = D.I(b, I_FLAGS) & F_RO;
   return fa == fb && (!fa || (D.I(a, I_RC) == D.I(b, I_RC) && D.I(a, I_RK) == D.I(b, I_RK)));
 }
-// the new item x is repaired (left / right / root set); links it into its root's sequence
-__device__ void cp_integrate(CDoc &D, uint32_t x) {
-  const uint32_t root = (D.I(x, I_FLAGS) >> 8) & 15;
+// the new item x is repaired (left / right / parent branch set); links it into its parent's
+// sequence or map entry (block.rs:482-771).  Returns true when x must be deleted right after
+// (its parent type is deleted, or it is not the current value of its map key).
+__device__ bool cp_integrate(CDoc &D, uint32_t x) {
+  const uint32_t par = D.I(x, I_PAR);
   uint32_t left = D.I(x, I_LEFT), right = D.I(x, I_RIGHT);
   const bool rnull_or_left = right == CNIL || D.I(right, I_LEFT) != CNIL;
   const bool left_other = left != CNIL && D.I(left, I_RIGHT) != right;
   if ((left == CNIL && rnull_or_left) || left_other) {
-    uint32_t o = left != CNIL ? D.I(left, I_RIGHT) : D.m[M_ROOTSTART + root];
+    uint32_t o = left != CNIL                  ? D.I(left, I_RIGHT)
+                 : (D.I(x, I_PSL) & PS_HAS) ? cp_map_first(D, par, x)
+                                            : cp_bw(D, par, B_START);
     uint32_t nl = left;
     const uint32_t gi = ++D.gen_i;
     uint32_t gc = ++D.gen_c;
@@ -379,7 +530,7 @@ __device__ void cp_integrate(CDoc &D, uint32_t x) {
     while (o != CNIL && o != D.I(x, I_RIGHT)) {
       if (guard-- == 0) {
         cp_unsup(D, CU_ITEMS);
-        return;
+        return false;
       }
       D.I(o, I_MKI) = gi;
       D.I(o, I_MKC) = gc;
@@ -403,19 +554,41 @@ __device__ void cp_integrate(CDoc &D, uint32_t x) {
     D.I(x, I_LEFT) = nl;
   }
   left = D.I(x, I_LEFT);
+  if (!(D.I(x, I_PSL) & PS_HAS) && left != CNIL) { // parent_sub from the neighbours
+    const uint32_t src = (D.I(left, I_PSL) & PS_HAS) ? left : D.I(x, I_RIGHT);
+    if (src != CNIL) {
+      D.I(x, I_PSO) = D.I(src, I_PSO);
+      D.I(x, I_PSL) = D.I(src, I_PSL);
+    }
+  }
+  const bool psub = D.I(x, I_PSL) & PS_HAS;
   if (left != CNIL) {
     D.I(x, I_RIGHT) = D.I(left, I_RIGHT);
     D.I(left, I_RIGHT) = x;
+  } else if (psub) {
+    D.I(x, I_RIGHT) = cp_map_first(D, par, x);
   } else {
-    D.I(x, I_RIGHT) = D.m[M_ROOTSTART + root];
-    D.m[M_ROOTSTART + root] = x;
+    D.I(x, I_RIGHT) = cp_bw(D, par, B_START);
+    cp_bw(D, par, B_START) = x;
   }
   right = D.I(x, I_RIGHT);
-  if (right != CNIL) D.I(right, I_LEFT) = x;
+  if (right != CNIL) {
+    D.I(right, I_LEFT) = x;
+  } else if (psub) { // the key's current value; the previous one is deleted
+    cp_map_set(D, par, x, x);
+    if (left != CNIL) cp_delete(D, left);
+  }
   if (D.I(x, I_FLAGS) & F_DELC) { // ItemContent::Deleted
     D.I(x, I_FLAGS) |= F_DEL;
     cp_txn_insert(D, D.cl_of(x), D.I(x, I_CLOCK), D.I(x, I_CLOCK) + D.I(x, I_LEN));
   }
+  if (cp_ref(D.I(x, I_FLAGS)) == 7) { // ItemContent::Type: its branch
+    const uint32_t b = cp_new_branch(D, x, CNIL);
+    if (b == CNIL) return false;
+    D.I(x, I_SEG1) = b;
+  }
+  const uint32_t pit = cp_bw(D, par, B_ITEM);
+  return (pit != CNIL && (D.I(pit, I_FLAGS) & F_DEL)) || (psub && D.I(x, I_RIGHT) != CNIL);
 }
 // appends a cell to its client's clock chain and arrival array
 __device__ void cp_push(CDoc &D, int c, uint32_t x) {
@@ -447,9 +620,9 @@ __device__ bool cp_try_squash(CDoc &D, uint32_t l, uint32_t r) { // squash r int
   const uint32_t c = fl >> 24;
   if (!(D.I(l, I_CLOCK) + D.I(l, I_LEN) == D.I(r, I_CLOCK) && (fr & F_ORIGIN) && D.I(r, I_OC) == D.m[M_CLID + c] &&
         D.I(r, I_OK) == D.I(l, I_CLOCK) + D.I(l, I_LEN) - 1 && cp_same_ro(D, l, r) && D.I(l, I_RIGHT) == r &&
-        (fl & F_DEL) == (fr & F_DEL) && (fl & F_DELC) == (fr & F_DELC) && !((fl | fr) & F_OPQ)))
-    return false; // (ItemContent::try_squash: String, Deleted; Binary / Embed / Format never)
-  if (!(fl & F_DELC)) { // String + String: segment lists concatenated
+        (fl & F_DEL) == (fr & F_DEL) && cp_ref(fl) == cp_ref(fr) && !((fl | fr) & F_OPQ)))
+    return false; // (ItemContent::try_squash, block.rs:1884-1906: String, Any, JSON, Deleted)
+  if (!(fl & F_DELC)) { // segment lists concatenated
     D.sg[3 * D.I(l, I_SEG1) + 2] = D.I(r, I_SEG0);
     D.I(l, I_SEG1) = D.I(r, I_SEG1);
   }
@@ -457,6 +630,9 @@ __device__ bool cp_try_squash(CDoc &D, uint32_t l, uint32_t r) { // squash r int
   const uint32_t rr = D.I(r, I_RIGHT);
   if (rr != CNIL) D.I(rr, I_LEFT) = l;
   D.I(l, I_RIGHT) = rr;
+  // the map's current value was r: now l (s_fix_map)
+  if ((D.I(r, I_PSL) & PS_HAS) && D.I(r, I_PAR) != CNIL && cp_map_get(D, D.I(r, I_PAR), r) == r)
+    cp_map_set(D, D.I(r, I_PAR), r, l);
   return true;
 }
 // unlinks r (squashed into its clock predecessor l) from the clock chain
@@ -481,6 +657,48 @@ __device__ void cp_squash_left(CDoc &D, uint32_t r) {
 }
 
 // ------------------------------------------------------------------ commit (transaction.rs:828-910)
+// ItemContent::gc of a Type (block.rs:1907-1926): every item of its sequence and of its map
+// entries' chains (current value leftwards) gets Item::gc(parent_gc = true): a deleted one is
+// marked (and its own type's children visited); the branch is emptied.  Work stack of branches.
+__device__ void cp_gc_content(CDoc &D, uint32_t x0) {
+  const uint32_t f0 = D.I(x0, I_FLAGS);
+  if (cp_ref(f0) != 7 || (f0 & (F_DELC | F_GC)) || D.I(x0, I_SEG1) == CNIL) return;
+  uint32_t sp = 0;
+  D.wk[sp++] = D.I(x0, I_SEG1);
+  auto visit = [&](uint32_t p) {
+    uint32_t &fl = D.I(p, I_FLAGS);
+    if ((fl & F_GC) || !(fl & F_DEL)) return;
+    if (cp_ref(fl) == 7 && !(fl & F_DELC) && D.I(p, I_SEG1) != CNIL) {
+      if (sp == D.cap_i) {
+        cp_unsup(D, CU_ITEMS);
+        return;
+      }
+      D.wk[sp++] = D.I(p, I_SEG1);
+      D.I(p, I_SEG1) = CNIL; // (visited once)
+    }
+    if (!(fl & F_GCM)) {
+      fl |= F_GCM;
+      if (D.ngm < D.cap_i) D.gm[D.ngm++] = p;
+      else cp_unsup(D, CU_ITEMS);
+    }
+  };
+  while (sp && !D.st) {
+    const uint32_t b = D.wk[--sp];
+    for (uint32_t p = cp_bw(D, b, B_START), g = D.ni; p != CNIL && g; g--) {
+      const uint32_t nx = D.I(p, I_RIGHT);
+      visit(p);
+      p = nx;
+    }
+    for (uint32_t e = cp_bw(D, b, B_MAP); e != CNIL; e = D.me[ME_W * e + E_NEXT])
+      for (uint32_t p = D.me[ME_W * e + E_VAL], g = D.ni; p != CNIL && g; g--) {
+        const uint32_t nx = D.I(p, I_LEFT);
+        visit(p);
+        p = nx;
+      }
+    cp_bw(D, b, B_START) = CNIL;
+    cp_bw(D, b, B_MAP) = CNIL;
+  }
+}
 __device__ void cp_commit(CDoc &D) {
   // 1. DeleteSet squash per client: sort by (client, start), join overlapping / adjacent
   for (uint32_t i = 1; i < D.nt; i++) {
@@ -507,8 +725,10 @@ __device__ void cp_commit(CDoc &D) {
     k++;
   }
   D.nt = k;
-  // 4. GC (gc.rs:17-40): deleted content in the ranges -> Deleted(len) (root parents never GC'd)
-  for (uint32_t i = D.nt; i-- > 0;) {
+  // 4. GC (gc.rs:10-66): deleted content in the ranges -> Deleted(len); a deleted type's
+  //    descendants that are deleted are marked and become GC structs after the loop
+  D.ngm = 0;
+  for (uint32_t i = D.nt; i-- > 0 && !D.st;) {
     const int c = (int)D.tx[3 * i];
     const uint32_t rs = D.tx[3 * i + 1], re = D.tx[3 * i + 2];
     uint32_t start = rs;
@@ -517,9 +737,19 @@ __device__ void cp_commit(CDoc &D) {
       if (start > re) break;
       uint32_t &fl = D.I(x, I_FLAGS);
       if (!(fl & F_GC) && (fl & F_DEL)) { // Item::gc(collector, false)
-        fl = (fl & ~(F_OPQ | 0xF000u)) | F_DELC;
+        cp_gc_content(D, x);
+        fl = (fl & ~(F_OPQ | 0xF000u)) | F_DELC | (1u << 12);
         D.I(x, I_SEG0) = D.I(x, I_SEG1) = CNIL;
       }
+    }
+  }
+  for (uint32_t k = 0; k < D.ngm; k++) { // collect_all_marked: GC structs
+    const uint32_t x = D.gm[k];
+    uint32_t &fl = D.I(x, I_FLAGS);
+    fl &= ~F_GCM;
+    if (!(fl & F_GC) && (fl & F_DEL)) {
+      fl = F_GC | (fl & 0xFF000000u);
+      D.I(x, I_SEG0) = D.I(x, I_SEG1) = CNIL;
     }
   }
   // 5. DeleteSet::try_squash_with (id_set.rs:571-598)
@@ -579,7 +809,8 @@ struct CpSink {
   bool over; // beyond the per-update buffers: outside the device shape
   __device__ void on_section(uint32_t) {}
   __device__ int on_block(uint32_t client, uint32_t clock, const BlockInfo &bi, uint32_t bpos, uint32_t) {
-    if (bi.kind == BK_ITEM && bi.ref != 1 && bi.ref != 4 && bi.ref != 3 && bi.ref != 5 && bi.ref != 6) over = true;
+    // (Doc / Move contents are outside the device shape; WeakLink types: cp_block)
+    if (bi.kind == BK_ITEM && (bi.ref == 9 || bi.ref >= 10)) over = true;
     if (D->nub == D->mB) {
       over = true;
       return 0;
@@ -650,6 +881,33 @@ __device__ int cp_block(CDoc &D, const uint32_t *ub, uint32_t &dep) {
       return 1;
     }
   }
+  // parent info (decode_block, update.rs:444-470): named root, ID of a type item, or from the
+  // neighbours (origins present); parent_sub only with a written parent
+  uint32_t pkind = 2, pc = 0, pk = 0, pno = 0, pnl = 0, pso = 0, psl = 0; // 0 named, 1 ID, 2 unknown
+  if (info != 0 && (info & 0xC0) == 0) {
+    uint32_t pi;
+    rd_var_u32(r, pi, cn);
+    if (pi == 1) {
+      pkind = 0;
+      rd_var_u32(r, pnl, cn);
+      pno = r.i;
+      r.i += pnl;
+    } else {
+      pkind = 1;
+      rd_var_u32(r, pc, cn);
+      rd_var_u32(r, pk, cn);
+      if (pc != client && pk >= cp_clock(D, cp_cl_find(D, pc))) { // (Update::missing: the parent)
+        dep = pc;
+        return 1;
+      }
+    }
+    if (info & 0x20) {
+      rd_var_u32(r, psl, cn);
+      pso = D.uoff + r.i;
+      psl |= PS_HAS;
+      r.i += psl & PS_LEN;
+    }
+  }
   const uint32_t offset = lc - clock;
   if (!(offset == 0 || offset < len)) return 0; // already known
   if (offset > 0) { // partially known: Item::integrate with an offset (not on the device)
@@ -672,76 +930,103 @@ __device__ int cp_block(CDoc &D, const uint32_t *ub, uint32_t &dep) {
   D.I(x, I_OK) = ok;
   D.I(x, I_RC) = rc;
   D.I(x, I_RK) = rk;
-  int root = -1;
-  if ((info & 0xC0) == 0) {
-    uint32_t pi;
-    rd_var_u32(r, pi, cn);
-    if (pi != 1 || (info & 0x20)) { // ID parent / parent_sub: outside the device shape
-      cp_unsup(D, CU_PARENT);
-      return -1;
-    }
-    uint32_t nl;
-    rd_var_u32(r, nl, cn);
-    for (uint32_t q = 0; q < D.nroot && root < 0; q++)
-      if (D.m[M_ROOTLEN + q] == nl && bytes_eq(D.p + D.m[M_ROOTOFF + q], D.up + r.i, nl)) root = (int)q;
-    if (root < 0) { // Store::get_or_create_type
-      if (D.nroot == CP_MAXROOT) {
-        cp_unsup(D, CU_ROOTS);
-        return -1;
-      }
-      root = (int)D.nroot++;
-      D.m[M_ROOTOFF + root] = D.uoff + r.i;
-      D.m[M_ROOTLEN + root] = nl;
-      D.m[M_ROOTSTART + root] = CNIL;
-    }
-    r.i += nl;
-  } else if (info & 0x20) {
-    cp_unsup(D, CU_PARENT);
-    return -1;
-  }
-  if (D.st) return -1;
+  D.I(x, I_PSO) = pso;
+  D.I(x, I_PSL) = psl;
+  // content (ItemContent::decode, block.rs:1786-1835)
   const uint32_t ref = info & 15;
+  fl |= ref << 12;
   if (ref == 1) {
     fl |= F_DELC;
-  } else if (ref != 4) { // Binary (buf) / Embed (json) / Format (key, json): the content's bytes
-    const uint32_t c0 = r.i;
-    uint32_t v;
-    if (ref == 6) {
-      rd_var_u32(r, v, cn);
-      r.i += v;
-    }
-    rd_var_u32(r, v, cn);
-    r.i += v;
-    const uint32_t sg = cp_new_seg(D, D.uoff + c0, r.i - c0);
-    if (sg == CNIL) return -1;
-    D.I(x, I_SEG0) = D.I(x, I_SEG1) = sg;
-    fl |= F_OPQ | (ref << 12);
-  } else { // String: one segment over the update's bytes
+  } else if (ref == 4) { // String: one segment over the update's bytes
     uint32_t sl;
     rd_var_u32(r, sl, cn);
     const uint32_t s = cp_new_seg(D, D.uoff + r.i, sl | (sl == len ? SEG_ASCII : 0u));
     if (s == CNIL) return -1;
     D.I(x, I_SEG0) = D.I(x, I_SEG1) = s;
+  } else if (ref == 8 || ref == 2) { // Any / JSON: one run of `len` elements
+    uint32_t n;
+    rd_var_u32(r, n, cn);
+    if (ref == 2) n++; // (JSON: the count is len - 1)
+    const uint32_t s = cp_new_seg(D, D.uoff + r.i, n);
+    if (s == CNIL) return -1;
+    D.I(x, I_SEG0) = D.I(x, I_SEG1) = s;
+  } else { // Binary (buf) / Embed (json) / Format (key, json) / Type (type ref, name)
+    const uint32_t c0 = r.i;
+    uint32_t v;
+    if (ref == 7) {
+      const uint8_t tr = D.up[r.i++];
+      if (tr == 7) { // WeakLink: not on the device
+        cp_unsup(D, CU_UPDATE_SHAPE);
+        return -1;
+      }
+      if (tr == 3) {
+        rd_var_u32(r, v, cn);
+        r.i += v;
+      }
+    } else {
+      if (ref == 6) {
+        rd_var_u32(r, v, cn);
+        r.i += v;
+      }
+      rd_var_u32(r, v, cn);
+      r.i += v;
+    }
+    const uint32_t sg = cp_new_seg(D, D.uoff + c0, r.i - c0);
+    if (sg == CNIL) return -1;
+    D.I(x, I_SEG0) = sg;
+    D.I(x, I_SEG1) = CNIL; // (a Type: its branch, set by cp_integrate)
+    fl |= F_OPQ;
   }
   D.I(x, I_FLAGS) = fl;
   // Item::repair (block.rs:1287-1350)
   if (fl & F_ORIGIN) D.I(x, I_LEFT) = cp_clean_end(D, D.I(x, I_OC), D.I(x, I_OK));
   if (fl & F_RO) D.I(x, I_RIGHT) = cp_clean_start(D, D.I(x, I_RC), D.I(x, I_RK));
   if (D.st) return -1;
-  if (root < 0) { // TypePtr::Unknown: the parent of a neighbour
+  uint32_t par = CNIL;
+  if (pkind == 0) { // Store::get_or_create_type
+    for (uint32_t q = 0; q < D.nroot && par == CNIL; q++)
+      if (D.m[M_ROOTLEN + q] == pnl && bytes_eq(D.p + D.m[M_ROOTOFF + q], D.up + pno, pnl)) par = D.m[M_ROOTBR + q];
+    if (par == CNIL) {
+      if (D.nroot == CP_MAXROOT) {
+        cp_unsup(D, CU_ROOTS);
+        return -1;
+      }
+      const uint32_t q = D.nroot++;
+      par = cp_new_branch(D, CNIL, q);
+      if (par == CNIL) return -1;
+      D.m[M_ROOTOFF + q] = D.uoff + pno;
+      D.m[M_ROOTLEN + q] = pnl;
+      D.m[M_ROOTBR + q] = par;
+    }
+  } else if (pkind == 1) { // the type item's branch; Deleted content or not found: unknown
+    const uint32_t pi = cp_get_item(D, pc, pk);
+    if (pi != CNIL) {
+      const uint32_t pf = D.I(pi, I_FLAGS);
+      if (cp_ref(pf) == 7 && !(pf & F_DELC)) par = D.I(pi, I_SEG1);
+      else if (!(pf & F_DELC)) { // "parent points to a block which is not a shared type"
+        D.st = E_PANIC;
+        return -1;
+      }
+    }
+  } else { // TypePtr::Unknown: the parent (and parent_sub) of a neighbour
     const uint32_t l = D.I(x, I_LEFT), rt = D.I(x, I_RIGHT);
-    if (l != CNIL) root = (int)((D.I(l, I_FLAGS) >> 8) & 15);
-    else if (rt != CNIL) root = (int)((D.I(rt, I_FLAGS) >> 8) & 15);
+    const uint32_t src = (l != CNIL && D.I(l, I_PAR) != CNIL) ? l : (rt != CNIL && D.I(rt, I_PAR) != CNIL) ? rt : CNIL;
+    if (src != CNIL) {
+      par = D.I(src, I_PAR);
+      D.I(x, I_PSO) = D.I(src, I_PSO);
+      D.I(x, I_PSL) = D.I(src, I_PSL);
+    }
   }
-  if (root < 0) { // parent unknown: integrated as a GC struct (update.rs:239-243)
+  if (par == CNIL) { // parent unknown: integrated as a GC struct (update.rs:239-243)
     D.I(x, I_FLAGS) = F_GC | ((uint32_t)c << 24);
     D.I(x, I_SEG0) = D.I(x, I_SEG1) = CNIL;
     cp_push(D, c, x);
     return D.st ? -1 : 0;
   }
-  D.I(x, I_FLAGS) |= (uint32_t)root << 8;
-  cp_integrate(D, x);
+  D.I(x, I_PAR) = par;
+  const bool del = cp_integrate(D, x);
   cp_push(D, c, x);
+  if (del && !D.st) cp_delete(D, x);
   return D.st ? -1 : 0;
 }
 
@@ -827,6 +1112,16 @@ template <class W> __device__ void cp_opaque(const uint8_t *p, uint32_t ref, W &
   Cur c{p, 0xFFFFFFFFu, 0};
   bool cn;
   uint32_t v;
+  if (ref == 7) { // TypeRef::encode: the type ref, XmlElement's name
+    const uint8_t tr = p[0];
+    w.u8(tr);
+    if (tr == 3) {
+      c.i = 1;
+      rd_var_u32(c, v, cn);
+      w_str(w, p + c.i, v);
+    }
+    return;
+  }
   if (ref == 6) {
     rd_var_u32(c, v, cn);
     w_str(w, p + c.i, v);
@@ -869,8 +1164,10 @@ template <class W> __device__ void cp_encode(CDoc &D, W &w) {
         w_var(w, D.I(x, I_LEN));
         continue;
       }
-      const uint32_t ref = (fl & F_DELC) ? 1 : (fl & F_OPQ) ? (fl >> 12) & 15 : 4;
-      w.u8((uint8_t)(((fl & F_ORIGIN) ? 0x80 : 0) | ((fl & F_RO) ? 0x40 : 0) | ref));
+      // Item::encode (block.rs:1363-1369 info, slice.rs:199-251 with no offset)
+      const uint32_t ref = (fl & F_DELC) ? 1 : cp_ref(fl);
+      const uint32_t psl = D.I(x, I_PSL);
+      w.u8((uint8_t)(((fl & F_ORIGIN) ? 0x80 : 0) | ((fl & F_RO) ? 0x40 : 0) | ((psl & PS_HAS) ? 0x20 : 0) | ref));
       if (fl & F_ORIGIN) {
         w_var(w, D.I(x, I_OC));
         w_var(w, D.I(x, I_OK));
@@ -879,16 +1176,41 @@ template <class W> __device__ void cp_encode(CDoc &D, W &w) {
         w_var(w, D.I(x, I_RC));
         w_var(w, D.I(x, I_RK));
       }
-      if (!(fl & (F_ORIGIN | F_RO))) {
-        const uint32_t root = (fl >> 8) & 15;
-        w_var(w, 1);
-        w_str(w, D.p + D.m[M_ROOTOFF + root], D.m[M_ROOTLEN + root]);
+      if (!(fl & (F_ORIGIN | F_RO))) { // parent: a root's name, or the ID of a nested type's item
+        const uint32_t b = D.I(x, I_PAR), bi = cp_bw(D, b, B_ITEM);
+        if (bi == CNIL) {
+          const uint32_t q = cp_bw(D, b, B_ROOT);
+          w_var(w, 1);
+          w_str(w, D.p + D.m[M_ROOTOFF + q], D.m[M_ROOTLEN + q]);
+        } else {
+          w_var(w, 0);
+          w_var(w, D.m[M_CLID + D.cl_of(bi)]);
+          w_var(w, D.I(bi, I_CLOCK));
+        }
+        if (psl & PS_HAS) w_str(w, D.p + D.I(x, I_PSO), psl & PS_LEN);
       }
       if (fl & F_DELC) {
         w_var(w, D.I(x, I_LEN));
       } else if (fl & F_OPQ) {
         const uint32_t sg = D.I(x, I_SEG0);
         cp_opaque(D.p + D.sg[3 * sg], ref, w);
+      } else if (ref == 8 || ref == 2) { // element runs: Any values re-encoded, JSON strings as they are
+        w_var(w, D.I(x, I_LEN)); // (JSON too: the decoder reads count + 1 texts, the encoder writes the count)
+        for (uint32_t s = D.I(x, I_SEG0); s != CNIL; s = D.sg[3 * s + 2]) {
+          Cur c{D.p, 0xFFFFFFFFu, D.sg[3 * s]};
+          for (uint32_t q = 0; q < D.sg[3 * s + 1]; q++) {
+            if (ref == 8) {
+              bool re;
+              any_walk(c, w, re);
+            } else {
+              uint32_t v;
+              bool cn;
+              rd_var_u32(c, v, cn);
+              w_str(w, D.p + c.i, v);
+              c.i += v;
+            }
+          }
+        }
       } else {
         uint32_t tb = 0;
         for (uint32_t s = D.I(x, I_SEG0); s != CNIL; s = D.sg[3 * s + 2]) tb += D.sg[3 * s + 1] & SEG_LEN;
@@ -1021,6 +1343,12 @@ __device__ void compact_doc(const BatchIn &b, const FastOut &o, uint32_t *hdr, c
   D.ur = D.stk + D.mB;
   D.mb = D.ur + 3ull * D.mR;
   D.tx = D.mb + 4ull * D.mR + 4;
+  D.bt = D.tx + 3ull * D.cap_i;
+  D.cap_b = h[H_NB] + CP_MAXROOT + 8;
+  D.me = D.bt + (size_t)BR_W * D.cap_b;
+  D.wk = D.me + (size_t)ME_W * D.cap_i;
+  D.gm = D.wk + D.cap_i;
+  D.nbr = D.nme = D.ngm = 0;
   for (uint64_t u = u0; u < u1 && !status; u++) {
     // transaction begin: clocks before it
     for (uint32_t c = 0; c < D.ncl; c++) D.m[M_BEFORE + c] = cp_clock(D, (int)c);
