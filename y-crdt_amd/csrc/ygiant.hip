@@ -22,6 +22,7 @@
 // Documents outside the shape keep path 2 and go to the tiled kernel as before.
 #include <algorithm>
 #include "ycodec.h"
+#include "ycopy.h"
 #include "ykernels.h"
 
 namespace ym {
@@ -217,9 +218,23 @@ __device__ __forceinline__ uint32_t gs_hdr(const GsArgs &a) { // bytes of the on
   return varlen(1) + varlen(nbt) + varlen(a.g[GS_CMIN]) + varlen((uint32_t)*(const uint64_t *)(a.g + GS_FIRST));
 }
 
+// verbatim blocks of >= GS_COOP bytes are copied by the whole workgroup after its lanes' walks
+constexpr uint32_t GS_COOP = 256, GS_COOP_N = 64;
+__device__ __forceinline__ void gs_write_lane(const GsArgs &a, uint32_t i, uint32_t &s_n, uint32_t *s_l, uint64_t *s_d,
+                                              uint64_t *s_s);
 __global__ void __launch_bounds__(256) k_gs_write(GsArgs a) {
+  __shared__ uint32_t s_n, s_l[GS_COOP_N];
+  __shared__ uint64_t s_d[GS_COOP_N], s_s[GS_COOP_N];
+  if (threadIdx.x == 0) s_n = 0;
+  __syncthreads();
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= a.U) return;
+  if (i < a.U) gs_write_lane(a, i, s_n, s_l, s_d, s_s);
+  __syncthreads();
+  const uint32_t nc = s_n < GS_COOP_N ? s_n : GS_COOP_N;
+  for (uint32_t e = 0; e < nc; e++) copy_coop((uint8_t *)s_d[e], (const uint8_t *)s_s[e], s_l[e], threadIdx.x, 256);
+}
+__device__ __forceinline__ void gs_write_lane(const GsArgs &a, uint32_t i, uint32_t &s_n, uint32_t *s_l, uint64_t *s_d,
+                                              uint64_t *s_s) {
   const uint32_t clock0 = (uint32_t)*(const uint64_t *)(a.g + GS_FIRST);
   uint64_t expect = clock0 + (a.s_bl[i] & 0xFFFFFFFFu);
   uint8_t *dst = gs_out(a) + gs_hdr(a) + (a.s_bl[i] >> 32);
@@ -239,7 +254,16 @@ __global__ void __launch_bounds__(256) k_gs_write(GsArgs a) {
         if (k != expect) bad |= GSB_GAP;
         expect += len;
         const uint32_t n = meta >> 8;
-        for (uint32_t q = 0; q < n; q++) dst[q] = src[pos + q];
+        uint32_t q = GS_COOP_N;
+        if (n >= GS_COOP) q = atomicAdd(&s_n, 1u);
+        if (q < GS_COOP_N) {
+          s_d[q] = (uint64_t)dst;
+          s_s[q] = (uint64_t)(src + pos);
+          s_l[q] = n;
+        } else {
+          Writer w{dst, 0}; // (16-byte load groups: a byte loop waits one load latency per byte)
+          w.bytes(src + pos, n);
+        }
         dst += n;
       },
       [&](uint32_t, uint32_t s, uint32_t e) {

@@ -173,7 +173,7 @@ inline uint64_t lean_scratch_words(uint64_t n_updates, uint64_t n_docs, uint64_t
 void launch_fast_merge(const BatchIn &b, const FastCaps &caps, const FastOut &o, int nt, hipStream_t s);
 // one long single-client document merged by grid-wide kernels (ygiant.hip)
 constexpr uint32_t GS_LIST = 16;     // such documents per batch (the rest: tiled kernel)
-constexpr uint32_t GS_MIN_U = 65536; // updates (env YMERGE_GIANT_MIN)
+constexpr uint32_t GS_MIN_U = 8192; // updates (env YMERGE_GIANT_MIN; editing traces: 4 of 5 documents on the grid path)
 constexpr uint8_t GS_PATH = 5;       // path of a listed document until k_gs_final decides
 struct GsArgs {
   const uint8_t *bytes;

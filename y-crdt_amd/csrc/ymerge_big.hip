@@ -22,6 +22,7 @@
 // Reference semantics: yrs/src/update.rs:537-704 (merge), :490-535 (encode),
 // yrs/src/id_set.rs:129-164, 385-410 (DeleteSet union and order).
 #include "yblock.h"
+#include "ycopy.h"
 
 namespace ym {
 
@@ -1375,6 +1376,9 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
       cK = sc[1];
       cS = sc[2];
       cH += HT;
+      // pass 0 stops at the first tile with a partial overlap: overlap mode classifies every
+      // block again (pass 1), so the rest of this pass would be discarded
+      if (!om && __syncthreads_or(viol)) break;
       __syncthreads();
     }
     NC = cH;
@@ -1498,19 +1502,8 @@ __global__ void __launch_bounds__(NT, OCC) k_big_merge(BatchIn b, const uint32_t
       __syncthreads();
       {
         const uint32_t nbig = s_nbig < BIG_COPY_N ? s_nbig : BIG_COPY_N;
-        for (uint32_t e = 0; e < nbig; e++) { // 4 bytes a lane: the loads, then the stores
-          uint8_t *d = (uint8_t *)s_bd[e];
-          const uint8_t *sp = (const uint8_t *)s_bs[e];
-          const uint32_t bl = s_bl[e];
-          for (uint32_t o = 4 * t; o < bl; o += 4 * NT) {
-            const uint32_t b0 = sp[o], b1 = o + 1 < bl ? sp[o + 1] : 0, b2 = o + 2 < bl ? sp[o + 2] : 0,
-                           b3 = o + 3 < bl ? sp[o + 3] : 0;
-            d[o] = (uint8_t)b0;
-            if (o + 1 < bl) d[o + 1] = (uint8_t)b1;
-            if (o + 2 < bl) d[o + 2] = (uint8_t)b2;
-            if (o + 3 < bl) d[o + 3] = (uint8_t)b3;
-          }
-        }
+        for (uint32_t e = 0; e < nbig; e++) // 16-byte stores (ycopy.h)
+          copy_coop((uint8_t *)s_bd[e], (const uint8_t *)s_bs[e], s_bl[e], t, NT);
       }
       if (staged) {
         __syncthreads();

@@ -217,8 +217,9 @@ static bool read_words(ymerge_ctx *c, const void *d_src, size_t bytes, uint64_t 
 // bounce buffers at a fraction of PCIe.  Large transfers go through two pinned 32 MB
 // buffers instead: the host threads copy chunk k + 1 while the DMA engine moves chunk k.
 constexpr size_t STAGE_CHUNK = 32u << 20;
-static unsigned stage_threads() {
+static unsigned stage_threads() { // env YMERGE_STAGE_THREADS
   static const unsigned t = [] {
+    if (const char *v = getenv("YMERGE_STAGE_THREADS")) return (unsigned)std::max(1, atoi(v));
     const unsigned h = std::thread::hardware_concurrency();
     return h >= 16 ? 8u : (h >= 4 ? h / 2 : 1u);
   }();
@@ -1375,16 +1376,36 @@ static int host_merge_pipelined(ymerge_ctx *c, const uint8_t *bytes, const uint6
   std::atomic<size_t> recorded{0}; // groups whose ev_in the producer has recorded
   std::thread producer([&] {
     hipSetDevice(c->device);
-    size_t i = 0;
-    auto stage = [&](uint8_t *dst, const uint8_t *src, uint64_t n) {
-      for (uint64_t off = 0; off < n; off += STAGE_CHUNK, i++) {
-        const int b = (int)(i & 1);
-        const size_t len = std::min<uint64_t>(STAGE_CHUNK, n - off);
-        if (i >= 2 && hipEventSynchronize(c->stage_ev[b]) != hipSuccess) return false;
-        par_memcpy(c->stage[b], src + off, len);
-        if (hipMemcpyAsync(dst + off, c->stage[b], len, hipMemcpyHostToDevice, c->s_in) != hipSuccess ||
-            hipEventRecord(c->stage_ev[b], c->s_in) != hipSuccess)
-          return false;
+    // pieces packed into whole 32 MB pinned chunks (a group's tables and bytes share chunks;
+    // a half-empty chunk per piece left the DMA idle between pieces), flushed at group ends
+    size_t i = 0, fill = 0; // chunks issued, bytes in the current one
+    struct Piece {
+      uint8_t *dst;
+      size_t at, n;
+    };
+    std::vector<Piece> pieces;
+    auto flush = [&]() -> bool {
+      if (!fill) return true;
+      const int b = (int)(i & 1);
+      for (const Piece &q : pieces)
+        if (hipMemcpyAsync(q.dst, c->stage[b] + q.at, q.n, hipMemcpyHostToDevice, c->s_in) != hipSuccess) return false;
+      if (hipEventRecord(c->stage_ev[b], c->s_in) != hipSuccess) return false;
+      pieces.clear();
+      fill = 0;
+      i++;
+      // the next chunk's buffer must have drained (its DMA was issued two chunks ago)
+      return i < 2 || hipEventSynchronize(c->stage_ev[i & 1]) == hipSuccess;
+    };
+    auto add = [&](uint8_t *dst, const uint8_t *src, uint64_t n) -> bool {
+      while (n) {
+        const size_t take = std::min<uint64_t>(STAGE_CHUNK - fill, n);
+        par_memcpy(c->stage[i & 1] + fill, src, take);
+        pieces.push_back({dst, fill, take});
+        fill += take;
+        dst += take;
+        src += take;
+        n -= take;
+        if (fill == STAGE_CHUNK && !flush()) return false;
       }
       return true;
     };
@@ -1392,14 +1413,15 @@ static int host_merge_pipelined(ymerge_ctx *c, const uint8_t *bytes, const uint6
       const uint64_t d0 = gd[k], nd = gd[k + 1] - gd[k], u0 = doc_upd[d0], nu = doc_upd[gd[k + 1]] - u0;
       uint64_t *guo = c->in_upd_off.as<uint64_t>() + guo_off[k], *gdu = c->grp_doc_upd.as<uint64_t>() + gdu_off[k];
       const uint64_t a = upd_off[u0], z = upd_off[u0 + nu];
-      if (!stage((uint8_t *)guo, (const uint8_t *)(upd_off + u0), (nu + 1) * 8) ||
-          !stage((uint8_t *)gdu, (const uint8_t *)(doc_upd + d0), (nd + 1) * 8)) {
+      if (!add((uint8_t *)guo, (const uint8_t *)(upd_off + u0), (nu + 1) * 8) ||
+          !add((uint8_t *)gdu, (const uint8_t *)(doc_upd + d0), (nd + 1) * 8) ||
+          !add(c->in_bytes.as<uint8_t>() + a, bytes + a, z - a) || !flush()) {
         prod_rc = DEV_FAIL();
         break;
       }
       ym::launch_rebase_u64(guo, nu + 1, gbase[k], c->s_in);
       ym::launch_rebase_u64(gdu, nd + 1, u0, c->s_in);
-      if (!stage(c->in_bytes.as<uint8_t>() + a, bytes + a, z - a) || hipEventRecord(c->ev_in[k], c->s_in) != hipSuccess) {
+      if (hipEventRecord(c->ev_in[k], c->s_in) != hipSuccess) {
         prod_rc = DEV_FAIL();
         break;
       }
