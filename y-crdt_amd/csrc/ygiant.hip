@@ -221,20 +221,25 @@ __device__ __forceinline__ uint32_t gs_hdr(const GsArgs &a) { // bytes of the on
 // verbatim blocks of >= GS_COOP bytes are copied by the whole workgroup after its lanes' walks
 constexpr uint32_t GS_COOP = 256, GS_COOP_N = 64;
 __device__ __forceinline__ void gs_write_lane(const GsArgs &a, uint32_t i, uint32_t &s_n, uint32_t *s_l, uint64_t *s_d,
-                                              uint64_t *s_s);
+                                              uint64_t *s_s, uint32_t &s_nr, uint32_t *s_r0, uint32_t *s_r1);
 __global__ void __launch_bounds__(256) k_gs_write(GsArgs a) {
-  __shared__ uint32_t s_n, s_l[GS_COOP_N];
+  __shared__ uint32_t s_n, s_l[GS_COOP_N], s_nr, s_r0[GS_COOP_N], s_r1[GS_COOP_N];
   __shared__ uint64_t s_d[GS_COOP_N], s_s[GS_COOP_N];
-  if (threadIdx.x == 0) s_n = 0;
+  if (threadIdx.x == 0) s_n = s_nr = 0;
   __syncthreads();
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i < a.U) gs_write_lane(a, i, s_n, s_l, s_d, s_s);
+  if (i < a.U) gs_write_lane(a, i, s_n, s_l, s_d, s_s, s_nr, s_r0, s_r1);
   __syncthreads();
   const uint32_t nc = s_n < GS_COOP_N ? s_n : GS_COOP_N;
   for (uint32_t e = 0; e < nc; e++) copy_coop((uint8_t *)s_d[e], (const uint8_t *)s_s[e], s_l[e], threadIdx.x, 256);
+  // whole bitmap words of long deleted ranges (every bit set: plain stores are exact against
+  // the other lanes' atomic ORs); one lane ORing a 60k-clock delete word by word took 0.5 ms
+  const uint32_t nr = s_nr < GS_COOP_N ? s_nr : GS_COOP_N;
+  for (uint32_t e = 0; e < nr; e++)
+    for (uint32_t q = s_r0[e] + threadIdx.x; q < s_r1[e]; q += 256) a.bm[q] = 0xFFFFFFFFu;
 }
 __device__ __forceinline__ void gs_write_lane(const GsArgs &a, uint32_t i, uint32_t &s_n, uint32_t *s_l, uint64_t *s_d,
-                                              uint64_t *s_s) {
+                                              uint64_t *s_s, uint32_t &s_nr, uint32_t *s_r0, uint32_t *s_r1) {
   const uint32_t clock0 = (uint32_t)*(const uint64_t *)(a.g + GS_FIRST);
   uint64_t expect = clock0 + (a.s_bl[i] & 0xFFFFFFFFu);
   uint8_t *dst = gs_out(a) + gs_hdr(a) + (a.s_bl[i] >> 32);
@@ -280,7 +285,14 @@ __device__ __forceinline__ void gs_write_lane(const GsArgs &a, uint32_t i, uint3
           atomicOr(&a.bm[w0], m0 & m1);
         } else {
           atomicOr(&a.bm[w0], m0);
-          for (uint32_t q = w0 + 1; q < w1; q++) atomicOr(&a.bm[q], 0xFFFFFFFFu);
+          uint32_t q = GS_COOP_N;
+          if (w1 - w0 > 64) q = atomicAdd(&s_nr, 1u);
+          if (q < GS_COOP_N) { // the workgroup fills the whole words after the walks
+            s_r0[q] = w0 + 1;
+            s_r1[q] = w1;
+          } else {
+            for (uint32_t z = w0 + 1; z < w1; z++) a.bm[z] = 0xFFFFFFFFu;
+          }
           atomicOr(&a.bm[w1], m1);
         }
       });

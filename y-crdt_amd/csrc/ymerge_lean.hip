@@ -43,10 +43,13 @@ constexpr uint32_t LN_AW = 1280;             // arena words: block records grow 
 constexpr uint32_t LN_BUF = LN_SW + LN_AW;   // stage + arena, reused whole by the DeleteSet phase
 constexpr uint32_t LN_NBK = 16;              // client buckets per document
 constexpr uint32_t LN_MAXBLEN = 1024;        // block bytes (a copy step must always fit one block)
+constexpr uint32_t LN_DSMAXI = 252;          // bytes of one update's DeleteSet
+constexpr uint32_t LN_DSW = 1024;            // DeleteSet batch window: 16 staged bytes per lane
 constexpr uint32_t LN_ORD = 7 * LN_NBK;      // DeleteSet client order scratch (end of buf, after the scatter):
                                              // order, hash slots (2x) + copy, clients, entry offsets
 constexpr uint32_t LN_NONE = 0xFFFFFFFFu;
-constexpr uint32_t LN_UMAX = 32768;          // BIG documents: above, the tiled kernel is faster per document
+constexpr uint32_t LN_UMAX = 16384;          // BIG documents: above, the grid path / tiled kernel (a 20k-update
+                                             // trace document held one wave 0.43 ms before a hand-over)
 
 // buf = [stage | arena]: block records (src | blen << 16 | bucket << 27) from the arena
 // bottom; from the top, one word per DeleteSet item: its end offset in the document's DS
@@ -361,9 +364,7 @@ __device__ __noinline__ uint32_t lean_ds_order(uint32_t nbk, const uint32_t *cli
 // [0, 2U), DeleteSet item ends at [2U, 3U), the DeleteSet bitmap from 3U, component starts /
 // ends after it.  LDS then holds only the stage and the DeleteSet batch.
 template <bool BIG, bool STAMPS>
-// Returns true when an LDS-mode document filled the arena: nothing was written, the caller runs
-// it again in BIG mode (when the scratch exists); every other outcome is written here.
-__device__ __forceinline__ bool lean_doc(const BatchIn &b, const FastOut &o, LeanLds &L, const uint32_t d,
+__device__ __forceinline__ void lean_doc(const BatchIn &b, const FastOut &o, LeanLds &L, const uint32_t d,
                                          const uint32_t lane, uint32_t *const scr) {
   uint64_t tst[16];
   auto stamp = [&](int k) {
@@ -391,11 +392,12 @@ __device__ __forceinline__ bool lean_doc(const BatchIn &b, const FastOut &o, Lea
   };
   if (U == 0 || (!BIG && (B1 - B0 >= 65536 || U > LN_AW))) {
     reject(0);
-    return false;
+    return;
   }
   // this document's HBM scratch (every document has one when scr is set; BIG documents
   // keep all their tables there, the others only component lists that outgrow LDS)
   uint32_t *const hs = scr ? scr + 4 * u0 + 64ull * d + B0 : nullptr;
+  auto item_end = [&](uint32_t j) -> uint32_t { return BIG ? hs[2 * U + j] : L.buf[LN_BUF - 1 - j]; };
   if (lane < LN_NBK) {
     L.bytes[lane] = 0;
     L.dsfirst[lane] = LN_NONE;
@@ -403,7 +405,11 @@ __device__ __forceinline__ bool lean_doc(const BatchIn &b, const FastOut &o, Lea
   wsync();
 
   // ---------------------------------------------------------------- 1 decode
-  uint32_t nbk = 0, NBk = 0, NRg = 0, blkmask = 0; // buckets, block records, DeleteSet range records
+  uint32_t nbk = 0, NBk = 0, NI = 0, blkmask = 0;
+  // DeleteSet scratch: the upper half of this document's output slot (capacity 2 x input +
+  // 64; a lean document's output is at most its input + 10 bytes), DSB bytes used
+  uint8_t *const dscr = out + (B1 - B0) + 64;
+  uint32_t DSB = 0;
   // per bucket (lane = bucket): client, first / next clock, block count
   uint32_t tabc = 0, bfirst = 0, bnext = 0, bcnt = 0;
   uint32_t bad = 0; // why + 1
@@ -420,7 +426,7 @@ __device__ __forceinline__ bool lean_doc(const BatchIn &b, const FastOut &o, Lea
     k = lead_ones(fm);
     if (k == 0) {
       reject(1);
-      return false;
+      return;
     }
     E = rdlane64(e, k - 1);
     n16 = (uint32_t)((E - al + 15) >> 4);
@@ -483,7 +489,7 @@ __device__ __forceinline__ bool lean_doc(const BatchIn &b, const FastOut &o, Lea
     }
     const uint64_t mall = __ballot(hb);
     const uint32_t nbr = (uint32_t)__builtin_popcountll(mall);
-    if (!BIG && NBk + nbr + NRg > LN_AW) { // arena full: not lean
+    if (!BIG && NBk + nbr + NI > LN_AW) { // arena full: not lean
       bad = 5;
       break;
     }
@@ -533,94 +539,31 @@ __device__ __forceinline__ bool lean_doc(const BatchIn &b, const FastOut &o, Lea
     }
     acc(10, tr2);
     const uint64_t tr3 = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
-    // DeleteSets (IdSet::decode, id_set.rs:412-426), parsed here by their lanes: entries of
-    // distinct clients that own blocks, every range non-empty and not below its client's first
-    // clock; each range becomes records at the arena top (LDS: rel << 15 | (len - 1) << 4 |
-    // bucket, rel = start - the bucket's first clock < 2^17, a range longer than 2048 clocks
-    // cut into pieces of 2048 -- the union is the same; BIG: one record of two words in the
-    // scratch), scattered into the union's bitmap by phase 4; the entries' first-occurrence
-    // keys (update << 8 | table position) go to dsfirst now
+    // DeleteSets: item bytes verbatim to the HBM scratch (input order), end offsets to the
+    // arena top; decoded in a few large batches by phase 4
     {
       const bool hd = act && r.nent > 0;
-      if (__ballot(hd)) {
-        const uint32_t end = (uint32_t)(e - al);
-        uint32_t p = r.dspos + (hd ? var_at(L.buf, r.dspos, end).n : 0u);
-        bool dok = true, full = false;
-        uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
-        int b0k = 0, b1k = 0, b2k = 0, b3k = 0;
-#pragma unroll
-        for (uint32_t en = 0; en < 4; en++) {
-          bool ae = hd && en < r.nent;
-          if (!__ballot(ae)) break;
-          uint32_t cv = 0, nr = 0;
-          if (ae) {
-            const VarR vc = var_at(L.buf, p, end), vn = var_at(L.buf, p + vc.n, end);
-            cv = vc.v;
-            nr = vn.v;
-            p += vc.n + vn.n;
-            dok = dok && vc.fine && vn.fine && nr >= 1 && nr <= end - p && !(en > 0 && c0 == cv) &&
-                  !(en > 1 && c1 == cv) && !(en > 2 && c2 == cv);
-          }
-          // the entry's client must own blocks already (its bucket's first clock)
-          const int bq = ae ? tab_find(tabc, nbk, cv) : 0;
-          ae = ae && dok;
-          dok = dok && (!ae || (bq >= 0 && ((blkmask >> (bq & 31)) & 1)));
-          ae = ae && dok;
-          const uint32_t bqq = (uint32_t)(bq < 0 ? 0 : bq) & 63;
-          const uint32_t f0 = shfl(bfirst, (int)bqq);
-          if (en == 0) { c0 = cv; b0k = bq; }
-          else if (en == 1) { c1 = cv; b1k = bq; }
-          else if (en == 2) { c2 = cv; b2k = bq; }
-          else { c3 = cv; b3k = bq; }
-          for (uint32_t t = 0;; t++) {
-            bool ar = ae && t < nr;
-            if (!__ballot(ar)) break;
-            uint32_t a = 0, l = 0;
-            if (ar) {
-              const VarR va = var_at(L.buf, p, end), vl = var_at(L.buf, p + va.n, end);
-              a = va.v;
-              l = vl.v;
-              p += va.n + vl.n;
-              const bool fit = BIG ? l < (1u << 27) : (uint64_t)(a - f0) + l <= (1u << 17);
-              dok = dok && va.fine && vl.fine && l != 0 && a >= f0 && (uint64_t)a + l <= 0xFFFFFFFFull && fit;
-              ar = dok;
-            }
-            const uint32_t k = ar ? (BIG ? 1u : (l + 2047) >> 11) : 0u; // records of this range
-            const uint32_t kinc = wincl(k, lane), ktot = rdlane(kinc, 63);
-            if (!BIG && NBk + NRg + ktot > LN_AW) {
-              full = true; // arena full: BIG mode (below)
-              dok = false;
-              break;
-            }
-            if (ar) {
-              const uint32_t ri = NRg + kinc - k;
-              if (BIG) {
-                hs[2 * U + 2 * ri] = a;
-                hs[2 * U + 2 * ri + 1] = l | (bqq << 27);
-              } else {
-                for (uint32_t q = 0; q < k; q++) {
-                  const uint32_t pl = l - 2048 * q < 2048 ? l - 2048 * q : 2048;
-                  L.buf[LN_BUF - 1 - (ri + q)] = ((a + 2048 * q - f0) << 15) | ((pl - 1) << 4) | bqq;
-                }
-              }
-            }
-            NRg += ktot;
-          }
+      const uint32_t ilen = hd ? (uint32_t)(e - al) - r.dspos : 0;
+      const uint64_t hm = __ballot(hd);
+      if (hm) {
+        const uint32_t binc = wincl(ilen, lane), btot = rdlane(binc, 63);
+        const uint32_t nit = (uint32_t)__builtin_popcountll(hm);
+        if (__ballot(ilen > LN_DSMAXI)) {
+          bad = 3;
+          break;
         }
-        dok = dok && (!hd || p == end); // nothing after the DeleteSet (trailing bytes: not lean)
-        if (__ballot(hd && !dok)) {
-          bad = full ? 5 : 7;
+        if (!BIG && NBk + NI + nit > LN_AW) {
+          bad = 5;
           break;
         }
         if (hd) {
-          uint32_t p0 = 0, p1 = 1, p2 = 2, p3 = 3;
-          const uint32_t ne = r.nent;
-          if (ne >= 2) ds_pos4(ne, c0, c1, c2, c3, p0, p1, p2, p3);
-          atomicMin(&L.dsfirst[b0k], (i << 8) | p0);
-          if (ne > 1) atomicMin(&L.dsfirst[b1k], (i << 8) | p1);
-          if (ne > 2) atomicMin(&L.dsfirst[b2k], (i << 8) | p2);
-          if (ne > 3) atomicMin(&L.dsfirst[b3k], (i << 8) | p3);
+          copy_out(L.buf, r.dspos, dscr + DSB + binc - ilen, ilen);
+          const uint32_t ii = NI + lanes_below(hm);
+          if (BIG) hs[2 * U + ii] = DSB + binc;
+          else L.buf[LN_BUF - 1 - ii] = DSB + binc;
         }
+        NI += nit;
+        DSB += btot;
       }
     }
     acc(11, tr3);
@@ -642,9 +585,8 @@ __device__ __forceinline__ bool lean_doc(const BatchIn &b, const FastOut &o, Lea
     wsync();
   }
   if (bad) {
-    if (!BIG && bad == 5 && scr && U <= LN_UMAX && B1 - B0 < (1ull << 31)) return true; // (arena)
     reject(bad - 1);
-    return false;
+    return;
   }
   wsync();
   stamp(2);
@@ -674,16 +616,18 @@ __device__ __forceinline__ bool lean_doc(const BatchIn &b, const FastOut &o, Lea
   const uint32_t dbase = hasb ? fst & ~31u : 0;
   const uint32_t words = hasb ? ((bnx - 1) >> 5) - (dbase >> 5) + 1 : 0;
   const uint32_t win = wincl(words, lane), W = rdlane(win, 63), woff = win - words;
-  const uint32_t Wr = (W + 3) & ~3u;
-  // The bitmap goes to LDS from word 0 when it stays below the range records at the arena top;
-  // else (and for BIG documents) to the HBM scratch after the records' words [2U, 2U + 2 NRg)
-  // (capacity 4U + 64 + bytes).  The component lists go after the bitmap in LDS, else to the
-  // records' words of the scratch (2 per range; the records are consumed by then)
-  const uint32_t nb_in = (uint32_t)(B1 - B0);
-  const bool bmg = BIG || Wr + NRg > LN_BUF;
-  if (bmg && (!hs || (uint64_t)Wr + 2ull * NRg > 2ull * U + 64 + nb_in)) {
+  const uint32_t Wr = (W + 3) & ~3u; // staging after the bitmap, 16-byte aligned
+  // DS batches need the bitmap, a staging window and its decoded varints below the item ends.
+  // The bitmap goes to the HBM scratch ([3U, 3U + Wr), then the component lists: 2 NR <= DSB
+  // words, within the scratch's last U + 64 + bytes words) for BIG documents and whenever
+  // it would leave no room for one batch of the largest item.
+  const bool bmg = BIG || Wr + LN_DSW / 4 + 8 + LN_DSMAXI + NI > LN_BUF;
+  const uint32_t lds_used = (BIG ? 0 : NI) + (bmg ? 0 : Wr);
+  const uint32_t dsavail = LN_BUF - lds_used > LN_DSW / 4 + 8 ? LN_BUF - lds_used - (LN_DSW / 4 + 8) : 0;
+  const uint32_t dslim = dsavail < LN_DSW - 16 ? dsavail : LN_DSW - 16; // batch bytes (<= varints)
+  if ((NI && dslim < LN_DSMAXI) || (bmg && (!hs || (uint64_t)Wr + DSB > U + 64 + (B1 - B0)))) {
     reject(6);
-    return false;
+    return;
   }
   // section headers (count, client, first clock: update.rs encode_diff :490-535) and NC
   if (lane == 0) {
@@ -759,55 +703,155 @@ __device__ __forceinline__ bool lean_doc(const BatchIn &b, const FastOut &o, Lea
 
   stamp(4);
   // ---------------------------------------------------------------- 4 DeleteSet
-  // The range records of phase 1 go into the bitmap (IdSet::merge + squash = union,
-  // id_set.rs:129-164, 385-395), a lane per record; a range past its client's last clock is
-  // not lean (the window)
-  uint32_t *const bmp = bmg ? hs + 2 * U + 2 * NRg : L.buf;
+  // IdSet::decode of every item (id_set.rs:412-426) in batches of whole items staged from the
+  // HBM scratch; ranges go straight into the bitmap (IdSet::merge + squash = union,
+  // id_set.rs:129-164, 385-395); first-occurrence keys give the union's client order.
+  uint32_t *const bmp = bmg ? hs + 3 * U : L.buf;
   for (uint32_t q = lane; q < W; q += 64) bmp[q] = 0;
   // the wave's scratch stores must be visible to its own loads below
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
   wsync();
-  const uint32_t NR = NRg; // ranges (bound the components)
+  uint32_t *const stg = bmg ? L.buf : L.buf + Wr, *const dsv = stg + LN_DSW / 4 + 8;
+  uint32_t NR = 0; // ranges (bound the components)
   {
     const uint64_t tp0 = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
-    bool wok = true;
-    for (uint32_t j0 = 0; j0 < NRg; j0 += 64) {
+    uint32_t i0 = 0, s0 = 0;
+    uint32_t dbad = 0; // why + 1
+    while (i0 < NI && !dbad) {
       if (STAMPS) tst[14]++;
-      const uint32_t j = j0 + lane;
-      const bool v = j < NRg;
-      uint32_t a = 0, l = 0, bq = 0;
-      if (v) {
-        if (BIG) {
-          a = hs[2 * U + 2 * j];
-          const uint32_t w1 = hs[2 * U + 2 * j + 1];
-          l = w1 & 0x7FFFFFFu;
-          bq = w1 >> 27;
-        } else {
-          const uint32_t rec = L.buf[LN_BUF - 1 - j];
-          a = rec >> 15; // (relative to the bucket's first clock)
-          l = ((rec >> 4) & 2047) + 1;
-          bq = rec & 15;
-        }
+      // items [i0, i1) with their bytes [s0, s1) <= dslim (item ends are ascending)
+      uint32_t i1 = i0;
+      for (;;) {
+        const uint32_t j = i1 + lane;
+        const uint64_t fm = __ballot(j < NI && item_end(j) - s0 <= dslim);
+        const uint32_t kf = lead_ones(fm);
+        i1 += kf;
+        if (kf < 64) break;
       }
-      // (every lane takes part in the shuffles)
-      const uint32_t f0 = shfl(fst, (int)bq), bn = shfl(bnx, (int)bq), wo = shfl(woff, (int)bq);
-      const uint32_t rel = BIG ? a - f0 : a;
-      const bool in = (uint64_t)f0 + rel + l <= bn;
-      wok = wok && (!v || in);
-      if (v && in) {
-        uint32_t x = (f0 & 31) + rel;
-        const uint32_t z = x + l;
-        while (x < z) {
-          const uint32_t wi = x >> 5, bo = x & 31, nb = (z - x < 32 - bo) ? z - x : 32 - bo;
-          atomicOr(&bmp[wo + wi], (nb == 32 ? 0xFFFFFFFFu : ((1u << nb) - 1)) << bo);
-          x += nb;
-        }
+      const uint32_t s1 = item_end(i1 - 1);
+      const uint64_t ga = (uint64_t)(uintptr_t)(dscr + s0), ga16 = ga & ~15ull;
+      const uint32_t so = (uint32_t)(ga - ga16), send = so + (s1 - s0);
+      {
+        uint4 d0 = make_uint4(0, 0, 0, 0), d1 = d0;
+        const uint32_t n16 = (send + 15) >> 4;
+        stage_load((const uint8_t *)(uintptr_t)ga16, 0, n16, lane, d0, d1);
+        stage_store(stg, n16, lane, d0, d1);
       }
+      wsync();
+      // 1 terminators (bit 7 clear) of bytes [16 lane, 16 lane + 16) within [so, send); a
+      // varint starts at so and after every terminator; its index = terminators before it
+      const uint32_t b0 = 16 * lane;
+      const uint32_t lo = so > b0 ? so - b0 : 0, hi = send > b0 ? send - b0 : 0;
+      const uint32_t vmask = (hi >= 16 ? 0xFFFFu : (1u << hi) - 1) & ~(lo >= 16 ? 0xFFFFu : (1u << lo) - 1);
+      uint32_t tm = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++) {
+        const uint32_t t = ~stg[4 * lane + q] & 0x80808080u;
+        tm |= (((t >> 7) & 1) | ((t >> 14) & 2) | ((t >> 21) & 4) | ((t >> 28) & 8)) << (4 * q);
+      }
+      tm &= vmask;
+      const uint32_t ns = (uint32_t)__builtin_popcount(tm);
+      const uint32_t ginc = wincl(ns, lane), gbase = ginc - ns;
+      const uint32_t tprev = shfl(tm, lane ? (int)lane - 1 : 0);
+      uint32_t sm = ((tm << 1) | (lane == 0 ? 1u << so : (tprev >> 15) & 1)) & vmask; // lane 0: the batch's first byte
+      bool vok = true;
+      while (sm) {
+        const uint32_t kb = (uint32_t)__builtin_ctz(sm);
+        const VarR r = var_at(stg, b0 + kb, send);
+        vok = vok && r.fine;
+        dsv[gbase + (uint32_t)__builtin_popcount(tm & ((1u << kb) - 1))] = r.v;
+        sm &= sm - 1;
+      }
+      if (__ballot(!vok)) {
+        dbad = 4;
+        break;
+      }
+      wsync();
+      // 2 one lane per item, groups of 64; entries in lockstep (uniform loop)
+      for (uint32_t g0i = i0; g0i < i1 && !dbad; g0i += 64) {
+        const uint32_t it = g0i + lane;
+        const bool iv = it < i1;
+        const uint32_t ist = iv ? (it ? item_end(it - 1) : 0) - s0 + so : so;
+        const uint32_t ien = iv ? item_end(it) - s0 + so : so + 1;
+        const uint32_t ja = ist >> 4, jz = (ien - 1) >> 4;
+        const uint32_t gba = shfl(gbase, (int)(ja & 63)), tma = shfl(tm, (int)(ja & 63));
+        const uint32_t gbz = shfl(gbase, (int)(jz & 63)), tmz = shfl(tm, (int)(jz & 63));
+        const uint32_t g0 = gba + (uint32_t)__builtin_popcount(tma & ((1u << (ist & 15)) - 1));
+        const uint32_t zb = (ien - 1) & 15;
+        const uint32_t gend = gbz + (uint32_t)__builtin_popcount(tmz & ((2u << zb) - 1));
+        bool ok = !iv || ((tmz >> zb) & 1); // the item's last byte ends a varint
+        const uint32_t nds = iv ? dsv[g0] : 0;
+        ok = ok && (!iv || (nds >= 1 && nds <= 4 && g0 < gend));
+        const uint32_t nent = iv && ok ? nds : 0;
+        uint32_t g = g0 + 1, nrec = 0;
+        uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+        int b0k = 0, b1k = 0, b2k = 0, b3k = 0;
+#pragma unroll
+        for (uint32_t e = 0; e < 4; e++) {
+          bool ae = ok && e < nent;
+          if (!__ballot(ae)) break;
+          uint32_t cv = 0, nr = 0;
+          if (ae) {
+            ae = g + 2 <= gend;
+            if (ae) {
+              cv = dsv[g];
+              nr = dsv[g + 1];
+              ae = nr >= 1 && nr <= ien - ist && g + 2 + 2 * nr <= gend && !(e > 0 && c0 == cv) &&
+                   !(e > 1 && c1 == cv) && !(e > 2 && c2 == cv);
+            }
+          }
+          // the entry's client must own blocks here (its window): else not lean
+          const int bq = ae ? tab_find(tabc, nbk, cv) : 0;
+          ae = ae && bq >= 0 && ((blkmask >> (bq & 31)) & 1);
+          const uint32_t bqq = (uint32_t)(bq < 0 ? 0 : bq) & 63;
+          const uint32_t f0 = shfl(fst, (int)bqq), bn = shfl(bnx, (int)bqq);
+          const uint32_t wo = shfl(woff, (int)bqq), bs = shfl(dbase, (int)bqq);
+          if (e == 0) { c0 = cv; b0k = bq; }
+          else if (e == 1) { c1 = cv; b1k = bq; }
+          else if (e == 2) { c2 = cv; b2k = bq; }
+          else { c3 = cv; b3k = bq; }
+          if (ae) {
+            for (uint32_t t = 0; t < nr && ae; t++) {
+              const uint32_t a = dsv[g + 2 + 2 * t], l = dsv[g + 3 + 2 * t];
+              ae = l != 0 && a >= f0 && (uint64_t)a + l <= bn;
+              if (!ae) break;
+              uint32_t x = a - bs;
+              const uint32_t z = x + l;
+              while (x < z) {
+                const uint32_t wi = x >> 5, bo = x & 31, nb = (z - x < 32 - bo) ? z - x : 32 - bo;
+                const uint32_t mask = (nb == 32 ? 0xFFFFFFFFu : ((1u << nb) - 1)) << bo;
+                atomicOr(&bmp[wo + wi], mask);
+                x += nb;
+              }
+            }
+            nrec += nr;
+            g += 2 + 2 * nr;
+          }
+          if (e < nent) ok = ae;
+        }
+        ok = ok && (!iv || g == gend); // no varints after the DeleteSet (trailing bytes: not lean)
+        if (__ballot(iv && !ok)) {
+          dbad = 7; // window (a range outside its client's blocks) or malformed: hand over
+          break;
+        }
+        if (iv) {
+          uint32_t p0 = 0, p1 = 1, p2 = 2, p3 = 3;
+          if (nent >= 2) ds_pos4(nent, c0, c1, c2, c3, p0, p1, p2, p3);
+          atomicMin(&L.dsfirst[b0k], (it << 8) | p0);
+          if (nent > 1) atomicMin(&L.dsfirst[b1k], (it << 8) | p1);
+          if (nent > 2) atomicMin(&L.dsfirst[b2k], (it << 8) | p2);
+          if (nent > 3) atomicMin(&L.dsfirst[b3k], (it << 8) | p3);
+        }
+        NR += rdlane(wincl(nrec, lane), 63);
+      }
+      wsync();
+      i0 = i1;
+      s0 = s1;
     }
     acc(13, tp0);
-    if (__ballot(!wok)) {
-      reject(6);
-      return false;
+    if (dbad) {
+      reject(dbad - 1);
+      return;
     }
   }
   const uint32_t dsf = lb ? L.dsfirst[lane] : LN_NONE;
@@ -818,14 +862,14 @@ __device__ __forceinline__ bool lean_doc(const BatchIn &b, const FastOut &o, Lea
   const bool cg = bmg || W + 2 * NR + LN_ORD > LN_BUF;
   if (cg && !hs) {
     reject(6);
-    return false;
+    return;
   }
   if (bmg) { // the bitmap's global atomics complete before the component scan reads it
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
     wsync();
   }
   // runs -> components: cst[c] / cen[c] per bucket in bucket-index order
-  uint32_t *const cst = cg ? hs + 2 * U : L.buf + W, *const cen = cst + NR;
+  uint32_t *const cst = cg ? hs + 3 * U + (bmg ? Wr : 0) : L.buf + W, *const cen = cst + NR;
   uint32_t ncomp = 0, cbase = 0, NCD = 0;
   for (uint32_t q = 0; q < nbk; q++) {
     const uint32_t wc = rdlane(words, q);
@@ -942,7 +986,6 @@ __device__ __forceinline__ bool lean_doc(const BatchIn &b, const FastOut &o, Lea
     tst[15] = 0x1EA4;
     for (int q = 0; q < 16; q++) o.stamps[(size_t)d * 16 + q] = tst[q];
   }
-  return false;
 }
 
 template <int WPB, int OCC, bool STAMPS>
@@ -958,8 +1001,8 @@ __global__ void __launch_bounds__(64 * WPB, OCC) k_lean(BatchIn b, FastOut o, ui
   const uint64_t nb = b.upd_off[u1] - b.upd_off[u0];
   if (scr && (u1 - u0 > LN_AW || nb >= 65536) && u1 - u0 <= LN_UMAX && nb < (1ull << 31))
     lean_doc<true, STAMPS>(b, o, lds[w], d, lane, scr);
-  else if (lean_doc<false, STAMPS>(b, o, lds[w], d, lane, scr)) // the LDS arena filled up
-    lean_doc<true, STAMPS>(b, o, lds[w], d, lane, scr);
+  else
+    lean_doc<false, STAMPS>(b, o, lds[w], d, lane, scr);
 }
 
 // update-count classes of the dispatch order (longest first)
