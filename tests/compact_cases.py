@@ -78,7 +78,7 @@ def fixture_reason(name):
 
 
 def edge_docs():
-    """Small hand-built documents: empty, malformed, KAT-style, nine clients, a split inside a
+    """Small hand-built documents: empty, malformed, KAT-style, 10 / 16 / 17 clients, a split inside a
     surrogate pair, a Skip block, a delete of a client the store has never seen."""
     t = var(1) + vstr("t")
 
@@ -101,11 +101,12 @@ def edge_docs():
                  b"\x00" + var(1) + var(1) + var(1) + var(2) + var(5)]); reasons.append(0)
     # a delete set for a client with no blocks: dropped (transaction.rs:474-476)
     docs.append([upd(1, 0, [s_root("ab")]), b"\x00" + var(1) + var(9) + var(1) + var(0) + var(1)]); reasons.append(0)
-    # nine clients
-    ups = [upd(1, 0, [s_root("a")])]
-    for c in range(2, 11):
-        ups.append(upd(c, 0, [s_after(c - 1, 0, "x")]))
-    docs.append(ups); reasons.append(CU["CLIENTS"])
+    # ten clients (on the device since round 6), sixteen (the most), seventeen (refused)
+    for ncl, why in ((10, 0), (16, 0), (17, CU["CLIENTS"])):
+        ups = [upd(1, 0, [s_root("a")])]
+        for c in range(2, ncl + 1):
+            ups.append(upd(c, 0, [s_after(c - 1, 0, "x")]))
+        docs.append(ups); reasons.append(why)
     # a split inside a surrogate pair (yrs keeps the pair on the left)
     docs.append([upd(1, 0, [s_root("a\U0001F600b")]), upd(2, 0, [s_after(1, 1, "z")])]); reasons.append(CU["SURROGATE"])
     # Skip block inside an update
@@ -331,7 +332,7 @@ def exhibits(updates, reason):
     if reason == CU["CLIENTS"]:
         cls = {b["client"] for bl, _ in parsed for b in bl}
         cls_ds = cls | {c for _, ds in parsed for c, _ in ds}
-        return len(cls) > 8 or len(cls_ds) > 8
+        return len(cls) > 16 or len(cls_ds) > 16  # ycompact.hip CP_MAXCL
     if reason == CU["PARENT"]:
         return any(b["id_parent"] is not None or b["psub"] for bl, _ in parsed for b in bl)
     if reason == CU["UPDATE_SHAPE"]:

@@ -92,8 +92,11 @@ def test_editing_traces(emu, oracle, name):
     check(emu, oracle, b)
 
 
-def test_more_than_eight_clients(emu, oracle):
-    st, why = check(emu, oracle, workloads.text_docs(40, 400, seed=5, max_clients=12), reasons=None, min_device=0.3)
+def test_many_clients(emu, oracle):
+    """up to CP_MAXCL = 16 clients on the device; documents with more are refused (CU_CLIENTS)"""
+    check(emu, oracle, workloads.text_docs(40, 400, seed=5, min_clients=9, max_clients=16))
+    st, why = check(emu, oracle, workloads.text_docs(40, 400, seed=6, min_clients=9, max_clients=24), reasons=None,
+                    min_device=0.2)
     assert set(why[st == 21].tolist()) <= {CU["CLIENTS"]}
 
 

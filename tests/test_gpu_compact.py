@@ -72,8 +72,11 @@ def test_fixtures_and_edges(engine, emu, oracle):
 
 
 def test_mixed_shapes_and_pending(engine, emu, oracle):
-    """Nine-plus clients and withheld updates interleaved with ordinary documents."""
-    check_gpu(engine, emu, oracle, workloads.text_docs(100, 300, seed=5, max_clients=12), min_device=0.3)
+    """9-16 clients (on the device), 17-24 (refused) and withheld updates interleaved with
+    ordinary documents."""
+    check_gpu(engine, emu, oracle, workloads.text_docs(100, 300, seed=5, min_clients=9, max_clients=16))
+    check_gpu(engine, emu, oracle, workloads.text_docs(100, 300, seed=6, min_clients=9, max_clients=24),
+              min_device=0.2)
     check_gpu(engine, emu, oracle, workloads.delete_heavy_docs(16, 1000), min_device=0.0)
 
 

@@ -31,9 +31,9 @@
 
 namespace ym {
 
-constexpr uint32_t CP_MAXCL = 8, CP_MAXROOT = 8;
+constexpr uint32_t CP_MAXCL = 16, CP_MAXROOT = 8;
 constexpr uint32_t CP_STAGE = 256; // per-lane LDS copy of the current update (bytes)
-constexpr uint32_t CP_IS = 16, CP_IN = 64; // arrival index: one sample per 16 arrivals, 64 samples
+constexpr uint32_t CP_IS = 32, CP_IN = 28; // arrival index: one sample per 32 arrivals, 28 samples
 constexpr uint32_t CP_LANES = 16;          // documents per wavefront at most (LDS sized for them)
 constexpr uint32_t CNIL = 0xFFFFFFFFu;
 // item words
@@ -69,31 +69,32 @@ constexpr uint32_t F_ORIGIN = 1, F_RO = 2, F_DEL = 4, F_DELC = 8, F_GC = 16, F_O
 __host__ __device__ inline uint32_t cp_ref(uint32_t fl) { return (fl >> 12) & 15; }
 // misc area layout (words)
 enum : uint32_t {
-  M_CLID = 0,                      // client ids [8]
-  M_HEAD = M_CLID + CP_MAXCL,      // first item in clock order [8]
-  M_TAIL = M_HEAD + CP_MAXCL,      // last item [8]
-  M_NBLK = M_TAIL + CP_MAXCL,      // arrived blocks [8]
-  M_BEFORE = M_NBLK + CP_MAXCL,    // clock before the transaction [8]
+  M_CLID = 0,                      // client ids [CP_MAXCL]
+  M_HEAD = M_CLID + CP_MAXCL,      // first item in clock order 
+  M_TAIL = M_HEAD + CP_MAXCL,      // last item 
+  M_NBLK = M_TAIL + CP_MAXCL,      // arrived blocks 
+  M_BEFORE = M_NBLK + CP_MAXCL,    // clock before the transaction 
   M_ROOTOFF = M_BEFORE + CP_MAXCL, // root name byte offset [4]
   M_ROOTLEN = M_ROOTOFF + CP_MAXROOT,
   M_ROOTBR = M_ROOTLEN + CP_MAXROOT, // its branch
   M_CBK = M_ROOTBR + CP_MAXROOT,     // client -> its arrival array (index into the count header)
   M_UE = M_CBK + CP_MAXCL,          // update DS entry clients [16] (table order)
   M_UEN = M_UE + 16,               // ranges per entry [16]
-  M_HCL = M_UEN + 16,               // the count header's block clients [8]
-  M_HCN = M_HCL + CP_MAXCL,         // their block counts (arrival capacities) [8]
-  M_HCO = M_HCN + CP_MAXCL,         // their arrival arrays' offsets (pairs) [8]
+  M_HCL = M_UEN + 16,               // the count header's block clients 
+  M_HCN = M_HCL + CP_MAXCL,         // their block counts (arrival capacities) 
+  M_HCO = M_HCN + CP_MAXCL,         // their arrival arrays' offsets (pairs) 
   M_HNCL = M_HCO + CP_MAXCL,        // header clients
-  M_CLKEND = M_HNCL + 1,            // ClientBlockList::clock of each client [8]
-  M_IDX = M_CLKEND + CP_MAXCL,      // per client: start clock of every CP_IS-th arrival [8 x CP_IN]
+  M_CLKEND = M_HNCL + 1,            // ClientBlockList::clock of each client 
+  M_IDX = M_CLKEND + CP_MAXCL,      // per client: start clock of every CP_IS-th arrival [CP_MAXCL x CP_IN]
   M_END = M_IDX + CP_MAXCL * CP_IN
 };
 static_assert(M_END <= 1024, "misc area");
 static_assert(CP_LANES * (M_END * 4 + CP_STAGE) <= 48 * 1024, "three workgroups per CU");
 // per-document counts from k_compact_count (CP_HDR words per document): blocks, deleted
-// ranges, the most blocks / ranges of one update, distinct block clients (<= 8), and each
+// ranges, the most blocks / ranges of one update, distinct block clients (<= CP_MAXCL), and each
 // client's block count (its arrival array)
-enum : uint32_t { H_NB = 0, H_NR, H_MB, H_MR, H_NCL, H_OVER, H_CL = 8, H_CN = 16, H_CO = 24, CP_HDR = 32 };
+enum : uint32_t { H_NB = 0, H_NR, H_MB, H_MR, H_NCL, H_OVER, H_CL = 8, H_CN = H_CL + CP_MAXCL, CP_HDR = H_CN + CP_MAXCL };
+static_assert(CP_HDR == COMPACT_HDR_WORDS, "count header (ykernels.h)");
 __device__ __forceinline__ uint64_t cp_words(const uint32_t *h) { // scratch words of one document
   const uint64_t items = 3ull * h[H_NB] + 2ull * h[H_NR] + 64;
   // misc, items + segments + transaction, arrivals, update buffers, branches, map entries +
@@ -1311,7 +1312,7 @@ __device__ void compact_doc(const BatchIn &b, const FastOut &o, uint32_t *hdr, c
       tq = now;
     }
   };
-  if (h[H_OVER]) { // more than 8 block clients / document bytes over 2^31
+  if (h[H_OVER]) { // more than CP_MAXCL block clients / document bytes over 2^31
     status = E_UNSUPPORTED;
     D.why = h[H_OVER];
     u1 = u0;
@@ -1384,7 +1385,7 @@ __device__ void compact_doc(const BatchIn &b, const FastOut &o, uint32_t *hdr, c
       }
       qe[q]++;
     }
-    if (nq == CP_MAXCL && D.nub) { // (a ninth client cannot pass k_compact_count)
+    if (nq == CP_MAXCL && D.nub) { // (one more client cannot pass k_compact_count)
       uint32_t tot = 0;
       for (uint32_t q = 0; q < nq; q++) tot += qe[q];
       if (tot != D.nub) {

@@ -201,7 +201,7 @@ void launch_gs_rest(const GsArgs &a, const FastOut &o, uint64_t *scan_tmp, hipSt
 // device block store; documents outside the device shape get status E_UNSUPPORTED.
 // k_compact_count fills a 32-word header per document and its scratch words (need[d]);
 // scr_off = exclusive scan of need (n_docs + 1 entries)
-constexpr uint32_t COMPACT_HDR_WORDS = 32;
+constexpr uint32_t COMPACT_HDR_WORDS = 40; // ycompact.hip CP_HDR (16 clients)
 void launch_compact_count(const BatchIn &b, uint32_t *hdr, uint64_t *need, hipStream_t s);
 void launch_compact(const BatchIn &b, const FastOut &o, uint32_t *hdr, const uint64_t *scr_off, uint32_t *scr,
                     uint32_t lpw, hipStream_t s);
