@@ -37,7 +37,11 @@
 
 namespace ym {
 
-constexpr uint32_t LN_STAGE = 1536;          // staged bytes per round / copy step
+#ifndef YM_LN_STAGE
+#define YM_LN_STAGE 2048
+#endif
+constexpr uint32_t LN_STAGE = YM_LN_STAGE; // staged bytes per round / copy step (2048: a C2 round takes 64
+                                           // updates, 1536 took ~57: -7% k_lean)
 constexpr uint32_t LN_SW = LN_STAGE / 4 + 4; // stage words (+ the word after the last one lvar reads)
 constexpr uint32_t LN_AW = 1280;             // arena words: block records grow up, DS ranges down
 constexpr uint32_t LN_BUF = LN_SW + LN_AW;   // stage + arena, reused whole by the DeleteSet phase
@@ -45,8 +49,7 @@ constexpr uint32_t LN_NBK = 16;              // client buckets per document
 constexpr uint32_t LN_MAXBLEN = 1024;        // block bytes (a copy step must always fit one block)
 constexpr uint32_t LN_DSMAXI = 252;          // bytes of one update's DeleteSet
 constexpr uint32_t LN_DSW = 1024;            // DeleteSet batch window: 16 staged bytes per lane
-constexpr uint32_t LN_ORD = 7 * LN_NBK;      // DeleteSet client order scratch (end of buf, after the scatter):
-                                             // order, hash slots (2x) + copy, clients, entry offsets
+constexpr uint32_t LN_ORD = LN_NBK;          // DeleteSet entry offsets (end of buf, after the scatter)
 constexpr uint32_t LN_NONE = 0xFFFFFFFFu;
 constexpr uint32_t LN_UMAX = 16384;          // BIG documents: above, the grid path / tiled kernel (a 20k-update
                                              // trace document held one wave 0.43 ms before a hand-over)
@@ -294,38 +297,36 @@ YM_INLINE void stage_store(uint32_t *buf, uint32_t n16, uint32_t lane, const uin
 // update's table into the result table in first-occurrence order (update.rs:542-548);
 // std's hashbrown with the identity ClientHasher (utils/client_hasher.rs) then iterates
 // in slot order.  Restated as k_fast_merge's emulation (ymerge_fast.hip, phase 5b) for
-// <= LN_NBK clients.  ord[] receives the buckets in iteration order; returns D.
-__device__ __noinline__ uint32_t lean_ds_order(uint32_t nbk, const uint32_t *client, const uint32_t *dsfirst,
-                                               uint32_t *ord, uint32_t *slot_arr) {
-  uint32_t D = 0;
-  for (uint32_t b = 0; b < nbk; b++) {
-    if (dsfirst[b] == LN_NONE) continue;
-    uint32_t j = D++;
-    while (j > 0 && dsfirst[ord[j - 1]] > dsfirst[b]) {
-      ord[j] = ord[j - 1];
-      j--;
-    }
-    ord[j] = b;
+// <= LN_NBK clients, with the table in registers (lane s = slot s < 32, bucket + 1 or 0),
+// computed by the whole wave (uniform control): a probe is one lane shuffle + ballot over
+// the 16 control bytes of the group (round 5: one lane, 16 dependent LDS reads per probe,
+// 5 % of k_lean on C2).  Lane b (a
+// bucket with a DeleteSet entry: hasd) gets its entry's offset; `total` = the end.
+YM_INLINE uint32_t lean_ds_order_wave(uint32_t lane, uint32_t nbk, bool hasd, uint32_t dsf, uint32_t cl,
+                                      uint32_t esz, uint32_t start, uint32_t *eoff, uint32_t &total) {
+  const uint64_t hm = __ballot(hasd);
+  const uint32_t D = (uint32_t)__builtin_popcountll(hm);
+  uint32_t rank = 0; // insertion order: first occurrence (dsfirst values are distinct)
+  for (uint32_t q = 0; q < nbk; q++) {
+    const uint32_t fq = rdlane(dsf, q);
+    rank += (((hm >> q) & 1) && fq < dsf) ? 1u : 0u;
   }
-  uint32_t *tmp = slot_arr + 2 * LN_NBK;
-  uint32_t buckets = 0, items = 0, growth = 0;
-  auto ctrl_empty = [&](uint32_t idx) -> bool {
-    if (idx < buckets) return slot_arr[idx] == 0;
-    if (buckets < 16) return idx < 16 ? true : slot_arr[idx - 16] == 0;
-    return slot_arr[idx - buckets] == 0;
-  };
+  uint32_t slotv = 0, buckets = 0, items = 0, growth = 0;
   auto find_slot = [&](uint32_t key) -> uint32_t {
     const uint32_t mask = buckets - 1;
     uint32_t pos = key & mask, stride = 0;
     for (;;) {
-      for (uint32_t j = 0; j < 16; j++) {
-        if (ctrl_empty(pos + j)) {
-          const uint32_t index = (pos + j) & mask;
-          if (slot_arr[index] != 0)
-            for (uint32_t k = 0; k < buckets; k++)
-              if (slot_arr[k] == 0) return k;
-          return index;
-        }
+      // ctrl_empty(pos + j) for j = lane < 16 (hashbrown's group probe): real slots, then the
+      // trailing control bytes (EMPTY beyond a small table's mirror)
+      const uint32_t idx = pos + (lane & 15);
+      const uint32_t si = idx < buckets ? idx : buckets < 16 ? idx - 16 : idx - buckets;
+      const uint32_t sv = shfl(slotv, (int)(si & 63));
+      const bool emp = idx < buckets ? sv == 0 : buckets < 16 ? (idx < 16 || sv == 0) : sv == 0;
+      const uint64_t em = __ballot(lane < 16 && emp);
+      if (em) {
+        const uint32_t index = (pos + (uint32_t)__builtin_ctzll(em)) & mask;
+        if (rdlane(slotv, index) != 0) return (uint32_t)__builtin_ctzll(__ballot(lane < buckets && slotv == 0));
+        return index;
       }
       stride += 16;
       pos = (pos + stride) & mask;
@@ -336,22 +337,33 @@ __device__ __noinline__ uint32_t lean_ds_order(uint32_t nbk, const uint32_t *cli
       const uint64_t full = buckets ? mask_to_cap(buckets - 1) : 0;
       const uint64_t need = items + 1;
       const uint32_t nb = (uint32_t)cap_to_buckets(need > full + 1 ? need : full + 1); // <= 32 for 16 items
-      const uint32_t ob = buckets;
-      for (uint32_t q = 0; q < ob; q++) tmp[q] = slot_arr[q];
+      const uint32_t ob = buckets, tmpv = slotv;
       buckets = nb;
-      for (uint32_t q = 0; q < buckets; q++) slot_arr[q] = 0;
-      for (uint32_t q = 0; q < ob; q++)
-        if (tmp[q]) slot_arr[find_slot(client[tmp[q] - 1])] = tmp[q];
+      slotv = 0;
+      for (uint32_t q = 0; q < ob; q++) {
+        const uint32_t t = rdlane(tmpv, q);
+        if (t) {
+          const uint32_t sl = find_slot(rdlane(cl, t - 1));
+          if (lane == sl) slotv = t;
+        }
+      }
       growth = (uint32_t)mask_to_cap(buckets - 1) - items;
     }
-    slot_arr[find_slot(client[ord[i]])] = ord[i] + 1;
+    const uint32_t bq = (uint32_t)__builtin_ctzll(__ballot(hasd && rank == i));
+    const uint32_t sl = find_slot(rdlane(cl, bq));
+    if (lane == sl) slotv = bq + 1;
     items++;
     growth--;
   }
-  uint32_t k = 0;
-  for (uint32_t q = 0; q < buckets; q++)
-    if (slot_arr[q]) ord[k++] = slot_arr[q] - 1;
-  return D;
+  // entries in slot order: offsets by a prefix over the slots, scattered to their buckets
+  const bool occ = slotv != 0;
+  const uint32_t sz = shfl(esz, (int)(occ ? slotv - 1 : 0));
+  const uint32_t mine = occ ? sz : 0u;
+  const uint32_t inc = wincl(mine, lane);
+  total = start + rdlane(inc, 63);
+  if (occ) eoff[slotv - 1] = start + inc - mine;
+  wsync();
+  return hasd ? eoff[lane] : 0u;
 }
 
 // ------------------------------------------------------------------ the kernel
@@ -363,6 +375,24 @@ __device__ __noinline__ uint32_t lean_ds_order(uint32_t nbk, const uint32_t *cli
 // 4 * u0 + 64 * d + B0, capacity 4 U + 64 + bytes words): block records (2 words) at
 // [0, 2U), DeleteSet item ends at [2U, 3U), the DeleteSet bitmap from 3U, component starts /
 // ends after it.  LDS then holds only the stage and the DeleteSet batch.
+// YM_LEAN_STOP=k (diagnostic builds only, tools/lean_phases.sh): end every document after
+// phase k (1 decode, 2 layout, 3 copy, 4 DeleteSet scatter, 5 components, 6 client order)
+// with an empty result, so that per-phase instruction
+// counts can be read from the SQ counters as differences
+#ifdef YM_LEAN_STOP
+#define LEAN_STOP(k)                                                                                                   \
+  if (YM_LEAN_STOP == (k)) {                                                                                           \
+    if (lane == 0) {                                                                                                   \
+      o.path[d] = 0;                                                                                                   \
+      o.status[d] = 0;                                                                                                 \
+      o.out_len[d] = 0;                                                                                                \
+      o.out_start[d] = slot;                                                                                           \
+    }                                                                                                                  \
+    return;                                                                                                            \
+  }
+#else
+#define LEAN_STOP(k)
+#endif
 template <bool BIG, bool STAMPS>
 __device__ __forceinline__ void lean_doc(const BatchIn &b, const FastOut &o, LeanLds &L, const uint32_t d,
                                          const uint32_t lane, uint32_t *const scr) {
@@ -590,6 +620,7 @@ __device__ __forceinline__ void lean_doc(const BatchIn &b, const FastOut &o, Lea
   }
   wsync();
   stamp(2);
+  LEAN_STOP(1)
 
   // ---------------------------------------------------------------- 2 layout
   const bool lb = lane < nbk;
@@ -643,6 +674,7 @@ __device__ __forceinline__ void lean_doc(const BatchIn &b, const FastOut &o, Lea
   }
   wsync();
 
+  LEAN_STOP(2)
   stamp(3);
   // ---------------------------------------------------------------- 3 copy blocks
   {
@@ -701,6 +733,7 @@ __device__ __forceinline__ void lean_doc(const BatchIn &b, const FastOut &o, Lea
     }
   }
 
+  LEAN_STOP(3)
   stamp(4);
   // ---------------------------------------------------------------- 4 DeleteSet
   // IdSet::decode of every item (id_set.rs:412-426) in batches of whole items staged from the
@@ -854,6 +887,7 @@ __device__ __forceinline__ void lean_doc(const BatchIn &b, const FastOut &o, Lea
       return;
     }
   }
+  LEAN_STOP(4)
   const uint32_t dsf = lb ? L.dsfirst[lane] : LN_NONE;
   const bool hasd = dsf != LN_NONE;
   const uint32_t D = (uint32_t)__builtin_popcountll(__ballot(hasd));
@@ -908,6 +942,7 @@ __device__ __forceinline__ void lean_doc(const BatchIn &b, const FastOut &o, Lea
   }
   wsync();
   stamp(5);
+  LEAN_STOP(5)
   // component bytes per client
   uint32_t dsb = 0;
   for (uint32_t q = 0; q < nbk; q++) {
@@ -920,34 +955,18 @@ __device__ __forceinline__ void lean_doc(const BatchIn &b, const FastOut &o, Lea
     }
     if (lane == q) dsb = acc;
   }
-  // client order and entry offsets (one lane, D <= 16)
-  // scratch at the end of buf (free once the ranges are scattered): order [16], hash slots
-  // [64], clients [16], entry offsets [16]
-  uint32_t *ord = L.buf + LN_BUF - LN_ORD, *slots = ord + LN_NBK, *clients = slots + 4 * LN_NBK,
-           *eoff = clients + LN_NBK;
+  // client order and entry offsets (the wave, D <= 16); entry offsets [16] at the end of buf
+  // (free once the ranges are scattered)
+  uint32_t *const eoff = L.buf + LN_BUF - LN_ORD;
   const uint32_t ds_start = blocks_size;
-  if (lb) clients[lane] = cl;
-  if (hasd) {
-    L.dsfirst[lane] = dsf;
-    L.bytes[lane] = varlen(cl) + varlen(ncomp) + dsb; // entry size (bytes[] is free after the copy)
-  }
-  wsync();
   uint32_t total = 0;
+  const uint32_t myeo = lean_ds_order_wave(lane, nbk, hasd, dsf, cl, hasd ? varlen(cl) + varlen(ncomp) + dsb : 0,
+                                           ds_start + varlen(D), eoff, total);
   if (lane == 0) {
-    lean_ds_order(nbk, clients, L.dsfirst, ord, slots);
-    uint32_t pos = ds_start + varlen(D);
-    for (uint32_t i2 = 0; i2 < D; i2++) {
-      const uint32_t bq = ord[i2];
-      eoff[bq] = pos;
-      pos += L.bytes[bq];
-    }
-    total = pos;
     Writer wr{out, ds_start};
     w_var(wr, D);
   }
-  total = rdlane(total, 0);
-  wsync();
-  const uint32_t myeo = hasd ? eoff[lane] : 0;
+  LEAN_STOP(6)
   if (hasd) {
     Writer wr{out, myeo};
     w_var(wr, cl);
