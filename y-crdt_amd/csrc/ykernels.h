@@ -163,6 +163,10 @@ size_t fast_lds_bytes(const FastCaps &c);
 // scr: HBM scratch of lean_scratch_words(...) u32 for documents above the LDS arena (null:
 // those are handed over)
 void launch_lean(const BatchIn &b, const FastOut &o, uint32_t *scr, hipStream_t s);
+// after k_lean: its hand-over count (counter word 10) and the sum of its 64 output-byte
+// partials (from word 32, 16 words apart) to the host-mapped sig[1..3], then sig[0] = seq;
+// with no hand-over it zeroes counter words [0, 32 + 1024) for the next merge
+void launch_lean_fin(uint32_t *counter, uint32_t *sig, uint32_t seq, hipStream_t s);
 // k_lean dispatch order for skewed batches: documents by update-count class, longest class
 // first (longest-processing-time-first: a long document starts early instead of ending the
 // kernel).  ctr: 16 zeroed words.

@@ -93,6 +93,13 @@ struct ymerge_ctx {
   DevBuf v2x, v2x_sz, v2x_off, v2_ust, v2_out, v2_osz, v2_ooff, v2_svoff, v2_svend, v2_pre;
   bool want_stamps = false;
   uint64_t *h_pinned = nullptr;
+  // k_lean's result words (hand-overs, output bytes) written by k_lean_fin into host-mapped
+  // memory behind a sequence number the host polls: no D2H copy, no stream-sync wake-up
+  // (env YMERGE_LEAN_SPIN=0: copy + hipStreamSynchronize)
+  uint32_t *h_sig = nullptr, *d_sig = nullptr;
+  uint32_t sig_seq = 0;
+  bool lean_spin = true;
+  void *counters_clean = nullptr; // k_lean_fin left `counter` zeroed (this allocation): no memset
   hipEvent_t ev[10];
   hipEvent_t v2ev[4] = {}; // lib0 v2 merge: start, after the v2 -> v1x transcode, after the merge, after the encode
   ymerge_stats stats{};
@@ -145,6 +152,7 @@ static bool ctx_init(ymerge_ctx *c, int device) {
   if (const char *v = getenv("YMERGE_GIANT_MIN")) c->giant_min = (uint32_t)atoi(v);
   if (const char *v = getenv("YMERGE_GIANT_LANE")) c->giant_lane = atoi(v) != 0;
   if (const char *v = getenv("YMERGE_LEAN_ORDER")) c->lean_order = atoi(v);
+  if (const char *v = getenv("YMERGE_LEAN_SPIN")) c->lean_spin = atoi(v) != 0;
   if (const char *v = getenv("YMERGE_PLANNER"))
     c->planner = strcmp(v, "ring") == 0 ? 1u : strcmp(v, "wave") == 0 ? 2u : 0u;
   if (const char *v = getenv("YMERGE_LEAN_SCR_MAX")) c->lean_scr_max = strtoull(v, nullptr, 10);
@@ -185,6 +193,7 @@ extern "C" void ymerge_ctx_destroy(ymerge_ctx *c) {
                     &c->v2_out, &c->v2_osz, &c->v2_ooff, &c->v2_svoff, &c->v2_svend, &c->v2_pre})
     b->release();
   if (c->h_pinned) hipHostFree(c->h_pinned);
+  if (c->h_sig) hipHostFree(c->h_sig);
   for (int k = 0; k < 2; k++) {
     if (c->stage[k]) hipHostFree(c->stage[k]);
     if (c->stage_ev[k]) hipEventDestroy(c->stage_ev[k]);
@@ -480,6 +489,43 @@ static void ls_bind(ym::LsArgs &a, const LsEntry &e, uint32_t *scr) {
 }
 
 // One batch: fast path for every document, exact engine for the documents it hands over.
+// k_lean_fin's signal (lean_spin): host-mapped coherent words, allocated on first use
+static bool ensure_sig(ymerge_ctx *c) {
+  if (c->h_sig) return true;
+  if (hipHostMalloc((void **)&c->h_sig, 4096, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+    (void)hipGetLastError();
+    c->h_sig = nullptr;
+    return false;
+  }
+  memset(c->h_sig, 0, 4096);
+  if (hipHostGetDevicePointer((void **)&c->d_sig, c->h_sig, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    hipHostFree(c->h_sig);
+    c->h_sig = nullptr;
+    return false;
+  }
+  return true;
+}
+// poll for sequence number `seq` (written last by k_lean_fin); the stream is queried now and
+// then so that a failed kernel ends the wait
+static bool wait_sig(ymerge_ctx *c, uint32_t seq) {
+  const volatile uint32_t *f = c->h_sig;
+  for (uint64_t it = 1;; it++) {
+    if (*f == seq) break;
+    if ((it & 4095) == 0) {
+      const hipError_t e = hipStreamQuery(c->s);
+      if (e == hipSuccess) {
+        if (*f == seq) break;
+        return false; // the stream drained without the signal
+      }
+      if (e != hipErrorNotReady) return false;
+    }
+    __builtin_ia32_pause();
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  return true;
+}
+
 static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes, const uint64_t *d_upd_off,
                         uint64_t n_updates, const uint64_t *d_doc_upd, uint64_t n_docs, ymerge_device_result *res) {
   resolve_times(c);
@@ -506,7 +552,9 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   uint64_t *ostart = c->out_start.as<uint64_t>(), *olen = c->out_len.as<uint64_t>();
   uint8_t *status = c->status.as<uint8_t>(), *path = c->path.as<uint8_t>();
   // counters [128 B] then k_lean's 64 output-byte partial sums [4 KB]: one memset, one copy back
-  hipMemsetAsync(c->counter.p, 0, 128 + 64 * 64, c->s);
+  // (none when the last merge ended in k_lean_fin, which zeroes them after reading)
+  if (c->counters_clean != c->counter.p) hipMemsetAsync(c->counter.p, 0, 128 + 64 * 64, c->s);
+  c->counters_clean = nullptr;
   uint64_t *stamps = nullptr;
   if (c->want_stamps) {
     if (!c->stamps.ensure(nn * 16 * 8)) return DEV_FAIL();
@@ -594,11 +642,22 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     }
     ym::launch_lean(bl, fo, lscr, c->s);
     if (hipGetLastError() != hipSuccess) return DEV_FAIL();
-    // hand-over count and k_lean's output bytes (npath[6] at counter byte 40, the 64 partial
-    // sums from byte 128) in one copy and one sync: byte 128 lands on h_pinned[512]
-    hipMemcpyAsync((uint8_t *)(c->h_pinned + 512) - 88, c->counter.as<uint8_t>() + 40, 88 + 64 * 64,
-                   hipMemcpyDeviceToHost, c->s);
-    if (hipStreamSynchronize(c->s) != hipSuccess) return DEV_FAIL();
+    if (c->lean_spin && ensure_sig(c)) {
+      // hand-over count and output bytes summed by k_lean_fin into the host-mapped words
+      const uint32_t seq = ++c->sig_seq ? c->sig_seq : ++c->sig_seq;
+      ym::launch_lean_fin(c->counter.as<uint32_t>(), c->d_sig, seq, c->s);
+      if (hipGetLastError() != hipSuccess || !wait_sig(c, seq)) return DEV_FAIL();
+      c->h_pinned[501] = c->h_sig[1];
+      for (int q = 0; q < 64; q++) c->h_pinned[512 + 8 * q] = 0;
+      c->h_pinned[512] = (uint64_t)c->h_sig[2] | ((uint64_t)c->h_sig[3] << 32);
+      if (c->h_pinned[501] == 0) c->counters_clean = c->counter.p; // (the other paths update them next)
+    } else {
+      // hand-over count and k_lean's output bytes (npath[6] at counter byte 40, the 64 partial
+      // sums from byte 128) in one copy and one sync: byte 128 lands on h_pinned[512]
+      hipMemcpyAsync((uint8_t *)(c->h_pinned + 512) - 88, c->counter.as<uint8_t>() + 40, 88 + 64 * 64,
+                     hipMemcpyDeviceToHost, c->s);
+      if (hipStreamSynchronize(c->s) != hipSuccess) return DEV_FAIL();
+    }
     n_rej = (uint32_t)(c->h_pinned[501] & 0xFFFFFFFFu);
     b.only_path3 = 1;
     if (n_rej && getenv("YMERGE_LEAN_DEBUG")) {
@@ -920,6 +979,7 @@ static int plan_exec(ymerge_ctx *c, bool diff, const uint8_t *d_bytes, const uin
     c->stamps_docs = n_docs;
   }
   hipMemsetAsync(c->counter.p, 0, 64, c->s);
+  c->counters_clean = nullptr;
   hipEventRecord(c->ev[0], c->s);
   // documents of >= ls_min_diff bytes: the parallel long-update parse, then the grid path for the
   // single-section ones (ylong.hip); the planners skip what it takes (b.ls_done)

@@ -1065,6 +1065,30 @@ void launch_lean_order(const uint64_t *doc_upd, uint32_t n_docs, uint32_t *ctr, 
   hipLaunchKernelGGL(k_lean_order_place, g, dim3(256), 0, s, doc_upd, n_docs, ctr, order);
 }
 
+// k_lean's hand-over count (npath[6]) and output bytes (the 64 partials) to the host-mapped
+// sig[1..3], then sig[0] = seq; when every document was written it also zeroes the counters
+// and partials for the next merge (the host skips its memset).  (Counting finished waves in
+// k_lean instead and letting the last one do this took k_lean 0.43 -> 1.03 ms on C2: the
+// agent-scope release before each wave's count writes back the XCD's L2.)
+__global__ void __launch_bounds__(64) k_lean_fin(uint32_t *counter, uint32_t *sig, uint32_t seq) {
+  const uint32_t l = threadIdx.x;
+  unsigned long long v = ((const unsigned long long *)(counter + 32))[8 * l];
+  const uint32_t nrej = counter[10];
+  for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads(); // every read above precedes the zeroing
+  if (nrej == 0)
+    for (uint32_t q = l; q < 32 + 64 * 16; q += 64) counter[q] = 0;
+  if (l == 0) {
+    __hip_atomic_store(sig + 1, nrej, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(sig + 2, (uint32_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(sig + 3, (uint32_t)(v >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(sig, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+void launch_lean_fin(uint32_t *counter, uint32_t *sig, uint32_t seq, hipStream_t s) {
+  hipLaunchKernelGGL(k_lean_fin, dim3(1), dim3(64), 0, s, counter, sig, seq);
+}
+
 void launch_lean(const BatchIn &b, const FastOut &o, uint32_t *scr, hipStream_t s) {
   if (!b.n_docs) return;
   constexpr int WPB = 1;
