@@ -185,6 +185,13 @@ __device__ uint32_t cp_cell(CDoc &D, int c, uint32_t clock) {
   const uint32_t n = D.m[M_NBLK + c];
   const uint32_t *a = D.cb + 2ull * D.m[M_HCO + D.m[M_CBK + c]];
   if (!n || D.m[M_IDX + c * CP_IN] > clock) return CNIL;
+  // the client's last item first (two loads): an insert's origin is most often its client's
+  // latest text, and a clock at or past that item's start is in it or in no cell
+  const uint32_t t = D.m[M_TAIL + c];
+  if (t != CNIL) {
+    const uint32_t t0 = D.I(t, I_CLOCK), tl = D.I(t, I_LEN);
+    if (clock >= t0) return clock - t0 < tl ? t : CNIL;
+  }
   // last arrived block starting <= clock: the sampled starts in LDS narrow the search of the
   // arrival array in HBM to one run of CP_IS arrivals (or to the arrivals past the samples)
   const uint32_t *ix = D.m + M_IDX + c * CP_IN;
@@ -1106,6 +1113,50 @@ struct CpWriter {
     n += k;
   }
 };
+// cp_encode's writer: the bytes gather in the lane's LDS stage (free after the update loop)
+// and go to the slot CP_STAGE at a time.  Written straight to HBM, every item-word load after
+// a byte store waited for the stores to complete (one counter covers loads and stores):
+// encode was 29 % of k_compact on C2.  Bytes past `cap` are counted, not written.
+struct CpBufWriter {
+  uint8_t *p;      // the document's slot
+  uint64_t n, cap; // bytes so far (flushed + buffered), slot capacity
+  uint8_t *buf;    // CP_STAGE bytes of LDS
+  uint32_t bn;     // buffered
+  uint64_t fl;     // flushed (n == fl + bn)
+  __device__ void put(const uint8_t *s, uint32_t k) { // k bytes to p + fl, bounded by cap
+    const uint64_t lim = fl >= cap ? 0 : (fl + k <= cap ? k : cap - fl);
+    uint8_t *d = p + fl;
+    uint32_t i = 0;
+    for (; i + 16 <= lim; i += 16) {
+      uint8_t t[16];
+#pragma unroll
+      for (int j = 0; j < 16; j++) t[j] = s[i + j];
+#pragma unroll
+      for (int j = 0; j < 16; j++) d[i + j] = t[j];
+    }
+    for (; i < lim; i++) d[i] = s[i];
+    fl += k;
+  }
+  __device__ void flush() {
+    put(buf, bn);
+    bn = 0;
+  }
+  __device__ __forceinline__ void u8(uint8_t b) {
+    if (bn == CP_STAGE) flush();
+    buf[bn++] = b;
+    n++;
+  }
+  __device__ void bytes(const uint8_t *s, uint32_t k) {
+    n += k;
+    if (bn + k <= CP_STAGE) {
+      for (uint32_t i = 0; i < k; i++) buf[bn + i] = s[i];
+      bn += k;
+      return;
+    }
+    flush();
+    put(s, k);
+  }
+};
 // ItemContent::encode of Binary / Embed / Format (block.rs:1731-1785; encoder.rs:170-179): the
 // buffer and the key as they are (canonical length varints), the JSON values re-serialised
 // (serde_json::from_str then Any::to_json: json_canon, already validated by the decode)
@@ -1454,10 +1505,18 @@ __device__ void compact_doc(const BatchIn &b, const FastOut &o, uint32_t *hdr, c
   }
   uint64_t olen = 0;
   if (!status) { // one pass into the slot, bounded by its capacity
-    CpWriter w{o.out + slot, 0, cap};
-    cp_encode(D, w);
-    if (w.n > cap) status = E_UNSUPPORTED, D.why = CU_OUTPUT;
-    olen = w.n;
+    if (stage) {
+      CpBufWriter w{o.out + slot, 0, cap, stage, 0, 0};
+      cp_encode(D, w);
+      w.flush();
+      if (w.n > cap) status = E_UNSUPPORTED, D.why = CU_OUTPUT;
+      olen = w.n;
+    } else {
+      CpWriter w{o.out + slot, 0, cap};
+      cp_encode(D, w);
+      if (w.n > cap) status = E_UNSUPPORTED, D.why = CU_OUTPUT;
+      olen = w.n;
+    }
   }
   lap(4);
   if (o.stamps)
