@@ -42,6 +42,7 @@ namespace ym {
 #endif
 constexpr uint32_t LN_STAGE = YM_LN_STAGE; // staged bytes per round / copy step (2048: a C2 round takes 64
                                            // updates, 1536 took ~57: -7% k_lean)
+static_assert(LN_STAGE < 65536, "copy phase: 16-bit per-bucket byte sums");
 constexpr uint32_t LN_SW = LN_STAGE / 4 + 4; // stage words (+ the word after the last one lvar reads)
 constexpr uint32_t LN_AW = 1280;             // arena words: block records grow up, DS ranges down
 constexpr uint32_t LN_BUF = LN_SW + LN_AW;   // stage + arena, reused whole by the DeleteSet phase
@@ -717,15 +718,27 @@ __device__ __forceinline__ void lean_doc(const BatchIn &b, const FastOut &o, Lea
       const bool act = lane < k1;
       const uint32_t src = mysrc, bl = mymeta & 0x7FF, bq = (mymeta >> 27) & 15;
       uint32_t off = 0;
-      uint64_t rem = __ballot(act);
-      while (rem) {
-        const uint32_t bb = rdlane(bq, (uint32_t)__builtin_ctzll(rem));
-        const bool mine = act && bq == bb;
-        rem &= ~__ballot(mine);
-        const uint32_t inc = wincl(mine ? bl : 0u, lane), tot = rdlane(inc, 63);
-        const uint32_t base = rdlane(curr, bb);
-        if (mine) off = base + inc - bl;
-        if (lane == bb) curr = base + tot;
+      if (nbk <= 4) {
+        // <= 4 clients: the per-bucket prefix sums as 16-bit fields of two scans (a step's
+        // blocks lie within LN_STAGE staged bytes, so no field carries)
+        const uint32_t sh = 16 * (bq & 1);
+        const uint32_t il = wincl(act && bq < 2 ? bl << sh : 0u, lane), ih = wincl(act && bq >= 2 ? bl << sh : 0u, lane);
+        const uint32_t tl = rdlane(il, 63), th = rdlane(ih, 63);
+        const uint32_t c0 = rdlane(curr, 0), c1 = rdlane(curr, 1), c2 = rdlane(curr, 2), c3 = rdlane(curr, 3);
+        const uint32_t inc = ((bq < 2 ? il : ih) >> sh) & 0xFFFFu;
+        if (act) off = (bq == 0 ? c0 : bq == 1 ? c1 : bq == 2 ? c2 : c3) + inc - bl;
+        if (lane < 4) curr += ((lane < 2 ? tl : th) >> (16 * (lane & 1))) & 0xFFFFu;
+      } else {
+        uint64_t rem = __ballot(act);
+        while (rem) {
+          const uint32_t bb = rdlane(bq, (uint32_t)__builtin_ctzll(rem));
+          const bool mine = act && bq == bb;
+          rem &= ~__ballot(mine);
+          const uint32_t inc = wincl(mine ? bl : 0u, lane), tot = rdlane(inc, 63);
+          const uint32_t base = rdlane(curr, bb);
+          if (mine) off = base + inc - bl;
+          if (lane == bb) curr = base + tot;
+        }
       }
       if (act) copy_out(L.buf, (uint32_t)(B0 + src - al1), out + off, bl);
       wsync();
