@@ -51,9 +51,14 @@ __device__ __forceinline__ void gs_rec(const GsArgs &a, uint32_t i, uint32_t w[6
   w[5] = x2.y;
 }
 
-// per-update blocks / ranges; calls blk(client, clock, len, pos, meta) and rng(client, s, e)
-template <class FB, class FR>
-__device__ __forceinline__ uint32_t gs_visit(const GsArgs &a, uint32_t i, FB blk, FR rng) {
+// an update whose DeleteSet entry has more than GS_DSCOOP ranges may hand them to its
+// workgroup (dfr returns true): one lane setting the 1,233 ranges of a `rustcode` update held
+// k_gs_write 0.56 ms
+constexpr uint32_t GS_DSCOOP = 32, GS_DSCOOP_N = 8;
+// per-update blocks / ranges; calls blk(client, clock, len, pos, meta) and rng(client, s, e),
+// or dfr(client, ranges, n) for a long range list (true: taken)
+template <class FB, class FR, class FD>
+__device__ __forceinline__ uint32_t gs_visit(const GsArgs &a, uint32_t i, FB blk, FR rng, FD dfr) {
   uint32_t w[6];
   gs_rec(a, i, w);
   if (w[0] & (REC_SLOW | REC_ORDER | 0xFF)) return GSB_SLOW; // (REC_ORDER: the exact engine)
@@ -71,6 +76,7 @@ __device__ __forceinline__ uint32_t gs_visit(const GsArgs &a, uint32_t i, FB blk
     const uint32_t *ov = a.ovf + w[4];
     for (uint32_t k = 0; k < nb; k++) blk(ov[5 * k], ov[5 * k + 1], ov[5 * k + 2], ov[5 * k + 3], ov[5 * k + 4]);
     const uint32_t *rv = ov + 5 * nb + 2 * ne;
+    if (nr > GS_DSCOOP && dfr(ov[5 * nb], rv, nr)) return 0;
     for (uint32_t k = 0; k < nr; k++) rng(ov[5 * nb], rv[3 * k], rv[3 * k + 1]);
   }
   return 0;
@@ -81,6 +87,10 @@ __global__ void __launch_bounds__(256) k_gs_pre(GsArgs a) {
   for (uint32_t j = i; j < a.nwords; j += gridDim.x * 256) a.bm[j] = 0; // (k_gs_write sets it)
   uint32_t nb = 0, nr = 0, bad = 0, cmin = 0xFFFFFFFFu, cmax = 0, maxend = 0, minst = 0xFFFFFFFFu;
   uint64_t bytes = 0, lens = 0, first = ~0ull;
+  __shared__ uint32_t s_nd, s_dn[GS_DSCOOP_N];
+  __shared__ uint64_t s_dp[GS_DSCOOP_N];
+  if (threadIdx.x == 0) s_nd = 0;
+  __syncthreads();
   if (i < a.U) bad |= gs_visit(
       a, i,
       [&](uint32_t c, uint32_t k, uint32_t len, uint32_t, uint32_t meta) {
@@ -99,11 +109,32 @@ __global__ void __launch_bounds__(256) k_gs_pre(GsArgs a) {
         minst = s < minst ? s : minst;
         cmin = c < cmin ? c : cmin;
         cmax = c > cmax ? c : cmax;
+      },
+      [&](uint32_t c, const uint32_t *rv, uint32_t n) { // the workgroup scans the ranges below
+        const uint32_t q = atomicAdd(&s_nd, 1u);
+        if (q >= GS_DSCOOP_N) return false;
+        s_dp[q] = (uint64_t)rv;
+        s_dn[q] = n;
+        nr += n;
+        cmin = c < cmin ? c : cmin;
+        cmax = c > cmax ? c : cmax;
+        return true;
       });
   if (i < a.U) {
     a.cnt[i] = nb | ((uint64_t)nr << 32);
     a.bl[i] = (bytes << 32) | lens;
   } // block bytes (< 2^31 per document) | clock lengths (< 2^32)
+  __syncthreads();
+  const uint32_t nd = s_nd < GS_DSCOOP_N ? s_nd : GS_DSCOOP_N;
+  for (uint32_t e = 0; e < nd; e++) { // (folded into this thread's partials)
+    const uint32_t *rv = (const uint32_t *)s_dp[e];
+    for (uint32_t k = threadIdx.x; k < s_dn[e]; k += 256) {
+      const uint32_t rs = rv[3 * k], re = rv[3 * k + 1];
+      if (re <= rs) bad |= GSB_DS;
+      maxend = re > maxend ? re : maxend;
+      minst = rs < minst ? rs : minst;
+    }
+  }
   // workgroup partials (wave shuffles, then LDS), reduced by k_gs_reduce: atomics from every
   // wave on the same five words serialised at one L2 channel (165 us for the C1 trace)
   for (int o = 32; o > 0; o >>= 1) {
@@ -220,18 +251,61 @@ __device__ __forceinline__ uint32_t gs_hdr(const GsArgs &a) { // bytes of the on
 
 // verbatim blocks of >= GS_COOP bytes are copied by the whole workgroup after its lanes' walks
 constexpr uint32_t GS_COOP = 256, GS_COOP_N = 64;
+// bits [s, e) of the deleted-clock bitmap (from the bitmap's base clock): the partial end
+// words by atomicOr, the whole words between them directly (ranges over 64 words: queued for
+// the workgroup's fill)
+__device__ __forceinline__ void gs_set_range(const GsArgs &a, uint32_t base, uint32_t s, uint32_t e, uint32_t &bad,
+                                             uint32_t &s_nr, uint32_t *s_r0, uint32_t *s_r1) {
+  if (e - base > a.nbits) {
+    bad |= GSB_RANGE;
+    return;
+  }
+  s -= base;
+  e -= base;
+  const uint32_t w0 = s >> 5, w1 = (e - 1) >> 5;
+  const uint32_t m0 = 0xFFFFFFFFu << (s & 31), m1 = 0xFFFFFFFFu >> (31 - ((e - 1) & 31));
+  if (w0 == w1) {
+    atomicOr(&a.bm[w0], m0 & m1);
+  } else {
+    atomicOr(&a.bm[w0], m0);
+    uint32_t q = GS_COOP_N;
+    if (w1 - w0 > 64) q = atomicAdd(&s_nr, 1u);
+    if (q < GS_COOP_N) { // the workgroup fills the whole words after the walks
+      s_r0[q] = w0 + 1;
+      s_r1[q] = w1;
+    } else {
+      for (uint32_t z = w0 + 1; z < w1; z++) a.bm[z] = 0xFFFFFFFFu;
+    }
+    atomicOr(&a.bm[w1], m1);
+  }
+}
 __device__ __forceinline__ void gs_write_lane(const GsArgs &a, uint32_t i, uint32_t &s_n, uint32_t *s_l, uint64_t *s_d,
-                                              uint64_t *s_s, uint32_t &s_nr, uint32_t *s_r0, uint32_t *s_r1);
+                                              uint64_t *s_s, uint32_t &s_nr, uint32_t *s_r0, uint32_t *s_r1,
+                                              uint32_t &s_nd, uint64_t *s_dp, uint32_t *s_dn);
 __global__ void __launch_bounds__(256) k_gs_write(GsArgs a) {
   __shared__ uint32_t s_n, s_l[GS_COOP_N], s_nr, s_r0[GS_COOP_N], s_r1[GS_COOP_N];
   __shared__ uint64_t s_d[GS_COOP_N], s_s[GS_COOP_N];
-  if (threadIdx.x == 0) s_n = s_nr = 0;
+  __shared__ uint32_t s_nd, s_dn[GS_DSCOOP_N];
+  __shared__ uint64_t s_dp[GS_DSCOOP_N];
+  if (threadIdx.x == 0) s_n = s_nr = s_nd = 0;
   __syncthreads();
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i < a.U) gs_write_lane(a, i, s_n, s_l, s_d, s_s, s_nr, s_r0, s_r1);
+  if (i < a.U) gs_write_lane(a, i, s_n, s_l, s_d, s_s, s_nr, s_r0, s_r1, s_nd, s_dp, s_dn);
   __syncthreads();
   const uint32_t nc = s_n < GS_COOP_N ? s_n : GS_COOP_N;
   for (uint32_t e = 0; e < nc; e++) copy_coop((uint8_t *)s_d[e], (const uint8_t *)s_s[e], s_l[e], threadIdx.x, 256);
+  // long range lists handed over by the lanes, one range per thread
+  const uint32_t nd = s_nd < GS_DSCOOP_N ? s_nd : GS_DSCOOP_N;
+  if (nd) {
+    const uint32_t base = 32 * a.g[GS_MINST];
+    uint32_t bad = 0;
+    for (uint32_t e = 0; e < nd; e++) {
+      const uint32_t *rv = (const uint32_t *)s_dp[e];
+      for (uint32_t k = threadIdx.x; k < s_dn[e]; k += 256) gs_set_range(a, base, rv[3 * k], rv[3 * k + 1], bad, s_nr, s_r0, s_r1);
+    }
+    if (bad) atomicOr(&a.g[GS_BAD], bad);
+  }
+  __syncthreads();
   // whole bitmap words of long deleted ranges (every bit set: plain stores are exact against
   // the other lanes' atomic ORs); one lane ORing a 60k-clock delete word by word took 0.5 ms
   const uint32_t nr = s_nr < GS_COOP_N ? s_nr : GS_COOP_N;
@@ -239,7 +313,8 @@ __global__ void __launch_bounds__(256) k_gs_write(GsArgs a) {
     for (uint32_t q = s_r0[e] + threadIdx.x; q < s_r1[e]; q += 256) a.bm[q] = 0xFFFFFFFFu;
 }
 __device__ __forceinline__ void gs_write_lane(const GsArgs &a, uint32_t i, uint32_t &s_n, uint32_t *s_l, uint64_t *s_d,
-                                              uint64_t *s_s, uint32_t &s_nr, uint32_t *s_r0, uint32_t *s_r1) {
+                                              uint64_t *s_s, uint32_t &s_nr, uint32_t *s_r0, uint32_t *s_r1,
+                                              uint32_t &s_nd, uint64_t *s_dp, uint32_t *s_dn) {
   const uint32_t clock0 = (uint32_t)*(const uint64_t *)(a.g + GS_FIRST);
   uint64_t expect = clock0 + (a.s_bl[i] & 0xFFFFFFFFu);
   uint8_t *dst = gs_out(a) + gs_hdr(a) + (a.s_bl[i] >> 32);
@@ -271,30 +346,13 @@ __device__ __forceinline__ void gs_write_lane(const GsArgs &a, uint32_t i, uint3
         }
         dst += n;
       },
-      [&](uint32_t, uint32_t s, uint32_t e) {
-        if (e - base > a.nbits) {
-          bad |= GSB_RANGE;
-          return;
-        }
-        s -= base;
-        e -= base;
-        // bits [s, e): the partial end words and the whole words between them
-        const uint32_t w0 = s >> 5, w1 = (e - 1) >> 5;
-        const uint32_t m0 = 0xFFFFFFFFu << (s & 31), m1 = 0xFFFFFFFFu >> (31 - ((e - 1) & 31));
-        if (w0 == w1) {
-          atomicOr(&a.bm[w0], m0 & m1);
-        } else {
-          atomicOr(&a.bm[w0], m0);
-          uint32_t q = GS_COOP_N;
-          if (w1 - w0 > 64) q = atomicAdd(&s_nr, 1u);
-          if (q < GS_COOP_N) { // the workgroup fills the whole words after the walks
-            s_r0[q] = w0 + 1;
-            s_r1[q] = w1;
-          } else {
-            for (uint32_t z = w0 + 1; z < w1; z++) a.bm[z] = 0xFFFFFFFFu;
-          }
-          atomicOr(&a.bm[w1], m1);
-        }
+      [&](uint32_t, uint32_t s, uint32_t e) { gs_set_range(a, base, s, e, bad, s_nr, s_r0, s_r1); },
+      [&](uint32_t, const uint32_t *rv, uint32_t n) {
+        const uint32_t q = atomicAdd(&s_nd, 1u);
+        if (q >= GS_DSCOOP_N) return false;
+        s_dp[q] = (uint64_t)rv;
+        s_dn[q] = n;
+        return true;
       });
   if (bad) atomicOr(&a.g[GS_BAD], bad);
 }
