@@ -215,8 +215,21 @@ def test_lean_big_documents(engine, oracle):
     docs.append(ups)
     docs.append([upd(3, 0, item("a" * 600)), upd(3, 600, item("b" * 300))] +
                 [upd(ds=[(3, [(2 * (i % 450), 1)])]) for i in range(1500)])  # 450 components
+    # (a batch of <= 64 documents hands its documents of >= 4,096 updates to the grid path /
+    # tiled kernel, ykernels.h GS_SMALL_DOCS: small documents make this a large batch)
+    docs += [[upd(100 + k, 0, item("z"))] for k in range(64)]
     st = run(engine, oracle, docs)
     assert st["docs_lean"] == len(docs), st
+
+
+def test_small_batch_long_documents(engine, oracle):
+    """A batch of <= 64 documents: its documents of >= 4,096 updates skip k_lean (the grid path
+    for one client, the tiled kernel otherwise), the others stay lean; byte-exact either way."""
+    rng = np.random.default_rng(0x5B)
+    docs = [text_log(rng, [11], 5000), text_log(rng, [12, 13], 4500), text_log(rng, [14], 4095),
+            text_log(rng, [15, 16, 17], 300)]
+    st = run(engine, oracle, docs)
+    assert st["docs_lean"] == 2 and st["docs_giant"] == 1, st
 
 
 def test_lean_c3_zipf(engine, oracle):

@@ -21,6 +21,7 @@ struct BatchIn {
   uint32_t v1x = 0;    // bytes are the internal v1x grammar (lib0 v2 path), not lib0 v1
   uint32_t only_path3 = 0; // k_fast_merge: only the documents k_lean handed over (path == 3)
   const uint32_t *order = nullptr; // k_lean: wavefront -> document (long documents first), or identity
+  uint32_t lean_umax = 0;          // k_lean: hand over documents of more updates (0: LN_UMAX)
 };
 
 // Per-update decode record written by k_decode (one lane per update over the whole
@@ -178,6 +179,10 @@ void launch_fast_merge(const BatchIn &b, const FastCaps &caps, const FastOut &o,
 // one long single-client document merged by grid-wide kernels (ygiant.hip)
 constexpr uint32_t GS_LIST = 16;     // such documents per batch (the rest: tiled kernel)
 constexpr uint32_t GS_MIN_U = 8192; // updates (env YMERGE_GIANT_MIN; editing traces: 4 of 5 documents on the grid path)
+// batches of <= GS_SMALL_DOCS documents (too few for k_lean's waves to fill the GPU): documents
+// of >= GS_MIN_SMALL updates skip k_lean (one wave serially: friendsforever_flat's 4,288
+// updates took 0.40 ms) and take the grid path when they are its shape
+constexpr uint32_t GS_SMALL_DOCS = 64, GS_MIN_SMALL = 4096;
 constexpr uint8_t GS_PATH = 5;       // path of a listed document until k_gs_final decides
 struct GsArgs {
   const uint8_t *bytes;

@@ -580,7 +580,9 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   // general route below, which keeps the records and does not list the document for the grid
   // path again (that second attempt failed the same way).
   bool decoded = false, giant_rejected = false;
-  if (n == 1 && c->giant_min && n_updates >= c->giant_min && n_updates < (1ull << 31) && c->fast_threads &&
+  // grid-path threshold of this batch: lower for a batch of few documents (ykernels.h)
+  const uint32_t gmin = c->giant_min && n <= ym::GS_SMALL_DOCS ? std::min(c->giant_min, ym::GS_MIN_SMALL) : c->giant_min;
+  if (n == 1 && gmin && n_updates >= gmin && n_updates < (1ull << 31) && c->fast_threads &&
       !c->want_stamps && c->giant_lane) {
     hipEventRecord(c->ev[7], c->s);
     hipEventRecord(c->ev[0], c->s);
@@ -632,6 +634,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     // large batches: long documents dispatched first (a skewed batch otherwise ends on the
     // last long document to start)
     ym::BatchIn bl = b;
+    if (gmin && n <= ym::GS_SMALL_DOCS) bl.lean_umax = gmin - 1; // (documents of >= gmin updates: grid path or tiled)
     // (batches of many small documents: Zipf-like tenants, where one long document would
     // otherwise end the kernel; also the ~48 MB groups of the pipelined host entry)
     if (c->lean_order == 1 || (c->lean_order < 0 && n >= 8192 && n_updates < 256ull * n)) {
@@ -734,7 +737,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   if (fast && n_p2) {
     // long single-client documents first (ygiant.hip): listed and marked GS_PATH, merged by the
     // grid-wide kernels; the ones that are not that shape return to path 2 before k_big_count
-    const bool giant = c->giant_min && n_updates >= c->giant_min && !c->want_stamps && !giant_rejected;
+    const bool giant = gmin && n_updates >= gmin && !c->want_stamps && !giant_rejected;
     // single long update documents (one REC_LONG record, ylong.hip): listed in the same round trip
     const bool lsg = c->long_parse && c->long_grid && !c->want_stamps;
     constexpr size_t GSL = 1 + 6 * ym::GS_LIST, LSL = 4 + ym::LS_EW * ym::LS_LIST;
@@ -742,7 +745,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
       if (!c->gs_list.ensure(GSL * 8) || !c->ls_list.ensure(LSL * 4)) return DEV_FAIL();
       if (giant) {
         hipMemsetAsync(c->gs_list.p, 0, 8, c->s);
-        ym::launch_gs_find(b, path, c->giant_min, c->gs_list.as<uint64_t>(), c->s);
+        ym::launch_gs_find(b, path, gmin, c->gs_list.as<uint64_t>(), c->s);
         hipMemcpyAsync(c->h_pinned + 128, c->gs_list.p, GSL * 8, hipMemcpyDeviceToHost, c->s);
       }
       if (lsg) {

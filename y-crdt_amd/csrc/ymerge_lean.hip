@@ -1031,7 +1031,8 @@ __global__ void __launch_bounds__(64 * WPB, OCC) k_lean(BatchIn b, FastOut o, ui
   const uint32_t d = b.order ? __builtin_amdgcn_readfirstlane(b.order[slot]) : slot;
   const uint64_t u0 = b.doc_upd[d], u1 = b.doc_upd[d + 1];
   const uint64_t nb = b.upd_off[u1] - b.upd_off[u0];
-  if (scr && (u1 - u0 > LN_AW || nb >= 65536) && u1 - u0 <= LN_UMAX && nb < (1ull << 31))
+  const uint32_t umax = b.lean_umax ? b.lean_umax : LN_UMAX;
+  if (scr && (u1 - u0 > LN_AW || nb >= 65536) && u1 - u0 <= umax && nb < (1ull << 31))
     lean_doc<true, STAMPS>(b, o, lds[w], d, lane, scr);
   else
     lean_doc<false, STAMPS>(b, o, lds[w], d, lane, scr);
