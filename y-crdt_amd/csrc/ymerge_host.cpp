@@ -645,10 +645,14 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     }
     ym::launch_lean(bl, fo, lscr, c->s);
     if (hipGetLastError() != hipSuccess) return DEV_FAIL();
+    // k_lean's end (ms_lean = ev7 -> ev0: the kernel, not the host's turnaround after it; the
+    // general route records ev0 again below)
+    hipEventRecord(c->ev[0], c->s);
     if (c->lean_spin && ensure_sig(c)) {
       // hand-over count and output bytes summed by k_lean_fin into the host-mapped words
       const uint32_t seq = ++c->sig_seq ? c->sig_seq : ++c->sig_seq;
       ym::launch_lean_fin(c->counter.as<uint32_t>(), c->d_sig, seq, c->s);
+      hipEventRecord(c->ev[3], c->s); // (the end of a merge that k_lean writes whole)
       if (hipGetLastError() != hipSuccess || !wait_sig(c, seq)) return DEV_FAIL();
       c->h_pinned[501] = c->h_sig[1];
       for (int q = 0; q < 64; q++) c->h_pinned[512 + 8 * q] = 0;
@@ -678,7 +682,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
         }
     }
   }
-  hipEventRecord(c->ev[0], c->s);
+  if (!lean || n_rej) hipEventRecord(c->ev[0], c->s);
   const bool fast = c->fast_threads && n_rej > 0;
   if (fast) {
     // diagnostic (env YMERGE_DECODE_DBG): k_decode_exact's slowest workgroups to stderr
@@ -861,14 +865,14 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
       }
     }
   }
-  hipEventRecord(c->ev[2], c->s);
   // total output bytes (and packed offsets for host copies); when k_lean wrote every
   // document its byte counter is the total and the scan waits for a host copy (pack_to_host)
   uint64_t total = 0;
   c->pack_stale = lean && n_rej == 0;
+  if (!c->pack_stale || !c->lean_spin || !c->h_sig) hipEventRecord(c->ev[2], c->s);
   if (c->pack_stale) {
     for (int q = 0; q < 64; q++) total += c->h_pinned[512 + 8 * q];
-    hipEventRecord(c->ev[3], c->s);
+    if (!c->lean_spin || !c->h_sig) hipEventRecord(c->ev[3], c->s); // (else recorded after k_lean_fin)
     if (hipGetLastError() != hipSuccess) return DEV_FAIL();
     c->stats = ymerge_stats{};
     c->stats.n_docs = n_docs;
