@@ -97,6 +97,12 @@ struct ymerge_ctx {
   // memory behind a sequence number the host polls: no D2H copy, no stream-sync wake-up
   // (env YMERGE_LEAN_SPIN=0: copy + hipStreamSynchronize)
   uint32_t *h_sig = nullptr, *d_sig = nullptr;
+  // the one-long-document lane (C1) replayed as a captured hipGraph: its ~35 small launches
+  // are host-bound at several us each.  A key (inputs + buffer addresses) seen twice in a row
+  // is captured on its second run and replayed after (env YMERGE_GIANT_GRAPH=0: eager).
+  uint64_t giant_key = 0, graph_key = 0;
+  hipGraphExec_t giant_exec = nullptr;
+  bool giant_graph = true;
   uint32_t sig_seq = 0;
   bool lean_spin = true;
   void *counters_clean = nullptr; // k_lean_fin left `counter` zeroed (this allocation): no memset
@@ -153,6 +159,7 @@ static bool ctx_init(ymerge_ctx *c, int device) {
   if (const char *v = getenv("YMERGE_GIANT_LANE")) c->giant_lane = atoi(v) != 0;
   if (const char *v = getenv("YMERGE_LEAN_ORDER")) c->lean_order = atoi(v);
   if (const char *v = getenv("YMERGE_LEAN_SPIN")) c->lean_spin = atoi(v) != 0;
+  if (const char *v = getenv("YMERGE_GIANT_GRAPH")) c->giant_graph = atoi(v) != 0;
   if (const char *v = getenv("YMERGE_PLANNER"))
     c->planner = strcmp(v, "ring") == 0 ? 1u : strcmp(v, "wave") == 0 ? 2u : 0u;
   if (const char *v = getenv("YMERGE_LEAN_SCR_MAX")) c->lean_scr_max = strtoull(v, nullptr, 10);
@@ -194,6 +201,7 @@ extern "C" void ymerge_ctx_destroy(ymerge_ctx *c) {
     b->release();
   if (c->h_pinned) hipHostFree(c->h_pinned);
   if (c->h_sig) hipHostFree(c->h_sig);
+  if (c->giant_exec) hipGraphExecDestroy(c->giant_exec);
   for (int k = 0; k < 2; k++) {
     if (c->stage[k]) hipHostFree(c->stage[k]);
     if (c->stage_ev[k]) hipEventDestroy(c->stage_ev[k]);
@@ -404,6 +412,16 @@ static void resolve_times(ymerge_ctx *c) {
 // when it is not that shape or outgrows a bound.  The deleted-clock bitmap holds one bit per input
 // byte (at least 2^20: a clock unit of text is a byte of it), the squashed ranges one per 2 input
 // bytes.
+// run_giant's buffers (allocated before a graph capture: no allocation inside one)
+static bool giant_ensure(ymerge_ctx *c, uint32_t U, uint64_t doc_bytes) {
+  const size_t nu = (size_t)U + 1;
+  const uint64_t nwc = std::min<uint64_t>(std::max<uint64_t>(doc_bytes / 32 + 2, 32768), 1ull << 26);
+  const size_t nw = nwc, kc = (size_t)std::min<uint64_t>(nwc * 16, doc_bytes / 2 + 2) + 2;
+  const size_t nparts = ((size_t)U + 255) / 256;
+  return c->gs1.ensure((4 * nu + 8) * 8 + nparts * 28 + 64) &&
+         c->scan_tmp.ensure(ym::scan_tmp_elems((uint32_t)std::max<size_t>(std::max<size_t>(nu, nw), kc)) * 8 + 64) &&
+         c->gs2.ensure(nw * 4 + (2 * nw + 1) * 8 + 2 * kc * 4 + 2 * kc * 8 + 64);
+}
 static int run_giant(ymerge_ctx *c, const ym::BatchIn &b, const ym::FastOut &fo, uint32_t d, uint32_t U, uint64_t u0,
                      uint64_t doc_bytes) {
   ym::GsArgs a{};
@@ -421,11 +439,7 @@ static int run_giant(ymerge_ctx *c, const ym::BatchIn &b, const ym::FastOut &fo,
   a.nbits = (uint32_t)((nwc - 2) * 32);
   a.kcap = (uint32_t)std::min<uint64_t>(nwc * 16, doc_bytes / 2 + 2);
   const size_t nw = a.nwords, kc = (size_t)a.kcap + 2;
-  const size_t nparts = ((size_t)U + 255) / 256;
-  if (!c->gs1.ensure((4 * nu + 8) * 8 + nparts * 28 + 64) ||
-      !c->scan_tmp.ensure(ym::scan_tmp_elems((uint32_t)std::max<size_t>(std::max<size_t>(nu, nw), kc)) * 8 + 64) ||
-      !c->gs2.ensure(nw * 4 + (2 * nw + 1) * 8 + 2 * kc * 4 + 2 * kc * 8 + 64))
-    return DEV_FAIL();
+  if (!giant_ensure(c, U, doc_bytes)) return DEV_FAIL();
   uint64_t *w = c->gs1.as<uint64_t>();
   a.cnt = w;
   a.bl = w + nu;
@@ -585,22 +599,64 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
   if (n == 1 && gmin && n_updates >= gmin && n_updates < (1ull << 31) && c->fast_threads &&
       !c->want_stamps && c->giant_lane) {
     hipEventRecord(c->ev[7], c->s);
-    hipEventRecord(c->ev[0], c->s);
-    ym::launch_decode(d_bytes, d_upd_off, n_updates, c->rec.as<uint32_t>(), c->ovf.as<uint32_t>(), c->huge.as<uint32_t>(),
-                      huge_words(n_bytes), c->s, lp_args(c, n_bytes, b.v1x), b.v1x); // (no probe: one sync less)
-    hipEventRecord(c->ev[5], c->s);
+    const ym::LpArgs *la = lp_args(c, n_bytes, b.v1x);
+    if (!giant_ensure(c, (uint32_t)n_updates, n_bytes)) return DEV_FAIL();
+    // the launch sequence's key: inputs, buffer addresses, grammar, parse settings
+    uint64_t key = 0xcbf29ce484222325ull;
+    auto mix = [&](uint64_t v) { key = (key ^ v) * 0x100000001b3ull; };
+    for (uint64_t v : {(uint64_t)d_bytes, n_bytes, (uint64_t)d_upd_off, n_updates, (uint64_t)d_doc_upd,
+                       (uint64_t)b.v1x, (uint64_t)c->rec.p, (uint64_t)c->ovf.p, (uint64_t)c->huge.p,
+                       (uint64_t)c->lp.p, (uint64_t)c->gs1.p, (uint64_t)c->gs2.p, (uint64_t)c->scan_tmp.p,
+                       (uint64_t)arena, (uint64_t)ostart, (uint64_t)olen, (uint64_t)status, (uint64_t)path,
+                       (uint64_t)c->counter.p, (uint64_t)(la != nullptr), (uint64_t)c->lp_mid})
+      mix(v);
+    bool graphed = false;
+    if (c->giant_graph && c->giant_exec && c->graph_key == key) {
+      graphed = hipGraphLaunch(c->giant_exec, c->s) == hipSuccess;
+    } else if (c->giant_graph && c->giant_key == key &&
+               hipStreamBeginCapture(c->s, hipStreamCaptureModeThreadLocal) == hipSuccess) {
+      ym::launch_decode(d_bytes, d_upd_off, n_updates, c->rec.as<uint32_t>(), c->ovf.as<uint32_t>(),
+                        c->huge.as<uint32_t>(), huge_words(n_bytes), c->s, la, b.v1x);
+      const int rc0 = run_giant(c, b, fo, 0, (uint32_t)n_updates, 0, n_bytes);
+      hipGraph_t g = nullptr;
+      const hipError_t ec = hipStreamEndCapture(c->s, &g);
+      if (ec == hipSuccess && rc0 == 0 && g) {
+        if (c->giant_exec) hipGraphExecDestroy(c->giant_exec);
+        c->giant_exec = nullptr;
+        if (hipGraphInstantiate(&c->giant_exec, g, nullptr, nullptr, 0) == hipSuccess) {
+          c->graph_key = key;
+          graphed = hipGraphLaunch(c->giant_exec, c->s) == hipSuccess;
+        } else {
+          c->giant_exec = nullptr;
+        }
+      }
+      if (g) hipGraphDestroy(g);
+      (void)hipGetLastError();
+      if (!graphed) c->giant_graph = false; // capture not usable here: eager from now on
+    }
+    if (!graphed) { // eager launches (the first run of a key, or graphs off)
+      hipEventRecord(c->ev[0], c->s);
+      ym::launch_decode(d_bytes, d_upd_off, n_updates, c->rec.as<uint32_t>(), c->ovf.as<uint32_t>(),
+                        c->huge.as<uint32_t>(), huge_words(n_bytes), c->s, la, b.v1x); // (no probe: one sync less)
+      hipEventRecord(c->ev[5], c->s);
+      const int rc = run_giant(c, b, fo, 0, (uint32_t)n_updates, 0, n_bytes);
+      if (rc) return rc;
+      c->giant_key = key;
+    }
     decoded = true;
-    const int rc = run_giant(c, b, fo, 0, (uint32_t)n_updates, 0, n_bytes);
-    if (rc) return rc;
     hipEventRecord(c->ev[1], c->s);
     hipMemcpyAsync(c->h_pinned + 20, path, 1, hipMemcpyDeviceToHost, c->s);
     hipMemcpyAsync(c->h_pinned + 21, olen, 8, hipMemcpyDeviceToHost, c->s);
     if (hipStreamSynchronize(c->s) != hipSuccess) return DEV_FAIL();
     if ((c->h_pinned[20] & 0xFF) == 0) {
       float t05 = 0, t51 = 0, t71 = 0;
-      hipEventElapsedTime(&t05, c->ev[0], c->ev[5]);
-      hipEventElapsedTime(&t51, c->ev[5], c->ev[1]);
       hipEventElapsedTime(&t71, c->ev[7], c->ev[1]);
+      if (graphed) { // (one graph: no split between decode and the grid kernels)
+        t51 = t71;
+      } else {
+        hipEventElapsedTime(&t05, c->ev[0], c->ev[5]);
+        hipEventElapsedTime(&t51, c->ev[5], c->ev[1]);
+      }
       c->stats = ymerge_stats{};
       c->stats.n_docs = n_docs;
       c->stats.bytes_in = n_bytes;
