@@ -183,6 +183,10 @@ int yconvert_updates_v1_to_v2_batch_device(ymerge_ctx *ctx, const uint8_t *d_byt
 int ymerge_result_to_host(ymerge_ctx *ctx, const ymerge_device_result *res, uint64_t n_docs, uint8_t *out,
                           uint64_t *out_off, uint8_t *status);
 void ymerge_last_stats(ymerge_ctx *ctx, ymerge_stats *stats);
+/* stage timing (the ms_* fields of ymerge_last_stats: HIP events around the stages), on by
+ * default.  Off (on = 0): a merge that k_lean writes whole records no events (one host call
+ * less per event on its critical path; its ms_* read 0).  Results are the same either way. */
+void ymerge_ctx_set_stage_timing(ymerge_ctx *ctx, int on);
 /* diagnostic builds (env YMERGE_STAMPS=1): per-document s_memtime phase stamps, 16 per doc */
 int ymerge_debug_stamps(ymerge_ctx *ctx, uint64_t n_docs, uint64_t *dst);
 

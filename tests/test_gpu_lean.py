@@ -255,3 +255,18 @@ def test_lean_scratch_unavailable_degrades(oracle):
         assert st["docs_lean"] == 1, st  # the 300-update document fits LDS
     finally:
         e.close()
+
+
+def test_stage_timing_off(engine, oracle):
+    """ymerge_ctx_set_stage_timing(ctx, 0): a merge k_lean writes whole records no stage
+    events (the stats' times read 0) and writes the same bytes; on again, the times return."""
+    rng = np.random.default_rng(0x71)
+    docs = [text_log(rng, [1, 2], 300) for _ in range(8)]
+    try:
+        engine.set_stage_timing(False)
+        st = run(engine, oracle, docs)
+        assert st["docs_lean"] == len(docs) and st["ms_lean"] == 0.0, st
+    finally:
+        engine.set_stage_timing(True)
+    st = run(engine, oracle, docs)
+    assert st["docs_lean"] == len(docs) and st["ms_lean"] > 0.0, st

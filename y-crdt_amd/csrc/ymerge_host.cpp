@@ -105,6 +105,7 @@ struct ymerge_ctx {
   bool giant_graph = true;
   uint32_t sig_seq = 0;
   bool lean_spin = true;
+  bool timing = true; // stage timing events (ymerge_ctx_set_stage_timing)
   void *counters_clean = nullptr; // k_lean_fin left `counter` zeroed (this allocation): no memset
   hipEvent_t ev[10];
   hipEvent_t v2ev[4] = {}; // lib0 v2 merge: start, after the v2 -> v1x transcode, after the merge, after the encode
@@ -677,7 +678,8 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     }
     giant_rejected = true; // k_gs_final left it on path 2: the general route takes it
   }
-  hipEventRecord(c->ev[7], c->s);
+  const bool no_ev = !c->timing; // (ymerge_ctx_set_stage_timing)
+  if (!no_ev) hipEventRecord(c->ev[7], c->s);
   if (lean) {
     // BIG k_lean documents keep their size-proportional tables in HBM (untouched otherwise)
     const uint64_t lw = ym::lean_scratch_words(n_updates, n_docs, n_bytes);
@@ -703,12 +705,12 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     if (hipGetLastError() != hipSuccess) return DEV_FAIL();
     // k_lean's end (ms_lean = ev7 -> ev0: the kernel, not the host's turnaround after it; the
     // general route records ev0 again below)
-    hipEventRecord(c->ev[0], c->s);
+    if (!no_ev) hipEventRecord(c->ev[0], c->s);
     if (c->lean_spin && ensure_sig(c)) {
       // hand-over count and output bytes summed by k_lean_fin into the host-mapped words
       const uint32_t seq = ++c->sig_seq ? c->sig_seq : ++c->sig_seq;
       ym::launch_lean_fin(c->counter.as<uint32_t>(), c->d_sig, seq, c->s);
-      hipEventRecord(c->ev[3], c->s); // (the end of a merge that k_lean writes whole)
+      if (!no_ev) hipEventRecord(c->ev[3], c->s); // (the end of a merge that k_lean writes whole)
       if (hipGetLastError() != hipSuccess || !wait_sig(c, seq)) return DEV_FAIL();
       c->h_pinned[501] = c->h_sig[1];
       for (int q = 0; q < 64; q++) c->h_pinned[512 + 8 * q] = 0;
@@ -935,7 +937,7 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
     c->stats.bytes_in = n_bytes;
     c->stats.docs_lean = n_docs;
     c->stats.bytes_out = total;
-    c->times_pending = true; // ms_lean / ms_total: resolve_times
+    c->times_pending = !no_ev; // ms_lean / ms_total: resolve_times
     res->d_out = arena;
     res->d_out_start = ostart;
     res->d_out_len = olen;
@@ -1423,6 +1425,12 @@ extern "C" int ymerge_debug_stamps(ymerge_ctx *c, uint64_t n_docs, uint64_t *dst
   hipSetDevice(c->device);
   if (hipMemcpy(dst, c->stamps.p, n_docs * 16 * 8, hipMemcpyDeviceToHost) != hipSuccess) return DEV_FAIL();
   return 0;
+}
+
+extern "C" void ymerge_ctx_set_stage_timing(ymerge_ctx *c, int on) {
+  if (!c) return;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->timing = on != 0;
 }
 
 extern "C" void ymerge_last_stats(ymerge_ctx *c, ymerge_stats *st) {

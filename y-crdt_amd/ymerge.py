@@ -100,6 +100,8 @@ def lib():
     L.yencode_state_vector_from_update_v1_batch_device.argtypes = [vp, vp, vp, u64, c.POINTER(_DevRes)]
     L.ymerge_result_to_host.argtypes = [vp, c.POINTER(_DevRes), u64, vp, vp, vp]
     L.ymerge_last_stats.argtypes = [vp, c.POINTER(_Stats)]
+    L.ymerge_ctx_set_stage_timing.argtypes = [vp, c.c_int]
+    L.ymerge_ctx_set_stage_timing.restype = None
     L.ymerge_updates_v1.restype = vp
     L.ymerge_updates_v1.argtypes = [c.POINTER(c.c_char_p), c.POINTER(u32), u32, c.POINTER(u32)]
     L.ydiff_updates_v1.restype = vp
@@ -355,6 +357,11 @@ class Engine:
         if rc:
             raise DeviceError(f"state-vector batch failed ({rc})")
         return DeviceResult(self, res, n_docs)
+
+    def set_stage_timing(self, on):
+        """Stage timing events on / off (ymerge_ctx_set_stage_timing); off, the stats' ms_*
+        of a merge k_lean writes whole read 0."""
+        lib().ymerge_ctx_set_stage_timing(self._ctx, 1 if on else 0)
 
     def stats(self):
         s = _Stats()
