@@ -263,6 +263,14 @@ void launch_v2_sv_parse(const uint8_t *sv, const uint64_t *sv_off, const uint8_t
                         uint64_t *rest_end, uint8_t *pre, hipStream_t s);
 void launch_v2_encode(bool write, const uint8_t *src, const uint64_t *src_start, const uint64_t *src_len,
                       const uint8_t *status, uint32_t n_docs, uint64_t *sz_off, uint8_t *out, int mode, hipStream_t s);
+// one-pass EncoderV2 (full updates): per-document column streams in scr (11 x (2 len + 64)
+// bytes at scr_off, scanned from need), column sizes (11 u32 per document), document sizes;
+// *over != 0: a column outgrew its stream (run the writing walk instead of k_v2_pack)
+void launch_v2_encode_one(const uint8_t *src, const uint64_t *src_start, const uint64_t *src_len, const uint8_t *status,
+                          uint32_t n_docs, uint64_t *need, uint64_t *scr_off, uint64_t *scan_tmp, uint8_t *scr,
+                          uint32_t *colsz, uint64_t *sz, uint32_t *over, hipStream_t s);
+void launch_v2_pack(const uint64_t *src_len, const uint8_t *status, uint32_t n_docs, const uint64_t *scr_off,
+                    const uint8_t *scr, const uint32_t *colsz, const uint64_t *out_off, uint8_t *out, hipStream_t s);
 void launch_sync_parse(const uint8_t *msg, const uint64_t *msg_off, uint32_t n, uint64_t *sv_off, uint64_t *sv_end,
                        uint8_t *status, hipStream_t s);
 struct PlanCaps {

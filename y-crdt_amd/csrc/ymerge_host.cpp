@@ -91,6 +91,8 @@ struct ymerge_ctx {
   // lib0 v2: v1x arena + offsets + per-update status, v2 output arena + sizes + offsets,
   // state-vector rest offsets + pre-status
   DevBuf v2x, v2x_sz, v2x_off, v2_ust, v2_out, v2_osz, v2_ooff, v2_svoff, v2_svend, v2_pre;
+  DevBuf v2_scr, v2_colsz, v2_over; // one-pass EncoderV2: column streams, sizes, overflow flag
+  bool v2_onepass = true;           // env YMERGE_V2_ONEPASS=0: counting walk + writing walk
   bool want_stamps = false;
   uint64_t *h_pinned = nullptr;
   // k_lean's result words (hand-overs, output bytes) written by k_lean_fin into host-mapped
@@ -160,6 +162,7 @@ static bool ctx_init(ymerge_ctx *c, int device) {
   if (const char *v = getenv("YMERGE_GIANT_LANE")) c->giant_lane = atoi(v) != 0;
   if (const char *v = getenv("YMERGE_LEAN_ORDER")) c->lean_order = atoi(v);
   if (const char *v = getenv("YMERGE_LEAN_SPIN")) c->lean_spin = atoi(v) != 0;
+  if (const char *v = getenv("YMERGE_V2_ONEPASS")) c->v2_onepass = atoi(v) != 0;
   if (const char *v = getenv("YMERGE_GIANT_GRAPH")) c->giant_graph = atoi(v) != 0;
   if (const char *v = getenv("YMERGE_PLANNER"))
     c->planner = strcmp(v, "ring") == 0 ? 1u : strcmp(v, "wave") == 0 ? 2u : 0u;
@@ -198,7 +201,8 @@ extern "C" void ymerge_ctx_destroy(ymerge_ctx *c) {
                     &c->out_start, &c->out_len, &c->pack_off, &c->counts, &c->need, &c->scr_off, &c->scratch,
                     &c->sizes, &c->spill_off, &c->scan_tmp, &c->arena, &c->packed, &c->counter, &c->stamps,
                     &c->plan_small, &c->plan_big, &c->big_scratch, &c->lean_scr, &c->lean_tot, &c->cscr, &c->gs_list, &c->gs1, &c->gs2, &c->big_list, &c->huge, &c->lp, &c->ls_list, &c->ls_scr, &c->ls_done, &c->ls_ovf, &c->lean_ord, &c->lean_dbg, &c->plan_wlist, &c->v2x, &c->v2x_sz, &c->v2x_off, &c->v2_ust,
-                    &c->v2_out, &c->v2_osz, &c->v2_ooff, &c->v2_svoff, &c->v2_svend, &c->v2_pre})
+                    &c->v2_out, &c->v2_osz, &c->v2_ooff, &c->v2_svoff, &c->v2_svend, &c->v2_pre, &c->v2_scr,
+                    &c->v2_colsz, &c->v2_over})
     b->release();
   if (c->h_pinned) hipHostFree(c->h_pinned);
   if (c->h_sig) hipHostFree(c->h_sig);
@@ -1283,14 +1287,36 @@ static int v2_encode(ymerge_ctx *c, ymerge_device_result *res, uint32_t n, int m
   if (!c->v2_osz.ensure(nn * 8) || !c->v2_ooff.ensure(nn * 8) || !c->pack_off.ensure(nn * 8) ||
       !c->scan_tmp.ensure(ym::scan_tmp_elems(n) * 8 + 64))
     return DEV_FAIL();
-  ym::launch_v2_encode(false, res->d_out, res->d_out_start, res->d_out_len, res->d_status, n,
-                       c->v2_osz.as<uint64_t>(), nullptr, mode, c->s);
+  // full updates: one walk into per-document column streams, then k_v2_pack (state vectors:
+  // the two walks, which only copy)
+  const uint64_t scr_bytes = 2 * 11 * res->out_bytes + 64ull * 11 * n + 64;
+  const bool one = mode == 0 && c->v2_onepass && c->need.ensure(nn * 8) && c->scr_off.ensure(nn * 8) &&
+                   c->v2_colsz.ensure(nn * 11 * 4) && c->v2_over.ensure(64) && c->v2_scr.ensure(scr_bytes);
+  (void)hipGetLastError(); // (a failed optional allocation: the two walks)
+  uint64_t total = 0, over = 0;
+  if (one) {
+    hipMemsetAsync(c->v2_over.p, 0, 4, c->s);
+    ym::launch_v2_encode_one(res->d_out, res->d_out_start, res->d_out_len, res->d_status, n, c->need.as<uint64_t>(),
+                             c->scr_off.as<uint64_t>(), c->scan_tmp.as<uint64_t>(), c->v2_scr.as<uint8_t>(),
+                             c->v2_colsz.as<uint32_t>(), c->v2_osz.as<uint64_t>(), c->v2_over.as<uint32_t>(), c->s);
+  } else {
+    ym::launch_v2_encode(false, res->d_out, res->d_out_start, res->d_out_len, res->d_status, n,
+                         c->v2_osz.as<uint64_t>(), nullptr, mode, c->s);
+  }
   ym::launch_scan_u64(c->v2_osz.as<uint64_t>(), c->v2_ooff.as<uint64_t>(), n, c->scan_tmp.as<uint64_t>(), c->s);
-  uint64_t total = 0;
-  if (!read_words(c, c->v2_ooff.as<uint64_t>() + n, 8, &total)) return DEV_FAIL();
+  if (hipMemcpyAsync(c->h_pinned, c->v2_ooff.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, c->s) != hipSuccess ||
+      (one && hipMemcpyAsync(c->h_pinned + 1, c->v2_over.p, 4, hipMemcpyDeviceToHost, c->s) != hipSuccess) ||
+      hipStreamSynchronize(c->s) != hipSuccess)
+    return DEV_FAIL();
+  total = c->h_pinned[0];
+  over = one ? (c->h_pinned[1] & 0xFFFFFFFFu) : 1;
   if (!c->v2_out.ensure(total + 64)) return DEV_FAIL();
-  ym::launch_v2_encode(true, res->d_out, res->d_out_start, res->d_out_len, res->d_status, n,
-                       c->v2_ooff.as<uint64_t>(), c->v2_out.as<uint8_t>(), mode, c->s);
+  if (one && !over)
+    ym::launch_v2_pack(res->d_out_len, res->d_status, n, c->scr_off.as<uint64_t>(), c->v2_scr.as<uint8_t>(),
+                       c->v2_colsz.as<uint32_t>(), c->v2_ooff.as<uint64_t>(), c->v2_out.as<uint8_t>(), c->s);
+  else
+    ym::launch_v2_encode(true, res->d_out, res->d_out_start, res->d_out_len, res->d_status, n,
+                         c->v2_ooff.as<uint64_t>(), c->v2_out.as<uint8_t>(), mode, c->s);
   // packed offsets of the result (pack_to_host copies the arena in their order)
   c->pack_stale = false;
   if (hipMemcpyAsync(c->pack_off.p, c->v2_ooff.p, nn * 8, hipMemcpyDeviceToDevice, c->s) != hipSuccess)

@@ -856,7 +856,127 @@ __global__ void __launch_bounds__(64) k_v2_encode(const uint8_t *src, const uint
   v1x_to_v2(p, n, ew);
 }
 
+// ------------------------------------------------------------------ one-pass encode
+// The counting walk and the writing walk above are the same lane-serial walk twice (the
+// walk is the whole cost).  One pass instead: each column is written into its own scratch
+// stream of V2_CAP(len) bytes (bytes past it are counted, not written), the sizes and the
+// document's total come out of the same walk, and k_v2_pack lays the columns out behind the
+// scanned offsets (a wave per document, coalesced copies).  A document whose column outgrew
+// its stream sets `over`; the host then runs the writing walk for the batch instead.
+struct V2CapW {
+  uint8_t *p;
+  uint64_t n, cap;
+  __device__ __forceinline__ void u8(uint8_t b) {
+    if (n < cap) p[n] = b;
+    n++;
+  }
+  __device__ __forceinline__ void bytes(const uint8_t *src, uint32_t k) {
+    const uint64_t lim = n >= cap ? 0 : (n + k <= cap ? k : cap - n);
+    uint8_t *d = p + n;
+    uint32_t i = 0;
+    for (; i + 16 <= lim; i += 16) {
+      uint8_t t[16];
+#pragma unroll
+      for (uint32_t j = 0; j < 16; j++) t[j] = src[i + j];
+#pragma unroll
+      for (uint32_t j = 0; j < 16; j++) d[i + j] = t[j];
+    }
+    for (; i < lim; i++) d[i] = src[i];
+    n += k;
+  }
+};
+__host__ __device__ inline uint64_t v2_cap(uint64_t len) { return 2 * len + 64; }
+__global__ void k_v2_need(const uint64_t *src_len, const uint8_t *status, uint32_t n, uint64_t *need) {
+  const uint32_t d = blockIdx.x * 256 + threadIdx.x;
+  if (d < n) need[d] = status[d] ? 0 : S_N * v2_cap(src_len[d]);
+}
+__global__ void __launch_bounds__(64) k_v2_encode_one(const uint8_t *src, const uint64_t *src_start,
+                                                      const uint64_t *src_len, const uint8_t *status, uint32_t n_docs,
+                                                      const uint64_t *scr_off, uint8_t *scr, uint32_t *colsz,
+                                                      uint64_t *sz, uint32_t *over) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= n_docs) return;
+  if (status[d]) {
+    sz[d] = 0;
+    return;
+  }
+  const uint8_t *p = src + src_start[d];
+  const uint32_t n = (uint32_t)src_len[d];
+  const uint64_t cap = v2_cap(n);
+  uint8_t *base = scr + scr_off[d];
+  V2Enc<V2CapW> e;
+#pragma unroll
+  for (int k = 0; k < S_N; k++) e.s[k] = V2CapW{base + (uint64_t)k * cap, 0, cap};
+  v1x_to_v2(p, n, e);
+  uint64_t t = 1;
+  bool ov = false;
+#pragma unroll
+  for (int k = 0; k < S_N; k++) {
+    colsz[(size_t)S_N * d + k] = (uint32_t)e.s[k].n;
+    ov = ov || e.s[k].n > cap;
+    if (k == S_SBUF || k == S_SLEN || k == S_REST) continue;
+    t += varlen(e.s[k].n) + e.s[k].n;
+  }
+  const uint64_t sc = varlen(e.s[S_SBUF].n) + e.s[S_SBUF].n + e.s[S_SLEN].n;
+  sz[d] = t + varlen(sc) + sc + e.s[S_REST].n;
+  if (ov) atomicOr(over, 1u);
+}
+// lays one document's columns out in EncoderV2::to_vec order (k_v2_encode<true>'s layout)
+__global__ void __launch_bounds__(64) k_v2_pack(const uint64_t *src_len, const uint8_t *status, uint32_t n_docs,
+                                                const uint64_t *scr_off, const uint8_t *scr, const uint32_t *colsz,
+                                                const uint64_t *out_off, uint8_t *out) {
+  const uint32_t d = blockIdx.x, t = threadIdx.x;
+  if (d >= n_docs || status[d]) return;
+  const uint64_t cap = v2_cap(src_len[d]);
+  const uint8_t *base = scr + scr_off[d];
+  uint8_t *o = out + out_off[d];
+  const uint32_t *cz = colsz + (size_t)S_N * d;
+  uint64_t at = 1;
+  if (t == 0) o[0] = 0; // feature flag
+  auto copy = [&](int k) {
+    const uint8_t *s = base + (uint64_t)k * cap;
+    for (uint32_t q = t; q < cz[k]; q += 64) o[at + q] = s[q];
+    at += cz[k];
+  };
+  for (int k = 0; k < S_N; k++) {
+    if (k == S_SLEN) continue;
+    if (k == S_SBUF) {
+      const uint64_t sc = varlen(cz[S_SBUF]) + cz[S_SBUF] + cz[S_SLEN];
+      Writer hw{o + at, 0};
+      if (t == 0) {
+        w_var(hw, sc);
+        w_var(hw, (uint64_t)cz[S_SBUF]);
+      }
+      at += varlen(sc) + varlen(cz[S_SBUF]);
+      copy(S_SBUF);
+      copy(S_SLEN);
+      continue;
+    }
+    if (k != S_REST) {
+      Writer hw{o + at, 0};
+      if (t == 0) w_var(hw, (uint64_t)cz[k]);
+      at += varlen(cz[k]);
+    }
+    copy(k);
+  }
+}
+
 // ------------------------------------------------------------------ launchers
+void launch_v2_encode_one(const uint8_t *src, const uint64_t *src_start, const uint64_t *src_len, const uint8_t *status,
+                          uint32_t n_docs, uint64_t *need, uint64_t *scr_off, uint64_t *scan_tmp, uint8_t *scr,
+                          uint32_t *colsz, uint64_t *sz, uint32_t *over, hipStream_t s) {
+  if (!n_docs) return;
+  hipLaunchKernelGGL(k_v2_need, dim3((n_docs + 255) / 256), dim3(256), 0, s, src_len, status, n_docs, need);
+  launch_scan_u64(need, scr_off, n_docs, scan_tmp, s);
+  hipLaunchKernelGGL(k_v2_encode_one, dim3((n_docs + 63) / 64), dim3(64), 0, s, src, src_start, src_len, status, n_docs,
+                     scr_off, scr, colsz, sz, over);
+}
+void launch_v2_pack(const uint64_t *src_len, const uint8_t *status, uint32_t n_docs, const uint64_t *scr_off,
+                    const uint8_t *scr, const uint32_t *colsz, const uint64_t *out_off, uint8_t *out, hipStream_t s) {
+  if (n_docs)
+    hipLaunchKernelGGL(k_v2_pack, dim3(n_docs), dim3(64), 0, s, src_len, status, n_docs, scr_off, scr, colsz, out_off,
+                       out);
+}
 void launch_v2_decode(bool write, const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_upd, uint64_t *sz_off,
                       uint8_t *out, uint8_t *ust, hipStream_t s) {
   if (!n_upd) return;
