@@ -269,6 +269,12 @@ void launch_v2_encode(bool write, const uint8_t *src, const uint64_t *src_start,
 void launch_v2_encode_one(const uint8_t *src, const uint64_t *src_start, const uint64_t *src_len, const uint8_t *status,
                           uint32_t n_docs, uint64_t *need, uint64_t *scr_off, uint64_t *scan_tmp, uint8_t *scr,
                           uint32_t *colsz, uint64_t *sz, uint32_t *over, hipStream_t s);
+// one-pass DecoderV2: v1x bytes of update u into scr at 4 (upd_off[u] - upd_off[0]) + 64 u
+// (4 len + 64 bytes), sizes; *over != 0: a slot overflowed (run the two walks instead)
+void launch_v2_decode_one(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_upd, uint8_t *scr, uint64_t *sz,
+                          uint8_t *ust, uint32_t *over, hipStream_t s);
+void launch_v2_xpack(const uint64_t *upd_off, uint64_t n_upd, const uint8_t *scr, const uint64_t *off, uint8_t *out,
+                     hipStream_t s);
 void launch_v2_pack(const uint64_t *src_len, const uint8_t *status, uint32_t n_docs, const uint64_t *scr_off,
                     const uint8_t *scr, const uint32_t *colsz, const uint64_t *out_off, uint8_t *out, hipStream_t s);
 void launch_sync_parse(const uint8_t *msg, const uint64_t *msg_off, uint32_t n, uint64_t *sv_off, uint64_t *sv_end,

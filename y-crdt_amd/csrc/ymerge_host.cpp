@@ -1265,12 +1265,33 @@ extern "C" int ycompact_updates_v1_batch_device(ymerge_ctx *c, const uint8_t *d_
 // ---------------------------------------------------------------- lib0 v2 (yv2.hip)
 // v2 updates -> v1x arena (c->v2x, offsets c->v2x_off[n_upd + 1], status c->v2_ust)
 static int v2_transcode(ymerge_ctx *c, const uint8_t *d_bytes, const uint64_t *d_upd_off, uint64_t n_upd,
-                        uint64_t *total) {
+                        uint64_t *total, uint64_t n_bytes = 0) {
   if (n_upd > 0xFFFFFFFFull) return YMERGE_ERR_OTHER;
   const size_t nn = (size_t)n_upd + 1;
   if (!c->v2x_sz.ensure(nn * 8) || !c->v2x_off.ensure(nn * 8) || !c->v2_ust.ensure(nn) ||
       !c->scan_tmp.ensure(ym::scan_tmp_elems((uint32_t)n_upd) * 8 + 64))
     return DEV_FAIL();
+  // one walk into per-update scratch slots, then a packing copy (n_bytes known: the merge
+  // entry; an overflowing slot falls back to the two walks below)
+  if (n_bytes && c->v2_onepass && c->v2_over.ensure(64) && c->v2_scr.ensure(4 * n_bytes + 64 * nn + 64)) {
+    hipMemsetAsync(c->v2_over.p, 0, 4, c->s);
+    ym::launch_v2_decode_one(d_bytes, d_upd_off, n_upd, c->v2_scr.as<uint8_t>(), c->v2x_sz.as<uint64_t>(),
+                             c->v2_ust.as<uint8_t>(), c->v2_over.as<uint32_t>(), c->s);
+    ym::launch_scan_u64(c->v2x_sz.as<uint64_t>(), c->v2x_off.as<uint64_t>(), (uint32_t)n_upd,
+                        c->scan_tmp.as<uint64_t>(), c->s);
+    if (hipMemcpyAsync(c->h_pinned, c->v2x_off.as<uint64_t>() + n_upd, 8, hipMemcpyDeviceToHost, c->s) != hipSuccess ||
+        hipMemcpyAsync(c->h_pinned + 1, c->v2_over.p, 4, hipMemcpyDeviceToHost, c->s) != hipSuccess ||
+        hipStreamSynchronize(c->s) != hipSuccess)
+      return DEV_FAIL();
+    if ((c->h_pinned[1] & 0xFFFFFFFFu) == 0) {
+      *total = c->h_pinned[0];
+      if (!c->v2x.ensure(*total + 64)) return DEV_FAIL();
+      ym::launch_v2_xpack(d_upd_off, n_upd, c->v2_scr.as<uint8_t>(), c->v2x_off.as<uint64_t>(), c->v2x.as<uint8_t>(),
+                          c->s);
+      return hipGetLastError() == hipSuccess ? 0 : DEV_FAIL();
+    }
+  }
+  (void)hipGetLastError();
   ym::launch_v2_decode(false, d_bytes, d_upd_off, n_upd, c->v2x_sz.as<uint64_t>(), nullptr, c->v2_ust.as<uint8_t>(),
                        c->s);
   ym::launch_scan_u64(c->v2x_sz.as<uint64_t>(), c->v2x_off.as<uint64_t>(), (uint32_t)n_upd,
@@ -1335,7 +1356,7 @@ static int merge_v2_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_byt
   if (n_docs > 0xFFFFFFFFull) return YMERGE_ERR_OTHER;
   uint64_t xbytes = 0;
   hipEventRecord(c->v2ev[0], c->s);
-  int st = v2_transcode(c, d_bytes, d_upd_off, n_updates, &xbytes);
+  int st = v2_transcode(c, d_bytes, d_upd_off, n_updates, &xbytes, n_bytes);
   if (st) return st;
   hipEventRecord(c->v2ev[1], c->s);
   st = merge_device(c, c->v2x.as<uint8_t>(), xbytes, c->v2x_off.as<uint64_t>(), n_updates, d_doc_upd, n_docs, res);

@@ -921,6 +921,45 @@ __global__ void __launch_bounds__(64) k_v2_encode_one(const uint8_t *src, const 
   sz[d] = t + varlen(sc) + sc + e.s[S_REST].n;
   if (ov) atomicOr(over, 1u);
 }
+// the decoder in one walk too: each update's v1x bytes into a scratch slot of 4 len + 64
+// bytes at 4 (upd_off[u] - upd_off[0]) + 64 u, sizes, then k_v2_xpack packs them
+__global__ void __launch_bounds__(64) k_v2_decode_one(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_upd,
+                                                      uint8_t *scr, uint64_t *sz, uint8_t *ust, uint32_t *over) {
+  const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= n_upd) return;
+  const uint8_t *p = bytes + upd_off[u];
+  const uint32_t n = (uint32_t)(upd_off[u + 1] - upd_off[u]);
+  V2CapW w{scr + 4 * (upd_off[u] - upd_off[0]) + 64 * u, 0, 4ull * n + 64};
+  const int e = v2_to_v1(p, n, w);
+  ust[u] = (uint8_t)e;
+  if (e) {
+    w.p[0] = 0; // an empty update [0, 0] for a failed one (the document's status reports it)
+    w.p[1] = 0;
+    sz[u] = 2;
+  } else {
+    sz[u] = w.n;
+    if (w.n > w.cap) atomicOr(over, 1u);
+  }
+}
+__global__ void __launch_bounds__(256) k_v2_xpack(const uint64_t *upd_off, uint64_t n_upd, const uint8_t *scr,
+                                                  const uint64_t *off, uint8_t *out) {
+  const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= n_upd) return;
+  Writer w{out + off[u], 0};
+  w.bytes(scr + 4 * (upd_off[u] - upd_off[0]) + 64 * u, (uint32_t)(off[u + 1] - off[u]));
+}
+void launch_v2_decode_one(const uint8_t *bytes, const uint64_t *upd_off, uint64_t n_upd, uint8_t *scr, uint64_t *sz,
+                          uint8_t *ust, uint32_t *over, hipStream_t s) {
+  if (n_upd)
+    hipLaunchKernelGGL(k_v2_decode_one, dim3((unsigned)((n_upd + 63) / 64)), dim3(64), 0, s, bytes, upd_off, n_upd, scr,
+                       sz, ust, over);
+}
+void launch_v2_xpack(const uint64_t *upd_off, uint64_t n_upd, const uint8_t *scr, const uint64_t *off, uint8_t *out,
+                     hipStream_t s) {
+  if (n_upd)
+    hipLaunchKernelGGL(k_v2_xpack, dim3((unsigned)((n_upd + 255) / 256)), dim3(256), 0, s, upd_off, n_upd, scr, off,
+                       out);
+}
 // lays one document's columns out in EncoderV2::to_vec order (k_v2_encode<true>'s layout)
 __global__ void __launch_bounds__(64) k_v2_pack(const uint64_t *src_len, const uint8_t *status, uint32_t n_docs,
                                                 const uint64_t *scr_off, const uint8_t *scr, const uint32_t *colsz,
