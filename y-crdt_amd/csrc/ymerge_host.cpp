@@ -16,6 +16,7 @@
 #include <cstring>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <map>
 #include <mutex>
 #include <thread>
@@ -247,10 +248,61 @@ static unsigned stage_threads() { // env YMERGE_STAGE_THREADS
   }();
   return t;
 }
+// Persistent copy threads: a 265 MB host entry is ~10 large copies, and starting seven
+// threads per copy cost more than the copies' tail (worker i takes slice i, the caller
+// slice 0; one user at a time, a second concurrent user starts its own threads)
+struct CopyPool {
+  std::mutex use, m;
+  std::condition_variable cv, done;
+  uint64_t gen = 0;
+  unsigned pending = 0, t = 0;
+  uint8_t *dst = nullptr;
+  const uint8_t *src = nullptr;
+  size_t n = 0, per = 0;
+  explicit CopyPool(unsigned threads) : t(threads) {
+    for (unsigned i = 1; i < t; i++) std::thread([this, i] { worker(i); }).detach();
+  }
+  void worker(unsigned i) {
+    uint64_t seen = 0;
+    for (;;) {
+      std::unique_lock<std::mutex> lk(m);
+      cv.wait(lk, [&] { return gen != seen; });
+      seen = gen;
+      uint8_t *d = dst;
+      const uint8_t *s = src;
+      const size_t a = i * per, len = a < n ? std::min(per, n - a) : 0;
+      lk.unlock();
+      if (len) memcpy(d + a, s + a, len);
+      lk.lock();
+      if (--pending == 0) done.notify_one();
+    }
+  }
+  void copy(void *d, const void *s, size_t bytes) {
+    {
+      std::lock_guard<std::mutex> lk(m);
+      dst = (uint8_t *)d;
+      src = (const uint8_t *)s;
+      n = bytes;
+      per = (bytes + t - 1) / t;
+      pending = t - 1;
+      gen++;
+    }
+    cv.notify_all();
+    memcpy(d, s, std::min(per, bytes));
+    std::unique_lock<std::mutex> lk(m);
+    done.wait(lk, [&] { return pending == 0; });
+  }
+};
 static void par_memcpy(void *dst, const void *src, size_t n) {
   const unsigned t = n >= (4u << 20) ? stage_threads() : 1;
   if (t <= 1) {
     memcpy(dst, src, n);
+    return;
+  }
+  static CopyPool *pool = new CopyPool(t); // (never destroyed: detached workers outlive it otherwise)
+  if (pool->use.try_lock()) {
+    pool->copy(dst, src, n);
+    pool->use.unlock();
     return;
   }
   std::vector<std::thread> th;
