@@ -778,6 +778,9 @@ static int merge_device(ymerge_ctx *c, const uint8_t *d_bytes, uint64_t n_bytes,
       hipMemcpyAsync((uint8_t *)(c->h_pinned + 512) - 88, c->counter.as<uint8_t>() + 40, 88 + 64 * 64,
                      hipMemcpyDeviceToHost, c->s);
       if (hipStreamSynchronize(c->s) != hipSuccess) return DEV_FAIL();
+      uint32_t sh = 0; // the hand-over shards: word 2 of each 64-byte partial
+      for (int q = 0; q < 64; q++) sh += (uint32_t)c->h_pinned[512 + 8 * q + 1];
+      c->h_pinned[501] = (uint32_t)c->h_pinned[501] + sh;
     }
     n_rej = (uint32_t)(c->h_pinned[501] & 0xFFFFFFFFu);
     b.only_path3 = 1;

@@ -414,11 +414,15 @@ __device__ __forceinline__ void lean_doc(const BatchIn &b, const FastOut &o, Lea
   uint8_t *out = o.out + slot;
   // hand-over; why: 0 size/empty, 1 stage, 2 walk, 3 clients, 4 arena, 5 contiguity, 6 DS window
   // (npath[7 + why]: diagnostics, env YMERGE_LEAN_DEBUG)
+  // The count goes to this document's shard (word 2 of its 64-byte output-byte partial,
+  // summed by k_lean_fin / the host): one counter for every handing-over wave serialised the
+  // corpus's 78 k hand-overs on one address (k_lean 1.53 ms, §5.10).
   auto reject = [&](uint32_t why) {
     if (lane == 0) {
       o.path[d] = 3;
-      atomicAdd(&o.npath[6], 1u);
-      atomicAdd(&o.npath[7 + (why < 7 ? why : 0)], 1u);
+      if (o.lean_total) atomicAdd((uint32_t *)(o.lean_total + 8 * (d & 63)) + 2, 1u);
+      else atomicAdd(&o.npath[6], 1u);
+      if (o.dbg) atomicAdd(&o.npath[7 + (why < 7 ? why : 0)], 1u);
     }
   };
   if (U == 0 || (!BIG && (B1 - B0 >= 65536 || U > LN_AW))) {
@@ -1087,8 +1091,12 @@ void launch_lean_order(const uint64_t *doc_upd, uint32_t n_docs, uint32_t *ctr, 
 __global__ void __launch_bounds__(64) k_lean_fin(uint32_t *counter, uint32_t *sig, uint32_t seq) {
   const uint32_t l = threadIdx.x;
   unsigned long long v = ((const unsigned long long *)(counter + 32))[8 * l];
-  const uint32_t nrej = counter[10];
-  for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o, 64);
+  uint32_t nrej = counter[32 + 16 * l + 2]; // the hand-over shards (k_lean's reject)
+  for (int o = 32; o; o >>= 1) {
+    v += __shfl_xor(v, o, 64);
+    nrej += __shfl_xor(nrej, o, 64);
+  }
+  nrej += counter[10];
   __syncthreads(); // every read above precedes the zeroing
   if (nrej == 0)
     for (uint32_t q = l; q < 32 + 64 * 16; q += 64) counter[q] = 0;
