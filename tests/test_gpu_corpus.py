@@ -62,6 +62,7 @@ def test_small_dataset_paths(engine, oracle, dataset):
     {"YMERGE_LP_MID": "16"},                                   # nearly every rich update on the parallel parse
     {"YMERGE_LONG_PARSE": "0"},                                # no parallel parse: the lockstep walker
     {"YMERGE_TINY": "4"},                                      # tiny documents on the exact engine's lanes
+    {"YMERGE_LEAN_SPIN": "0"},  # k_lean's sharded hand-over count read by a copy, not the mapped signal
 ])
 def test_small_dataset_decode_routes(oracle, dataset, env):
     """The corpus through every decode route the knobs select: the same bytes each time."""
